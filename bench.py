@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Throughput bench of the batched Avalanche vote-record update path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3|c5]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+One *step* = one synchronous round of go-avalanche's poll loop for every
+simulated node: k peers sampled per node, k Responses
+registered, VoteRecord updates (vote.go:54-91) and StatusUpdate emission
+(processor.go:111). Inputs (records, preferences) are resident in HBM before
+the timed region starts.
+
+metric : vote-record updates/s = regsiterVote applications on live records
+         (vote.go:54) per second, whole job (all ranks). triples/s (node, target,
+         round) = updates/s / k is reported beside it.
+workload (N=1 default) : C4 of BASELINE.json — 1M nodes x 1000 targets, k=8,
+         IsAccepted() ~ Bernoulli(0.8), honest, synthetic (seeded), rounds
+         W..W+K-1 (< 17: every record stays live). With N GPUs the same
+         network is split by target blocks (no per-round exchange; strong
+         scaling) or, with --shard nodes, by nodes with an RCCL all-gather of
+         the published preferences every round.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "go-avalanche_amd", "python"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (device plumbing + torch.distributed only)
+import torch.distributed as dist  # noqa: E402
+
+import avhip  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+P80 = int(0.8 * 2**32)
+BYZ20 = int(0.2 * 2**32)
+
+WORKLOADS = {
+    # name: (nodes, targets, k, init_mode, init_param, byz_threshold, replay, description)
+    "c4": (1_000_000, 1000, 8, avhip.INIT_BERNOULLI, P80, 0, False,
+           "C4: 1M nodes x 1000 targets, k=8, Bernoulli(0.8) initial acceptance, honest, sim mode"),
+    "c2": (1000, 10_000, 8, avhip.INIT_BERNOULLI, 0x80000000, 0, True,
+           "C2: 1k nodes x 10k targets, k=8, replayed vote streams (70/25/5 yes/no/neutral), 4096 poll cap binds"),
+    "c3": (100_000, 2000, 8, avhip.INIT_PAIRS, 0, BYZ20, False,
+           "C3: 100k nodes x 1000 double-spend pairs, k=8, 20% Byzantine flip-flop voters"),
+    "c5": (10_000_000, 256, 8, avhip.INIT_BERNOULLI, P80, 0, False,
+           "C5: 10M nodes x 256 targets, k=8, Bernoulli(0.8), honest"),
+}
+
+BYTES_PER_LANE_PLANES = 25 * 4 * 2  # 25 u32 state planes read + written per 32-record block
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=14)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
+    ap.add_argument("--shard", default="targets", choices=["targets", "nodes"])
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xA7A1A9C4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def shard_targets(m, world, rank):
+    blocks = (m + 31) // 32
+    b0, b1 = rank * blocks // world, (rank + 1) * blocks // world
+    return b0 * 32, min(b1 * 32, m)
+
+
+def cpu_baseline(wl, seed, budget_s):
+    """Oracle ("port": C restatement of the reference semantics) on host cores,
+    on a bounded sample of the same workload: fewer nodes, same targets/k."""
+    from oracle import cabi
+
+    n, m, k, init_mode, init_param, byz, replay, _ = WORKLOADS[wl]
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    ns = min(n, 8000 if wl != "c2" else 200)
+    sim = cabi.Sim(ns, m, k, seed=seed, byz_threshold=byz, init_mode=init_mode, init_param=init_param)
+    applied = 0
+    dt = 0.0
+    rounds = 0
+    while dt < budget_s and rounds < 16:
+        errs = cabi.gen_replay_errs(seed, rounds, 0, ns, m, k) if replay else None  # input, untimed
+        ts = time.perf_counter()
+        _, a = sim.run_round(errs, threads=threads)
+        dt += time.perf_counter() - ts
+        applied += a
+        rounds += 1
+    sim.close()
+    return {"value": applied / dt, "unit": "vote-record updates/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/avalanche_oracle.c Sim, {ns} nodes x {m} targets, k={k}, {rounds} rounds "
+                      f"({applied} regsiterVote applications, {dt:.1f}s, OpenMP over nodes)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[args.workload]
+    if args.shard == "targets" and world > 1 and m > 4096:
+        raise SystemExit("target sharding needs M <= 4096 (poll cap couples targets); use --shard nodes")
+    kw = dict(k=k, seed=args.seed, byz_threshold=byz, device=local_rank)
+    if world > 1 and args.shard == "targets":
+        kw["target_range"] = shard_targets(m, world, rank)
+    elif world > 1:
+        assert n % world == 0, "node sharding needs N % world == 0"
+        kw["node_range"] = (rank * n // world, (rank + 1) * n // world)
+    total_rounds = args.warmup + args.steps
+    est_updates = int(0.25 * n * m) + (1 << 20)
+    eng = avhip.Engine(n, m, log_capacity=min(est_updates, 1 << 29), **kw)
+    eng.init_records(init_mode, init_param)
+    if world > 1 and args.shard == "nodes":
+        obj = [avhip.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        eng.comm_init(world, rank, obj[0])
+    if replay:
+        eng.replay_prepare(total_rounds)
+    run = eng.replay_rounds if replay else eng.run_rounds
+    info = eng.layout_info()
+
+    # ---- warmup (untimed), then drain the StatusUpdate log
+    run(args.warmup)
+    eng.synchronize()
+    eng.fetch_updates(decode=False)
+    applied0 = eng.applied_votes()
+
+    # ---- timed region: K rounds
+    eng.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_timing(False)
+    kern_ms, launches = eng.kernel_stats()
+    applied = eng.applied_votes() - applied0
+    emitted = eng.updates_count()
+
+    stats = torch.tensor([elapsed, float(applied), float(emitted), kern_ms / max(launches, 1),
+                          float(info["lanes"])], dtype=torch.float64, device="cuda")
+    if world > 1:
+        tmax = stats[0].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tot = stats[1:3].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        kavg = stats[3].clone()
+        dist.all_reduce(kavg, op=dist.ReduceOp.MAX)
+        elapsed, applied, emitted, kavg_ms = float(tmax), float(tot[0]), float(tot[1]), float(kavg)
+    else:
+        kavg_ms = float(stats[3])
+    lanes_local = info["lanes"]
+
+    if rank == 0:
+        value = applied / elapsed
+        # algorithmic bytes of one round-kernel launch on one GPU (DESIGN.md "Roofline"):
+        #   per 32-record lane: 25 state planes read+written (200 B), k gathered
+        #   peer-preference words (4k B) or 2k replayed vote planes (8k B), one
+        #   published-preference word (4 B); + 8 B per emitted StatusUpdate.
+        per_lane = BYTES_PER_LANE_PLANES + (8 * k if replay else 4 * k) + 4
+        emitted_per_launch = emitted / max(args.steps, 1) / world
+        alg_bytes = lanes_local * per_lane + emitted_per_launch * 8
+        achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
+        if world == 1 and os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        line = {
+            "metric": "vote-record updates/sec (node·target·round) at 1/2/4/8 GPU; % HBM roofline",
+            "value": value,
+            "unit": "vote-record updates/s (1 update = 1 regsiterVote on a live record; k=8 per node·target·round)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded Philox4x32-10 network; no dataset)",
+            "config": {
+                "workload": desc,
+                "n_nodes": n, "n_targets": m, "k": k,
+                "rounds": f"{args.warmup}..{total_rounds - 1}",
+                "parallelism": f"{args.shard}-sharded x{world}" if world > 1 else "single GPU",
+                "layout": "bit-sliced: 25 u32 planes per 32 records; tile of 64 lanes contiguous",
+                "capped_poll_path": info["capped"],
+            },
+            "triples_per_s": value / k,
+            "updates_emitted": int(emitted),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_round_fast<8,%s>" % ("true" if replay else "false") if not info["capped"] else
+                          "k_round_capped<8,%s>" % ("true" if replay else "false"),
+                "kernel_ms_avg": kavg_ms,
+                "alg_bytes_per_launch": alg_bytes,
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(args.workload, args.seed, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,804 @@
+// libavhip.so — C ABI (include/avhip.h) over the CDNA4 kernels in kernels.hip.
+//
+// The engine owns all device memory: the bit-sliced VoteRecord planes, the two
+// published-preference snapshots, validity / Byzantine bitsets, the sharded
+// StatusUpdate log and the applied-vote counters. Host buffers passed in are
+// only read or written for the duration of the call.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/avhip.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define AV_HIP(call)                                                                                    \
+  do {                                                                                                  \
+    hipError_t _e = (call);                                                                             \
+    if (_e != hipSuccess) return fail(AV_ERR_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(_e), \
+                                      __FILE__, __LINE__);                                              \
+  } while (0)
+
+#define AV_CHECK(cond, code, ...) \
+  do {                            \
+    if (!(cond)) return fail(code, __VA_ARGS__); \
+  } while (0)
+
+template <typename T>
+hipError_t dev_alloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T));
+}
+
+}  // namespace
+
+struct av_engine {
+  av_config cfg{};
+  int64_t N = 0, M = 0, n0 = 0, n1 = 0, t0 = 0, t1 = 0;
+  uint32_t NL = 0, BL = 0, L = 0, Lpad = 0;
+  int k = 0;
+  bool capped = false;
+  hipStream_t stream = nullptr;
+  uint32_t* planes = nullptr;
+  uint32_t* pref[2] = {nullptr, nullptr};
+  int cur = 0;
+  uint32_t* valid = nullptr;
+  uint32_t* byz = nullptr;
+  uint64_t* log = nullptr;
+  uint32_t* log_count = nullptr;
+  uint32_t* log_overflow = nullptr;
+  uint32_t log_cap = 0;
+  unsigned long long* applied = nullptr;
+  int64_t round = 0, log_base = 0;
+  std::vector<uint32_t> valid_host;
+  // replay stream
+  uint32_t* replay = nullptr;
+  int64_t replay_cap_rounds = 0, replay_first = 0, replay_ready = 0;
+  // timing
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  double timed_ms = 0.0;
+  int64_t timed_launches = 0;
+  // RCCL
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0;
+
+  size_t round_replay_words() const { return (size_t)k * 2 * Lpad; }
+};
+
+namespace {
+
+int set_device(av_engine* e) {
+  AV_CHECK(e, AV_ERR_INVALID_ARG, "null engine");
+  AV_HIP(hipSetDevice(e->cfg.device));
+  return AV_OK;
+}
+
+#define AV_ENTER(e)              \
+  do {                           \
+    int _rc = set_device(e);     \
+    if (_rc != AV_OK) return _rc; \
+  } while (0)
+
+bool local_node(const av_engine* e, int64_t node) { return node >= e->n0 && node < e->n1; }
+bool local_target(const av_engine* e, int64_t t) { return t >= e->t0 && t < e->t1; }
+
+// Growable device scratch (drop-in / readback paths only; never inside a round).
+struct Scratch {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~Scratch() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= bytes) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+};
+
+int launch_one_round(av_engine* e, const uint32_t* replay) {
+  AV_CHECK(e->round - e->log_base < 4096, AV_ERR_OVERFLOW,
+           "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
+  AV_CHECK(e->NL == (uint32_t)e->N || e->comm != nullptr || e->N == e->n1 - e->n0, AV_ERR_UNSUPPORTED,
+           "node-sharded engine needs av_comm_init before running rounds");
+  avk::RoundParams p{};
+  p.planes = e->planes;
+  p.pref_in = e->pref[e->cur];
+  p.pref_out = e->pref[e->cur ^ 1];
+  p.valid = e->valid;
+  p.byz = e->byz;
+  p.replay = replay;
+  p.log = e->log;
+  p.log_count = e->log_count;
+  p.log_overflow = e->log_overflow;
+  p.applied = e->applied;
+  p.seed = e->cfg.seed;
+  p.log_cap = e->log_cap;
+  p.n_nodes = (uint32_t)e->N;
+  p.n0 = (uint32_t)e->n0;
+  p.NL = e->NL;
+  p.BL = e->BL;
+  p.L = e->L;
+  p.Lpad = e->Lpad;
+  p.t0 = (uint32_t)e->t0;
+  p.round = (uint32_t)e->round;
+  p.round_rel = (uint32_t)(e->round - e->log_base);
+  p.peer_mode = e->cfg.peer_mode;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (e->timing) {
+    AV_HIP(hipEventCreate(&ev0));
+    AV_HIP(hipEventCreate(&ev1));
+    AV_HIP(hipEventRecord(ev0, e->stream));
+  }
+  AV_HIP(avk::launch_round(p, e->k, replay != nullptr, e->capped, e->stream));
+  if (e->timing) {
+    AV_HIP(hipEventRecord(ev1, e->stream));
+    e->events.emplace_back(ev0, ev1);
+  }
+  if (e->comm) {
+    const size_t count = (size_t)e->NL * e->BL;
+    uint32_t* out = e->pref[e->cur ^ 1];
+    ncclResult_t r = ncclAllGather(out + (size_t)e->n0 * e->BL, out, count, ncclUint32, e->comm, e->stream);
+    AV_CHECK(r == ncclSuccess, AV_ERR_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
+  }
+  e->cur ^= 1;
+  e->round++;
+  return AV_OK;
+}
+
+int refresh_pref(av_engine* e) {
+  AV_HIP(avk::launch_refresh_pref(e->planes, e->pref[e->cur], e->byz, (uint32_t)e->n0, e->NL, e->BL,
+                                  (uint32_t)e->round, e->stream));
+  return AV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int av_abi_version(void) { return AVHIP_ABI_VERSION; }
+
+void av_config_init(av_config* c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof(*c));
+  c->k = 8;
+  c->seed = 0xA7A1A9C4ull;
+}
+
+const char* av_strerror(int code) {
+  switch (code) {
+    case AV_OK: return "ok";
+    case AV_ERR_INVALID_ARG: return "invalid argument";
+    case AV_ERR_HIP: return "HIP runtime error";
+    case AV_ERR_OOM: return "out of device memory";
+    case AV_ERR_NOT_FOUND: return "VoteRecord not found";
+    case AV_ERR_OVERFLOW: return "buffer overflow";
+    case AV_ERR_UNSUPPORTED: return "unsupported configuration";
+    case AV_ERR_RCCL: return "RCCL error";
+    default: return "unknown error";
+  }
+}
+
+const char* av_last_error(void) { return g_last_error.c_str(); }
+
+int av_destroy(av_engine* e) {
+  if (!e) return AV_OK;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (auto& ev : e->events) {
+    (void)hipEventDestroy(ev.first);
+    (void)hipEventDestroy(ev.second);
+  }
+  if (e->comm) (void)ncclCommDestroy(e->comm);
+  void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->valid, e->byz, e->log, e->log_count, e->log_overflow,
+                  e->applied, e->replay};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return AV_OK;
+}
+
+int av_create(const av_config* cfg, av_engine** out) {
+  AV_CHECK(cfg && out, AV_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  const av_config& c = *cfg;
+  AV_CHECK(c.n_nodes >= 2 && c.n_nodes < (1ll << 24), AV_ERR_INVALID_ARG, "n_nodes must be in [2, 2^24)");
+  AV_CHECK(c.n_targets >= 1 && c.n_targets < (1ll << 22), AV_ERR_INVALID_ARG, "n_targets must be in [1, 2^22)");
+  AV_CHECK(c.k >= 1 && c.k <= avk::kMaxK, AV_ERR_INVALID_ARG, "k must be in [1, 16]");
+  AV_CHECK(c.peer_mode == AV_PEERS_RANDOM || c.peer_mode == AV_PEERS_ROUND_ROBIN, AV_ERR_INVALID_ARG,
+           "bad peer_mode");
+  auto* e = new av_engine();
+  e->cfg = c;
+  e->N = c.n_nodes;
+  e->M = c.n_targets;
+  e->n0 = c.node_begin;
+  e->n1 = c.node_end;
+  if (e->n0 == 0 && e->n1 == 0) e->n1 = e->N;
+  e->t0 = c.target_begin;
+  e->t1 = c.target_end;
+  if (e->t0 == 0 && e->t1 == 0) e->t1 = e->M;
+  e->k = c.k;
+  auto bad = [&](const char* msg) {
+    delete e;
+    return fail(AV_ERR_INVALID_ARG, "%s", msg);
+  };
+  if (!(e->n0 >= 0 && e->n0 < e->n1 && e->n1 <= e->N)) return bad("bad node shard");
+  if (!(e->t0 >= 0 && e->t0 < e->t1 && e->t1 <= e->M && e->t0 % 32 == 0)) return bad("bad target shard");
+  e->capped = e->M > (int64_t)avk::kMaxPoll;
+  if (e->capped && (e->t0 != 0 || e->t1 != e->M)) {
+    delete e;
+    return fail(AV_ERR_UNSUPPORTED,
+                "target sharding needs M <= 4096: the 4096 poll cap couples targets (processor.go:165-167)");
+  }
+  e->NL = (uint32_t)(e->n1 - e->n0);
+  e->BL = (uint32_t)((e->t1 - e->t0 + 31) / 32);
+  if (e->capped && e->BL > 1024) return bad("capped path supports M <= 32768");
+  const uint64_t L = (uint64_t)e->NL * e->BL;
+  if (L >= (1ull << 31)) return bad("too many lanes for one engine: shard further");
+  e->L = (uint32_t)L;
+  e->Lpad = (uint32_t)((L + 63) / 64 * 64);
+
+  int rc = AV_OK;
+  auto hip_fail = [&](hipError_t he, const char* what) {
+    av_destroy(e);
+    return fail(he == hipErrorOutOfMemory ? AV_ERR_OOM : AV_ERR_HIP, "%s: %s", what, hipGetErrorString(he));
+  };
+  hipError_t he = hipSetDevice(c.device);
+  if (he != hipSuccess) return hip_fail(he, "hipSetDevice");
+  if ((he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess)
+    return hip_fail(he, "hipStreamCreate");
+  const size_t plane_words = (size_t)(e->Lpad / 64) * avk::kPlanes * 64;
+  const size_t pref_words = (size_t)e->N * e->BL;
+  int64_t cap = c.update_log_capacity;
+  if (cap <= 0) cap = std::min<int64_t>(std::max<int64_t>((int64_t)L * 8, 1 << 20), 1ll << 28);
+  e->log_cap = (uint32_t)std::max<int64_t>((cap + avk::kLogShards - 1) / avk::kLogShards, 64);
+  if ((he = dev_alloc(&e->planes, plane_words)) != hipSuccess) return hip_fail(he, "alloc planes");
+  if ((he = dev_alloc(&e->pref[0], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
+  if ((he = dev_alloc(&e->pref[1], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
+  if ((he = dev_alloc(&e->valid, e->BL)) != hipSuccess) return hip_fail(he, "alloc valid");
+  if ((he = dev_alloc(&e->byz, (e->N + 31) / 32)) != hipSuccess) return hip_fail(he, "alloc byz");
+  if ((he = dev_alloc(&e->log, (size_t)e->log_cap * avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  if ((he = dev_alloc(&e->log_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  if ((he = dev_alloc(&e->log_overflow, 1)) != hipSuccess) return hip_fail(he, "alloc log");
+  if ((he = dev_alloc(&e->applied, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
+  (void)hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream);
+  (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
+  (void)hipMemsetAsync(e->applied, 0, avk::kLogShards * 8, e->stream);
+  (void)hipMemsetAsync(e->pref[1], 0, pref_words * 4, e->stream);
+  // every real target starts valid
+  e->valid_host.assign(e->BL, 0u);
+  for (uint32_t b = 0; b < e->BL; ++b) {
+    const int64_t tb = e->t0 + 32ll * b;
+    const int64_t r = std::min<int64_t>(e->t1 - tb, 32);
+    e->valid_host[b] = r >= 32 ? ~0u : ((1u << r) - 1u);
+  }
+  if ((he = hipMemcpyAsync(e->valid, e->valid_host.data(), e->BL * 4, hipMemcpyHostToDevice, e->stream)) !=
+      hipSuccess)
+    return hip_fail(he, "upload valid");
+  if ((he = avk::launch_byz(e->byz, (uint32_t)e->N, c.seed, c.byz_threshold, e->stream)) != hipSuccess)
+    return hip_fail(he, "byz kernel");
+  *out = e;
+  rc = av_init_records(e, AV_INIT_NONE, 0);
+  if (rc != AV_OK) {
+    av_destroy(e);
+    *out = nullptr;
+    return rc;
+  }
+  return AV_OK;
+}
+
+int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
+  AV_ENTER(e);
+  AV_CHECK(init_mode >= AV_INIT_NONE && init_mode <= AV_INIT_PAIRS, AV_ERR_INVALID_ARG, "bad init_mode");
+  avk::InitParams p{};
+  p.planes = e->planes;
+  p.pref = e->pref[e->cur];
+  p.byz = e->byz;
+  p.seed = e->cfg.seed;
+  p.n_nodes = (uint32_t)e->N;
+  p.n0 = (uint32_t)e->n0;
+  p.NL = e->NL;
+  p.BL = e->BL;
+  p.L = e->L;
+  p.Lpad = e->Lpad;
+  p.t0 = (uint32_t)e->t0;
+  p.n_targets = (uint32_t)e->t1;  // targets >= t1 belong to another shard (or do not exist)
+  p.round = (uint32_t)e->round;
+  p.mode = init_mode;
+  p.param = init_param;
+  AV_HIP(avk::launch_init(p, e->stream));
+  // lanes of the padded tail of the last tile hold no records
+  if (e->Lpad > e->L) {
+    // padded lanes are never loaded (active = g < L), nothing to do
+  }
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_set_valid(av_engine* e, int64_t target, int32_t valid) {
+  AV_ENTER(e);
+  AV_CHECK(target >= 0 && target < e->M, AV_ERR_INVALID_ARG, "target out of range");
+  if (!local_target(e, target)) return AV_OK;
+  const int64_t tl = target - e->t0;
+  const uint32_t b = (uint32_t)(tl >> 5), m = 1u << (tl & 31);
+  e->valid_host[b] = valid ? (e->valid_host[b] | m) : (e->valid_host[b] & ~m);
+  AV_HIP(hipMemcpyAsync(e->valid + b, &e->valid_host[b], 4, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uint8_t* accepted, int64_t n,
+                   uint8_t* added) {
+  AV_ENTER(e);
+  AV_CHECK(n >= 0 && (n == 0 || (targets && accepted && added)), AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
+  std::vector<uint32_t> tl;
+  std::vector<uint8_t> acc;
+  std::vector<int64_t> pos;
+  for (int64_t i = 0; i < n; ++i) {
+    added[i] = 0;
+    if (!local_target(e, targets[i])) continue;
+    tl.push_back((uint32_t)(targets[i] - e->t0));
+    acc.push_back(accepted[i] ? 1 : 0);
+    pos.push_back(i);
+  }
+  if (tl.empty()) return AV_OK;
+  const size_t m = tl.size();
+  Scratch s;
+  AV_HIP(s.ensure(m * 6 + 64));
+  auto* dt = static_cast<uint32_t*>(s.p);
+  auto* da = reinterpret_cast<uint8_t*>(dt + m);
+  auto* dadd = da + m;
+  AV_HIP(hipMemcpyAsync(dt, tl.data(), m * 4, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(hipMemcpyAsync(da, acc.data(), m, hipMemcpyHostToDevice, e->stream));
+  avk::AddParams p{};
+  p.planes = e->planes;
+  p.pref = e->pref[e->cur];
+  p.valid = e->valid;
+  p.byz = e->byz;
+  p.targets = dt;
+  p.accepted = da;
+  p.added = dadd;
+  p.n = (uint32_t)m;
+  p.node_local = (uint32_t)(node - e->n0);
+  p.node = (uint32_t)node;
+  p.BL = e->BL;
+  p.round = (uint32_t)e->round;
+  AV_HIP(avk::launch_add_targets(p, e->stream));
+  std::vector<uint8_t> res(m);
+  AV_HIP(hipMemcpyAsync(res.data(), dadd, m, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  for (size_t i = 0; i < m; ++i) added[pos[i]] = res[i];
+  return AV_OK;
+}
+
+int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const uint32_t* errs, int64_t n,
+                      int32_t* status_out) {
+  AV_ENTER(e);
+  AV_CHECK(n >= 0 && (n == 0 || (targets && errs && status_out)), AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
+  for (int64_t i = 0; i < n; ++i) status_out[i] = -1;
+  // group votes by block, keeping Response order inside each block
+  std::vector<uint32_t> cnt(e->BL + 1, 0);
+  int64_t nv = 0;
+  for (int64_t i = 0; i < n; ++i)
+    if (local_target(e, targets[i])) {
+      cnt[(uint32_t)((targets[i] - e->t0) >> 5)]++;
+      nv++;
+    }
+  if (nv == 0) return AV_OK;
+  std::vector<uint32_t> blocks, offs;
+  std::vector<uint32_t> start(e->BL, 0);
+  uint32_t acc = 0;
+  for (uint32_t b = 0; b < e->BL; ++b) {
+    if (cnt[b]) {
+      blocks.push_back(b);
+      offs.push_back(acc);
+      start[b] = acc;
+      acc += cnt[b];
+    }
+  }
+  offs.push_back(acc);
+  std::vector<uint32_t> entries(2 * (size_t)nv);
+  for (int64_t i = 0; i < n; ++i) {
+    if (!local_target(e, targets[i])) continue;
+    const int64_t tl = targets[i] - e->t0;
+    const uint32_t b = (uint32_t)(tl >> 5);
+    const uint32_t err = errs[i];
+    const uint32_t meta = (uint32_t)(tl & 31) | ((err == 0u ? 1u : 0u) << 5) | (((int32_t)err >= 0 ? 1u : 0u) << 6);
+    const uint32_t slot = start[b]++;
+    entries[2 * (size_t)slot] = (uint32_t)i;
+    entries[2 * (size_t)slot + 1] = meta;
+  }
+  const size_t nb = blocks.size();
+  Scratch s;
+  const size_t words = nb + (nb + 1) + entries.size() + (size_t)n;
+  AV_HIP(s.ensure(words * 4 + 64));
+  auto* dblocks = static_cast<uint32_t*>(s.p);
+  auto* doffs = dblocks + nb;
+  auto* dent = doffs + nb + 1;
+  auto* dstat = reinterpret_cast<int32_t*>(dent + entries.size());
+  AV_HIP(hipMemcpyAsync(dblocks, blocks.data(), nb * 4, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(hipMemcpyAsync(doffs, offs.data(), (nb + 1) * 4, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(hipMemcpyAsync(dent, entries.data(), entries.size() * 4, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(hipMemsetAsync(dstat, 0xFF, (size_t)n * 4, e->stream));
+  avk::DropInParams p{};
+  p.planes = e->planes;
+  p.pref = e->pref[e->cur];
+  p.valid = e->valid;
+  p.byz = e->byz;
+  p.blocks = dblocks;
+  p.offs = doffs;
+  p.entries = dent;
+  p.status_out = dstat;
+  p.n_blocks = (uint32_t)nb;
+  p.node_local = (uint32_t)(node - e->n0);
+  p.node = (uint32_t)node;
+  p.BL = e->BL;
+  p.round = (uint32_t)e->round;
+  AV_HIP(avk::launch_register_votes(p, e->stream));
+  AV_HIP(hipMemcpyAsync(status_out, dstat, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint32_t* out) {
+  AV_ENTER(e);
+  AV_CHECK(out && n0 >= e->n0 && n0 <= n1 && n1 <= e->n1 && t0 >= e->t0 && t0 <= t1 && t1 <= e->t1,
+           AV_ERR_INVALID_ARG, "range outside this engine's shard");
+  const size_t n = (size_t)(n1 - n0) * (size_t)(t1 - t0);
+  if (!n) return AV_OK;
+  Scratch s;
+  AV_HIP(s.ensure(n * 4));
+  AV_HIP(avk::launch_read_records(e->planes, e->BL, (uint32_t)(n0 - e->n0), (uint32_t)(n1 - e->n0),
+                                  (uint32_t)(t0 - e->t0), (uint32_t)(t1 - e->t0), static_cast<uint32_t*>(s.p),
+                                  e->stream));
+  AV_HIP(hipMemcpyAsync(out, s.p, n * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, const uint32_t* in) {
+  AV_ENTER(e);
+  AV_CHECK(in && n0 >= e->n0 && n0 <= n1 && n1 <= e->n1 && t0 >= e->t0 && t0 <= t1 && t1 <= e->t1,
+           AV_ERR_INVALID_ARG, "range outside this engine's shard");
+  const size_t n = (size_t)(n1 - n0) * (size_t)(t1 - t0);
+  if (!n) return AV_OK;
+  Scratch s;
+  AV_HIP(s.ensure(n * 4));
+  AV_HIP(hipMemcpyAsync(s.p, in, n * 4, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(avk::launch_write_records(e->planes, e->BL, (uint32_t)(n0 - e->n0), (uint32_t)(n1 - e->n0),
+                                   (uint32_t)(t0 - e->t0), (uint32_t)(t1 - e->t0), static_cast<uint32_t*>(s.p),
+                                   e->stream));
+  int rc = refresh_pref(e);
+  if (rc != AV_OK) return rc;
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_is_accepted(av_engine* e, int64_t node, int64_t target, int32_t* out) {
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  *out = 0;
+  if (!local_node(e, node) || !local_target(e, target)) return AV_OK;  // no record -> false
+  uint32_t w = 0;
+  int rc = av_read_records(e, node, node + 1, target, target + 1, &w);
+  if (rc != AV_OK) return rc;
+  if (((w >> 17) < (uint32_t)AV_FINALIZATION_SCORE)) *out = (int32_t)((w >> 16) & 1u);
+  return AV_OK;
+}
+
+int av_get_confidence(av_engine* e, int64_t node, int64_t target, uint16_t* out) {
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  if (!local_node(e, node) || !local_target(e, target)) return fail(AV_ERR_NOT_FOUND, "VoteRecord not found");
+  uint32_t w = 0;
+  int rc = av_read_records(e, node, node + 1, target, target + 1, &w);
+  if (rc != AV_OK) return rc;
+  if ((w >> 17) >= (uint32_t)AV_FINALIZATION_SCORE) return fail(AV_ERR_NOT_FOUND, "VoteRecord not found");
+  *out = (uint16_t)(w >> 17);
+  return AV_OK;
+}
+
+int av_get_invs(av_engine* e, int64_t node, int64_t* out_targets, int64_t cap, int64_t* n_out) {
+  AV_CHECK(n_out && (cap == 0 || out_targets), AV_ERR_INVALID_ARG, "null argument");
+  *n_out = 0;
+  AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node not in this shard");
+  std::vector<uint32_t> w((size_t)(e->t1 - e->t0));
+  int rc = av_read_records(e, node, node + 1, e->t0, e->t1, w.data());
+  if (rc != AV_OK) return rc;
+  int64_t cnt = 0;
+  for (int64_t tl = 0; tl < (int64_t)w.size() && cnt < AV_MAX_ELEMENT_POLL; ++tl) {
+    const bool live = (w[tl] >> 17) < (uint32_t)AV_FINALIZATION_SCORE;
+    const bool valid = (e->valid_host[tl >> 5] >> (tl & 31)) & 1u;
+    if (!live || !valid) continue;
+    if (cnt < cap) out_targets[cnt] = e->t0 + tl;
+    cnt++;
+  }
+  *n_out = cnt;
+  AV_CHECK(cnt <= cap, AV_ERR_OVERFLOW, "cap too small (%lld needed)", (long long)cnt);
+  return AV_OK;
+}
+
+int av_run_rounds(av_engine* e, int32_t rounds) {
+  AV_ENTER(e);
+  AV_CHECK(rounds >= 0, AV_ERR_INVALID_ARG, "rounds < 0");
+  for (int32_t r = 0; r < rounds; ++r) {
+    int rc = launch_one_round(e, nullptr);
+    if (rc != AV_OK) return rc;
+  }
+  return AV_OK;
+}
+
+int av_replay_round_errs(av_engine* e, const uint32_t* errs) {
+  AV_ENTER(e);
+  AV_CHECK(errs, AV_ERR_INVALID_ARG, "null argument");
+  const int64_t TL = e->t1 - e->t0;
+  std::vector<uint32_t> planes(e->round_replay_words(), 0u);
+  for (uint32_t nl = 0; nl < e->NL; ++nl)
+    for (int s = 0; s < e->k; ++s) {
+      const uint32_t* row = errs + ((size_t)nl * e->k + s) * TL;
+      for (uint32_t b = 0; b < e->BL; ++b) {
+        uint32_t y = 0, c = 0;
+        for (uint32_t i = 0; i < 32; ++i) {
+          const int64_t tl = 32ll * b + i;
+          if (tl >= TL) break;
+          const uint32_t err = row[tl];
+          y |= (err == 0u ? 1u : 0u) << i;             // vote.go:55
+          c |= ((int32_t)err >= 0 ? 1u : 0u) << i;     // vote.go:56
+        }
+        const size_t g = (size_t)nl * e->BL + b;
+        planes[(size_t)(2 * s) * e->Lpad + g] = y;
+        planes[(size_t)(2 * s + 1) * e->Lpad + g] = c;
+      }
+    }
+  Scratch s;
+  AV_HIP(s.ensure(planes.size() * 4));
+  AV_HIP(hipMemcpyAsync(s.p, planes.data(), planes.size() * 4, hipMemcpyHostToDevice, e->stream));
+  int rc = launch_one_round(e, static_cast<uint32_t*>(s.p));
+  if (rc != AV_OK) return rc;
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_replay_prepare(av_engine* e, int32_t rounds) {
+  AV_ENTER(e);
+  AV_CHECK(rounds >= 1, AV_ERR_INVALID_ARG, "rounds < 1");
+  const size_t per = e->round_replay_words();
+  if (rounds > e->replay_cap_rounds) {
+    if (e->replay) AV_HIP(hipFree(e->replay));
+    e->replay = nullptr;
+    e->replay_cap_rounds = 0;
+    hipError_t he = dev_alloc(&e->replay, per * rounds);
+    AV_CHECK(he == hipSuccess, he == hipErrorOutOfMemory ? AV_ERR_OOM : AV_ERR_HIP, "alloc replay: %s",
+             hipGetErrorString(he));
+    e->replay_cap_rounds = rounds;
+  }
+  for (int32_t r = 0; r < rounds; ++r)
+    AV_HIP(avk::launch_gen_replay(e->cfg.seed, (uint32_t)e->n0, e->NL, e->BL, e->L, e->Lpad, (uint32_t)e->t0,
+                                  (uint32_t)e->t1, (uint32_t)(e->round + r), e->k, e->replay + per * r, e->stream));
+  e->replay_first = e->round;
+  e->replay_ready = rounds;
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_replay_rounds(av_engine* e, int32_t rounds) {
+  AV_ENTER(e);
+  AV_CHECK(rounds >= 0, AV_ERR_INVALID_ARG, "rounds < 0");
+  AV_CHECK(e->round >= e->replay_first && e->round + rounds <= e->replay_first + e->replay_ready,
+           AV_ERR_INVALID_ARG, "replay stream not prepared for these rounds");
+  const size_t per = e->round_replay_words();
+  for (int32_t r = 0; r < rounds; ++r) {
+    int rc = launch_one_round(e, e->replay + per * (size_t)(e->round - e->replay_first));
+    if (rc != AV_OK) return rc;
+  }
+  return AV_OK;
+}
+
+int av_synchronize(av_engine* e) {
+  AV_ENTER(e);
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_round_index(av_engine* e, int64_t* out) {
+  AV_CHECK(e && out, AV_ERR_INVALID_ARG, "null argument");
+  *out = e->round;
+  return AV_OK;
+}
+
+int av_updates_count(av_engine* e, int64_t* n) {
+  AV_ENTER(e);
+  AV_CHECK(n, AV_ERR_INVALID_ARG, "null argument");
+  std::vector<uint32_t> counts(avk::kLogShards);
+  AV_HIP(hipMemcpyAsync(counts.data(), e->log_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  int64_t total = 0;
+  for (uint32_t c : counts) total += c;
+  *n = total;
+  return AV_OK;
+}
+
+int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
+  AV_ENTER(e);
+  AV_CHECK(n_out && (cap == 0 || out), AV_ERR_INVALID_ARG, "null argument");
+  std::vector<uint32_t> counts(avk::kLogShards);
+  uint32_t ovf = 0;
+  AV_HIP(hipMemcpyAsync(counts.data(), e->log_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpyAsync(&ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  int64_t total = 0;
+  std::vector<uint64_t> offs(avk::kLogShards);
+  for (uint32_t i = 0; i < avk::kLogShards; ++i) {
+    offs[i] = (uint64_t)total;
+    total += std::min<uint32_t>(counts[i], e->log_cap);
+  }
+  *n_out = total;
+  if (ovf) {
+    int64_t all = 0;
+    for (uint32_t c : counts) all += c;
+    *n_out = all;
+    AV_HIP(hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream));
+    AV_HIP(hipMemsetAsync(e->log_overflow, 0, 4, e->stream));
+    AV_HIP(hipStreamSynchronize(e->stream));
+    e->log_base = e->round;
+    return fail(AV_ERR_OVERFLOW, "device StatusUpdate log overflowed (%lld updates, capacity %lld per shard)",
+                (long long)all, (long long)e->log_cap);
+  }
+  AV_CHECK(total <= cap, AV_ERR_OVERFLOW, "cap too small: %lld updates pending", (long long)total);
+  if (total > 0) {
+    Scratch s;
+    AV_HIP(s.ensure((size_t)total * 8 + avk::kLogShards * 8));
+    auto* dense = static_cast<uint64_t*>(s.p);
+    auto* doffs = dense + total;
+    AV_HIP(hipMemcpyAsync(doffs, offs.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
+    AV_HIP(avk::launch_compact_log(e->log, e->log_count, doffs, e->log_cap, dense, e->stream));
+    AV_HIP(hipMemcpyAsync(out, dense, (size_t)total * 8, hipMemcpyDeviceToHost, e->stream));
+    AV_HIP(hipStreamSynchronize(e->stream));
+    std::sort(out, out + total);
+  }
+  AV_HIP(hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  e->log_base = e->round;
+  return AV_OK;
+}
+
+int av_applied_votes(av_engine* e, int64_t* out) {
+  AV_ENTER(e);
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  std::vector<unsigned long long> c(avk::kLogShards);
+  AV_HIP(hipMemcpyAsync(c.data(), e->applied, avk::kLogShards * 8, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  unsigned long long t = 0;
+  for (auto v : c) t += v;
+  *out = (int64_t)t;
+  return AV_OK;
+}
+
+int av_read_pref(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint8_t* out) {
+  AV_ENTER(e);
+  AV_CHECK(out && n0 >= 0 && n0 <= n1 && n1 <= e->N && t0 >= e->t0 && t0 <= t1 && t1 <= e->t1,
+           AV_ERR_INVALID_ARG, "bad range");
+  const size_t rows = (size_t)(n1 - n0);
+  std::vector<uint32_t> w(rows * e->BL);
+  if (rows) {
+    AV_HIP(hipMemcpyAsync(w.data(), e->pref[e->cur] + (size_t)n0 * e->BL, w.size() * 4, hipMemcpyDeviceToHost,
+                          e->stream));
+    AV_HIP(hipStreamSynchronize(e->stream));
+  }
+  const int64_t W = t1 - t0;
+  for (size_t r = 0; r < rows; ++r)
+    for (int64_t t = t0; t < t1; ++t) {
+      const int64_t tl = t - e->t0;
+      out[r * W + (t - t0)] = (uint8_t)((w[r * e->BL + (tl >> 5)] >> (tl & 31)) & 1u);
+    }
+  return AV_OK;
+}
+
+int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t* out) {
+  AV_ENTER(e);
+  AV_CHECK(out && n0 >= 0 && n0 <= n1 && n1 <= e->N && round >= 0, AV_ERR_INVALID_ARG, "bad range");
+  const size_t n = (size_t)(n1 - n0) * e->k;
+  if (!n) return AV_OK;
+  Scratch s;
+  AV_HIP(s.ensure(n * 4));
+  AV_HIP(avk::launch_sample_peers(e->cfg.seed, (uint32_t)e->N, (uint32_t)n0, (uint32_t)n1, (uint32_t)round, e->k,
+                                  e->cfg.peer_mode, static_cast<uint32_t*>(s.p), e->stream));
+  AV_HIP(hipMemcpyAsync(out, s.p, n * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_set_timing(av_engine* e, int32_t enable) {
+  AV_ENTER(e);
+  e->timing = enable != 0;
+  return AV_OK;
+}
+
+int av_kernel_stats(av_engine* e, double* total_ms, int64_t* launches) {
+  AV_ENTER(e);
+  AV_CHECK(total_ms && launches, AV_ERR_INVALID_ARG, "null argument");
+  AV_HIP(hipStreamSynchronize(e->stream));
+  for (auto& ev : e->events) {
+    float ms = 0.f;
+    AV_HIP(hipEventElapsedTime(&ms, ev.first, ev.second));
+    e->timed_ms += ms;
+    e->timed_launches++;
+    (void)hipEventDestroy(ev.first);
+    (void)hipEventDestroy(ev.second);
+  }
+  e->events.clear();
+  *total_ms = e->timed_ms;
+  *launches = e->timed_launches;
+  e->timed_ms = 0.0;
+  e->timed_launches = 0;
+  return AV_OK;
+}
+
+int av_layout_info(av_engine* e, int64_t* lanes, int64_t* local_nodes, int64_t* local_blocks, int32_t* capped) {
+  AV_CHECK(e, AV_ERR_INVALID_ARG, "null engine");
+  if (lanes) *lanes = e->L;
+  if (local_nodes) *local_nodes = e->NL;
+  if (local_blocks) *local_blocks = e->BL;
+  if (capped) *capped = e->capped ? 1 : 0;
+  return AV_OK;
+}
+
+int av_comm_unique_id(uint8_t out[128]) {
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  AV_CHECK(r == ncclSuccess, AV_ERR_RCCL, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  std::memcpy(out, &id, 128);
+  return AV_OK;
+}
+
+int av_comm_init(av_engine* e, int32_t world, int32_t rank, const uint8_t id[128]) {
+  AV_ENTER(e);
+  AV_CHECK(id && world >= 1 && rank >= 0 && rank < world, AV_ERR_INVALID_ARG, "bad world/rank");
+  AV_CHECK(e->N % world == 0 && (int64_t)e->NL * world == e->N && e->n0 == (int64_t)rank * e->NL,
+           AV_ERR_UNSUPPORTED, "node shards must be equal, contiguous and rank-ordered (N %% world == 0)");
+  AV_CHECK(e->t0 == 0 && e->t1 == e->M, AV_ERR_UNSUPPORTED, "node sharding needs the full target range");
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  ncclResult_t r = ncclCommInitRank(&e->comm, world, uid, rank);
+  AV_CHECK(r == ncclSuccess, AV_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+  e->world = world;
+  e->rank = rank;
+  // make every rank's initial preference rows visible everywhere
+  const size_t count = (size_t)e->NL * e->BL;
+  uint32_t* cur = e->pref[e->cur];
+  r = ncclAllGather(cur + (size_t)e->n0 * e->BL, cur, count, ncclUint32, e->comm, e->stream);
+  AV_CHECK(r == ncclSuccess, AV_ERR_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,119 @@
+// Internal interface between the C-ABI engine (engine.cpp) and the CDNA4
+// kernels (kernels.hip). Not part of the public ABI (include/avhip.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace avk {
+
+// ---------------------------------------------------------------------------
+// State layout in HBM (see DESIGN.md "Data layout").
+//
+// One *block* = 32 consecutive targets of one node. Its 32 VoteRecords
+// (vote.go:25-29) are stored bit-sliced as 25 u32 planes:
+//   V0..V7  votes shift register, V0 = most recent vote   (vote.go:26)
+//   C0..C7  consider shift register                         (vote.go:27)
+//   A       accepted bit = confidence & 1                   (vote.go:38-40)
+//   K0..K7  count = confidence >> 1 (0..127 live); K7 = 1 marks "no live
+//           record" (deleted after finalization, processor.go:114-116, or
+//           never added). A dead record keeps A = published decision.
+// A *lane* is one (local node, local block) pair, g = node_local * BL + b.
+// Lanes are grouped in tiles of 64 (one wavefront); a tile stores its 25
+// planes contiguously: word(g, p) = planes[((g >> 6) * 25 + p) * 64 + (g & 63)]
+// so one wave reads/writes one contiguous 6400-byte span per round.
+// ---------------------------------------------------------------------------
+constexpr int kPlanes = 25;
+constexpr int kPV = 0, kPC = 8, kPA = 16, kPK = 17;
+constexpr uint32_t kLogShards = 1024;   // update-log / counter shards
+constexpr uint32_t kMaxPoll = 4096;     // AvalancheMaxElementPoll, avalanche.go:17
+constexpr int kMaxK = 16;
+
+struct RoundParams {
+  uint32_t* planes;
+  const uint32_t* pref_in;   // [N_pad][BL] published preference (round start)
+  uint32_t* pref_out;        // [N_pad][BL] published preference (round end)
+  const uint32_t* valid;     // [BL] Target.IsValid() bits
+  const uint32_t* byz;       // [ceil(N/32)] Byzantine node bits
+  const uint32_t* replay;    // [k][2][Lpad] yes/consider planes (replay mode)
+  uint64_t* log;             // [kLogShards][log_cap]
+  uint32_t* log_count;       // [kLogShards]
+  uint32_t* log_overflow;    // [1]
+  unsigned long long* applied;  // [kLogShards] regsiterVote applications
+  uint64_t seed;
+  uint32_t log_cap;          // entries per shard
+  uint32_t n_nodes;          // N (global)
+  uint32_t n0;               // first local node (global id)
+  uint32_t NL;               // local nodes
+  uint32_t BL;               // local blocks per node
+  uint32_t L;                // lanes = NL * BL
+  uint32_t Lpad;             // tiles * 64
+  uint32_t t0;               // first local target (global id, multiple of 32)
+  uint32_t round;            // global round index (RNG counter, byz pattern)
+  uint32_t round_rel;        // round - log base (update key field)
+  int32_t peer_mode;
+};
+
+// Update-log entry (one StatusUpdate, avalanche.go:59-62):
+//   [63:52] round - log_base | [51:28] node | [27:24] slot | [23:2] target | [1:0] status
+// Ascending order of the packed word == canonical (round, node, slot, target).
+__host__ __device__ inline uint64_t pack_update(uint32_t round_rel, uint32_t node, uint32_t slot,
+                                                uint32_t target, uint32_t status) {
+  return ((uint64_t)round_rel << 52) | ((uint64_t)node << 28) | ((uint64_t)slot << 24) |
+         ((uint64_t)target << 2) | (uint64_t)status;
+}
+
+hipError_t launch_round(const RoundParams& p, int k, bool replay, bool capped, hipStream_t s);
+
+struct InitParams {
+  uint32_t* planes;
+  uint32_t* pref;       // [N_pad][BL]
+  const uint32_t* byz;
+  uint64_t seed;
+  uint32_t n_nodes, n0, NL, BL, L, Lpad, t0, n_targets, round;
+  int32_t mode;
+  uint32_t param;
+};
+hipError_t launch_init(const InitParams& p, hipStream_t s);
+hipError_t launch_byz(uint32_t* byz, uint32_t n_nodes, uint64_t seed, uint32_t threshold, hipStream_t s);
+
+struct DropInParams {
+  uint32_t* planes;
+  uint32_t* pref;          // current published snapshot row for the node
+  const uint32_t* valid;
+  const uint32_t* byz;
+  const uint32_t* blocks;  // touched local blocks
+  const uint32_t* offs;    // [n_blocks + 1] into entries
+  const uint32_t* entries; // pairs (pos, meta = bit | yes<<5 | considered<<6)
+  int32_t* status_out;     // per vote position, -1 = no update
+  uint32_t n_blocks, node_local, node, BL, round;
+};
+hipError_t launch_register_votes(const DropInParams& p, hipStream_t s);
+
+struct AddParams {
+  uint32_t* planes;
+  uint32_t* pref;
+  const uint32_t* valid;
+  const uint32_t* byz;
+  const uint32_t* targets;  // local target index
+  const uint8_t* accepted;
+  uint8_t* added;
+  uint32_t n, node_local, node, BL, round;
+};
+hipError_t launch_add_targets(const AddParams& p, hipStream_t s);
+
+hipError_t launch_read_records(const uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1,
+                               uint32_t tl0, uint32_t tl1, uint32_t* out, hipStream_t s);
+hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0,
+                                uint32_t tl1, const uint32_t* in, hipStream_t s);
+hipError_t launch_refresh_pref(const uint32_t* planes, uint32_t* pref, const uint32_t* byz, uint32_t n0,
+                               uint32_t NL, uint32_t BL, uint32_t round, hipStream_t s);
+hipError_t launch_sample_peers(uint64_t seed, uint32_t n_nodes, uint32_t a, uint32_t b, uint32_t round,
+                               int k, int mode, uint32_t* out, hipStream_t s);
+hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t BL, uint32_t L, uint32_t Lpad,
+                             uint32_t t0, uint32_t n_targets, uint32_t round, int k, uint32_t* out,
+                             hipStream_t s);
+hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets,
+                              uint32_t log_cap, uint64_t* out, hipStream_t s);
+
+}  // namespace avk

@@ -1,0 +1,839 @@
+// CDNA4 (gfx950) kernels of the batched Avalanche voting engine.
+//
+// The hot path is one round of go-avalanche's poll loop for every simulated
+// node at once: peer sampling (processor.go:173-182 / main.go:110-116 replaced
+// by a counter-RNG k-peer draw), the peer-preference gather (main.go:168-192
+// responder), the VoteRecord shift-register / confidence update
+// (vote.go:54-91) inside RegisterVotes (processor.go:92-117) and StatusUpdate
+// emission (processor.go:111) with deletion on finalization (:114-116).
+//
+// Records are bit-sliced: one lane owns 32 records (a block of 32 targets of
+// one node) as 25 u32 planes, so every VALU instruction advances 32
+// VoteRecords. Nothing here is a dense contraction; there is no MFMA. The
+// kernels are HBM-bound streaming kernels (DESIGN.md "Roofline").
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace avk {
+namespace {
+
+constexpr uint32_t kDomPeers = 1u, kDomByz = 2u, kDomInit = 3u, kDomPairs = 4u, kDomReplay = 5u;
+// replay class thresholds: P(yes)=0.70, P(no)=0.25, P(neutral)=0.05
+constexpr uint32_t kReplayYes = 3006477107u, kReplayNo = 4080218931u;
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. SC'11), same counter/key conventions as the
+// oracle's restatement (oracle/avalanche_oracle.c) and Random123's KATs.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void philox(uint32_t x[4], uint64_t seed, uint32_t a, uint32_t b, uint32_t c,
+                                       uint32_t dom) {
+  uint32_t c0 = a, c1 = b, c2 = c, c3 = dom;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+  }
+  x[0] = c0; x[1] = c1; x[2] = c2; x[3] = c3;
+}
+
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+// Byzantine flip-flop answer: err = ((r ^ t) & 1) ? 1 : 0, so
+// "yes" on even targets in even rounds. Blocks start at multiples of 32.
+__device__ __forceinline__ uint32_t byz_pattern(uint32_t round) { return (round & 1u) ? 0xAAAAAAAAu : 0x55555555u; }
+
+__device__ __forceinline__ bool is_byz(const uint32_t* byz, uint32_t node) { return (byz[node >> 5] >> (node & 31u)) & 1u; }
+
+struct St {
+  uint32_t V[8], C[8], A, K[8];
+};
+
+__device__ __forceinline__ const uint32_t* tile_base(const uint32_t* planes, uint32_t g) {
+  return planes + (size_t)(g >> 6) * (kPlanes * 64) + (g & 63u);
+}
+
+__device__ __forceinline__ void load_state(const uint32_t* planes, uint32_t g, St& s) {
+  const uint32_t* t = tile_base(planes, g);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.V[i] = t[(kPV + i) * 64];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.C[i] = t[(kPC + i) * 64];
+  s.A = t[kPA * 64];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s.K[i] = t[(kPK + i) * 64];
+}
+
+__device__ __forceinline__ void store_state(uint32_t* planes, uint32_t g, const St& s) {
+  uint32_t* t = const_cast<uint32_t*>(tile_base(planes, g));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[(kPV + i) * 64] = s.V[i];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[(kPC + i) * 64] = s.C[i];
+  t[kPA * 64] = s.A;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[(kPK + i) * 64] = s.K[i];
+}
+
+// No live record in any of the 32 slots (canonical dead form).
+__device__ __forceinline__ void dead_state(St& s) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s.V[i] = 0u;
+    s.C[i] = ~0u;
+    s.K[i] = 0u;
+  }
+  s.K[7] = ~0u;
+  s.A = 0u;
+}
+
+// Bit-sliced "popcount of 8 > 6" (vote.go:58,61): at most one zero among x[].
+__device__ __forceinline__ uint32_t atleast7(const uint32_t (&x)[8]) {
+  uint32_t t = x[0], u = ~0u;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    u = (u & x[i]) | t;
+    t &= x[i];
+  }
+  return u;
+}
+
+// One regsiterVote (vote.go:54-75) applied to the records of `part`.
+//   yw : err == 0            (vote.go:55)
+//   cw : int32(err) >= 0     (vote.go:56)
+// MASKED=false shifts every bit (caller restores non-participants at the end
+// of the round); MASKED=true leaves non-participating records untouched.
+// Outputs E = records whose regsiterVote returned true, fin = finalized now.
+template <bool MASKED>
+__device__ __forceinline__ void vote_step(St& s, uint32_t yw, uint32_t cw, uint32_t part, uint32_t& E,
+                                          uint32_t& fin) {
+  yw &= cw;
+  if (MASKED) {
+#pragma unroll
+    for (int i = 7; i > 0; --i) {
+      s.V[i] = bfi(part, s.V[i - 1], s.V[i]);
+      s.C[i] = bfi(part, s.C[i - 1], s.C[i]);
+    }
+    s.V[0] = bfi(part, yw, s.V[0]);
+    s.C[0] = bfi(part, cw, s.C[0]);
+  } else {
+#pragma unroll
+    for (int i = 7; i > 0; --i) {
+      s.V[i] = s.V[i - 1];
+      s.C[i] = s.C[i - 1];
+    }
+    s.V[0] = yw;
+    s.C[0] = cw;
+  }
+  uint32_t y[8], n[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    y[i] = s.V[i] & s.C[i];   // votes & consider            (vote.go:58)
+    n[i] = ~s.V[i] & s.C[i];  // (-votes-1) & consider        (vote.go:61)
+  }
+  const uint32_t yes = atleast7(y);
+  const uint32_t no = atleast7(n);
+  const uint32_t concl = (yes | no) & part;  // conclusive     (vote.go:61-63)
+  const uint32_t flip = concl & (s.A ^ yes);  // disagrees      (vote.go:72-74)
+  uint32_t carry = concl ^ flip;              // agrees: conf+=2 (vote.go:66-69)
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    const uint32_t c2 = s.K[i] & carry;
+    s.K[i] = (s.K[i] ^ carry) & ~flip;  // flip resets the count
+    carry = c2;
+  }
+  s.K[7] |= carry;  // count reached exactly 128 (vote.go:68), record deleted
+  s.A = bfi(flip, yes, s.A);
+  E = flip | carry;
+  fin = carry;
+}
+
+// k distinct peers != node, uniform over the other N-1 nodes (first K
+// distinct values of the Philox candidate stream; same definition as
+// avo_sample_peers in the oracle). Fast path = the first ceil(K/4) Philox
+// blocks give K distinct candidates; otherwise a rarely taken general loop.
+template <int K>
+__device__ __forceinline__ void sample_peers(uint64_t seed, uint32_t node, uint32_t round, uint32_t n_nodes,
+                                             int mode, uint32_t (&out)[K]) {
+  const uint32_t others = n_nodes - 1u;
+  if (mode == 1 || (uint32_t)K >= others) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint64_t q = (mode == 1) ? (uint64_t)round * (uint64_t)K + (uint64_t)j : (uint64_t)j;
+      const uint32_t idx = (uint32_t)(q % others);
+      out[j] = idx + (idx >= node ? 1u : 0u);
+    }
+    return;
+  }
+  constexpr int NB = (K + 3) / 4;
+  uint32_t cand[NB * 4];
+#pragma unroll
+  for (int blk = 0; blk < NB; ++blk) {
+    uint32_t x[4];
+    philox(x, seed, node, round, (uint32_t)blk, kDomPeers);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t u = (uint32_t)(((uint64_t)x[i] * others) >> 32);
+      cand[blk * 4 + i] = u + (u >= node ? 1u : 0u);
+    }
+  }
+  bool distinct = true;
+#pragma unroll
+  for (int i = 1; i < K; ++i)
+#pragma unroll
+    for (int j = 0; j < i; ++j) distinct &= cand[i] != cand[j];
+  if (distinct) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) out[j] = cand[j];
+    return;
+  }
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) out[j] = 0u;
+  for (uint32_t blk = 0; cnt < (uint32_t)K; ++blk) {
+    uint32_t x[4];
+    philox(x, seed, node, round, blk, kDomPeers);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t u = (uint32_t)(((uint64_t)x[i] * others) >> 32);
+      const uint32_t pp = u + (u >= node ? 1u : 0u);
+      bool dup = false;
+#pragma unroll
+      for (int j = 0; j < K; ++j) dup |= ((uint32_t)j < cnt) && (out[j] == pp);
+      if (!dup && cnt < (uint32_t)K) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) out[j] = ((uint32_t)j == cnt) ? pp : out[j];
+        ++cnt;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)v, (unsigned)d, 64);
+    if (lane >= (uint32_t)d) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d, 64);
+  return v;
+}
+
+// End-of-round StatusUpdate emission (processor.go:111) for one wave: one
+// atomic per emitting wave on a sharded log counter, entries in
+// (slot, lane, target) order inside the wave's reservation. Status is
+// derived from the final A plane: after slot j, A_j = A_final ^ parity(E at
+// later slots) (only flips change A); a record finalized this round has a
+// single E bit (count 127 -> 128 cannot follow a flip within 16 votes).
+template <int K>
+__device__ __forceinline__ void emit_updates(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t node,
+                                             uint32_t tbase, const uint32_t (&E)[K], uint32_t A_final,
+                                             uint32_t died) {
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) cnt += __popc(E[j]);
+  if (__ballot(cnt != 0u) == 0ull) return;
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+  const uint32_t shard = wave_id & (kLogShards - 1u);
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(&p.log_count[shard], total);
+  base = (uint32_t)__shfl((int)base, 0, 64);
+  if (cnt == 0u) return;
+  uint32_t Aj[K];
+  uint32_t par = 0;
+#pragma unroll
+  for (int j = K - 1; j >= 0; --j) {
+    Aj[j] = A_final ^ par;
+    par ^= E[j];
+  }
+  uint64_t* dst = p.log + (size_t)shard * p.log_cap;
+  uint32_t pos = base + incl - cnt;
+  bool ovf = false;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    uint32_t e = E[j];
+    while (e) {
+      const uint32_t bit = (uint32_t)__ffs(e) - 1u;
+      e &= e - 1u;
+      const uint32_t a = (Aj[j] >> bit) & 1u;
+      const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
+      if (pos < p.log_cap)
+        dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
+      else
+        ovf = true;
+      ++pos;
+    }
+  }
+  if (ovf) atomicOr(p.log_overflow, 1u);
+}
+
+__device__ __forceinline__ void count_applied(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied) {
+  const uint32_t s = wave_sum(applied);
+  if (lane == 0 && s) atomicAdd(&p.applied[wave_id & (kLogShards - 1u)], (unsigned long long)s);
+}
+
+// ---------------------------------------------------------------------------
+// Round kernel, uncapped path (every node has <= 4096 live valid targets, so
+// GetInvsForNextPoll never truncates: processor.go:165-167). One lane = one
+// 32-record block; no cross-lane dependence except the emission scan.
+// ---------------------------------------------------------------------------
+template <int K, bool REPLAY>
+__global__ __launch_bounds__(256) void k_round_fast(const RoundParams p) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  if ((g & ~63u) >= p.L) return;  // whole wave beyond the last tile
+  const bool active = g < p.L;
+  const uint32_t nl = active ? g / p.BL : 0u;
+  const uint32_t b = active ? g - nl * p.BL : 0u;
+  const uint32_t node = p.n0 + nl;
+
+  St s;
+  if (active)
+    load_state(p.planes, g, s);
+  else
+    dead_state(s);
+
+  uint32_t w[K], cw[K];
+  if (REPLAY) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      w[j] = active ? p.replay[(size_t)(2 * j) * p.Lpad + g] : 0u;
+      cw[j] = active ? p.replay[(size_t)(2 * j + 1) * p.Lpad + g] : 0u;
+    }
+  } else {
+    uint32_t peers[K];
+    sample_peers<K>(p.seed, node, p.round, p.n_nodes, p.peer_mode, peers);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      w[j] = active ? p.pref_in[(size_t)peers[j] * p.BL + b] : 0u;  // peer's published preference
+      cw[j] = ~0u;                                                  // honest/Byzantine votes are 0 or 1
+    }
+  }
+  const uint32_t vmask = active ? p.valid[b] : 0u;
+  const uint32_t live0 = ~s.K[7];
+  const uint32_t P0 = live0 & vmask;
+
+  uint32_t alive = P0, applied = 0, E[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    applied += __popc(alive);
+    uint32_t fin;
+    vote_step<false>(s, w[j], cw[j], alive, E[j], fin);
+    alive &= ~fin;
+  }
+  const uint32_t died = P0 & ~alive;
+  const uint32_t keep = live0 & ~vmask;  // live but !IsValid(): skipped (processor.go:101-103)
+
+  if (active) {
+    uint32_t Vo[8], Co[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Vo[i] = Co[i] = 0u;
+    if (keep) {
+      const uint32_t* t = tile_base(p.planes, g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        Vo[i] = t[(kPV + i) * 64];
+        Co[i] = t[(kPC + i) * 64];
+      }
+    }
+    const uint32_t dead = ~(alive | keep);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s.V[i] = (s.V[i] & alive) | (Vo[i] & keep);
+      s.C[i] = (s.C[i] & alive) | (Co[i] & keep) | dead;
+    }
+    store_state(p.planes, g, s);
+    p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
+  }
+  const uint32_t wave_id = g >> 6;
+  count_applied(p, wave_id, lane, applied);
+  emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
+}
+
+// ---------------------------------------------------------------------------
+// Round kernel, capped path: one workgroup per node; per slot a workgroup
+// prefix count of live valid records selects the first 4096 in ascending
+// target order (GetInvsForNextPoll truncation, processor.go:165-167).
+// ---------------------------------------------------------------------------
+template <int K, bool REPLAY>
+__global__ __launch_bounds__(1024) void k_round_capped(const RoundParams p) {
+  __shared__ uint32_t wsum[2][16];
+  const uint32_t nl = blockIdx.x;
+  const uint32_t b = threadIdx.x;
+  const uint32_t lane = b & 63u, wave = b >> 6;
+  const bool active = b < p.BL;
+  const uint32_t g = nl * p.BL + b;
+  const uint32_t node = p.n0 + nl;
+
+  St s;
+  if (active)
+    load_state(p.planes, g, s);
+  else
+    dead_state(s);
+  uint32_t w[K], cw[K];
+  if (REPLAY) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      w[j] = active ? p.replay[(size_t)(2 * j) * p.Lpad + g] : 0u;
+      cw[j] = active ? p.replay[(size_t)(2 * j + 1) * p.Lpad + g] : 0u;
+    }
+  } else {
+    uint32_t peers[K];
+    sample_peers<K>(p.seed, node, p.round, p.n_nodes, p.peer_mode, peers);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      w[j] = active ? p.pref_in[(size_t)peers[j] * p.BL + b] : 0u;
+      cw[j] = ~0u;
+    }
+  }
+  const uint32_t vmask = active ? p.valid[b] : 0u;
+  const uint32_t P0 = ~s.K[7] & vmask;
+
+  uint32_t alive = P0, applied = 0, E[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t c = __popc(alive);
+    const uint32_t incl = wave_incl_scan(c, lane);
+    if (lane == 63u) wsum[j & 1][wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t q = 0; q < wave; ++q) before += wsum[j & 1][q];
+    const uint32_t excl = before + incl - c;
+    uint32_t polled;
+    if (excl >= kMaxPoll) {
+      polled = 0u;
+    } else if (excl + c <= kMaxPoll) {
+      polled = alive;
+    } else {  // keep the lowest (4096 - excl) set bits
+      uint32_t x = alive;
+      polled = 0u;
+      for (uint32_t q = 0; q < kMaxPoll - excl; ++q) {
+        const uint32_t low = x & (0u - x);
+        polled |= low;
+        x ^= low;
+      }
+    }
+    applied += __popc(polled);
+    uint32_t fin;
+    vote_step<true>(s, w[j], cw[j], polled, E[j], fin);
+    alive &= ~fin;
+  }
+  const uint32_t died = P0 & ~alive;
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s.V[i] &= ~died;
+      s.C[i] |= died;
+    }
+    store_state(p.planes, g, s);
+    p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
+  }
+  const uint32_t wave_id = blockIdx.x * 16u + wave;
+  count_applied(p, wave_id, lane, applied);
+  emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
+}
+
+// ---------------------------------------------------------------------------
+// Drop-in RegisterVotes for one node (processor.go:61-122): one thread per
+// touched block applies that block's votes in Response order, so duplicate
+// hashes in one Response apply sequentially. Status per vote position.
+// ---------------------------------------------------------------------------
+__global__ void k_register_votes(const DropInParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_blocks) return;
+  const uint32_t b = p.blocks[i];
+  const uint32_t g = p.node_local * p.BL + b;
+  St s;
+  load_state(p.planes, g, s);
+  const uint32_t vmask = p.valid[b];
+  uint32_t died = 0;
+  for (uint32_t e = p.offs[i]; e < p.offs[i + 1]; ++e) {
+    const uint32_t pos = p.entries[2 * e];
+    const uint32_t meta = p.entries[2 * e + 1];
+    const uint32_t m = 1u << (meta & 31u);
+    const uint32_t part = ~s.K[7] & vmask & m;  // skip unknown/deleted (:95-99) and invalid (:101-103)
+    uint32_t E, fin;
+    vote_step<true>(s, (meta >> 5) & 1u ? m : 0u, (meta >> 6) & 1u ? m : 0u, part, E, fin);
+    died |= fin;
+    int32_t st = -1;
+    if (E & m) st = (fin & m) ? ((s.A & m) ? 3 : 0) : ((s.A & m) ? 2 : 1);
+    p.status_out[pos] = st;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    s.V[q] &= ~died;
+    s.C[q] |= died;
+  }
+  store_state(p.planes, g, s);
+  p.pref[(size_t)p.node * p.BL + b] = is_byz(p.byz, p.node) ? byz_pattern(p.round) : s.A;
+}
+
+// AddTargetToReconcile (processor.go:45-58) for a list of targets of one
+// node, applied sequentially by one thread (duplicates return false).
+__global__ void k_add_targets(const AddParams p) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  for (uint32_t i = 0; i < p.n; ++i) {
+    const uint32_t t = p.targets[i];
+    const uint32_t b = t >> 5, m = 1u << (t & 31u);
+    const uint32_t g = p.node_local * p.BL + b;
+    uint32_t* base = const_cast<uint32_t*>(tile_base(p.planes, g));
+    const bool valid = (p.valid[b] & m) != 0u;       // isWorthyPolling (:46-48)
+    const bool exists = (base[(kPK + 7) * 64] & m) == 0u;  // record present (:50-53)
+    if (!valid || exists) {
+      p.added[i] = 0;
+      continue;
+    }
+    for (int q = 0; q < 8; ++q) {  // NewVoteRecord(t.IsAccepted()) (vote.go:33-35)
+      base[(kPV + q) * 64] &= ~m;
+      base[(kPC + q) * 64] &= ~m;
+      base[(kPK + q) * 64] &= ~m;
+    }
+    base[kPA * 64] = p.accepted[i] ? (base[kPA * 64] | m) : (base[kPA * 64] & ~m);
+    p.added[i] = 1;
+    p.pref[(size_t)p.node * p.BL + b] = is_byz(p.byz, p.node) ? byz_pattern(p.round) : base[kPA * 64];
+  }
+}
+
+__device__ __forceinline__ uint32_t init_accept_block(uint64_t seed, int mode, uint32_t param, uint32_t node,
+                                                      uint32_t tb /* first target, multiple of 32 */) {
+  uint32_t a = 0;
+  if (mode == 2) return ~0u;
+  if (mode == 3) {  // Bernoulli: philox(node, t>>2, 0, INIT)[t&3] < param
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      uint32_t x[4];
+      philox(x, seed, node, (tb >> 2) + q, 0u, kDomInit);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a |= (x[i] < param ? 1u : 0u) << (q * 4 + i);
+    }
+  } else if (mode == 4) {  // pairs (2p, 2p+1): coin = philox(node, p>>2, 0, PAIRS)[p&3] >> 31
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t x[4];
+      philox(x, seed, node, (tb >> 3) + q, 0u, kDomPairs);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t coin = x[i] >> 31;
+        const int pr = q * 4 + i;  // pair index inside the block (0..15)
+        a |= (coin << (2 * pr)) | ((coin ^ 1u) << (2 * pr + 1));
+      }
+    }
+  }
+  return a;
+}
+
+__device__ __forceinline__ uint32_t target_mask(uint32_t tb, uint32_t n_targets) {
+  if (tb >= n_targets) return 0u;
+  const uint32_t r = n_targets - tb;
+  return r >= 32u ? ~0u : ((1u << r) - 1u);
+}
+
+__global__ void k_init_planes(const InitParams p) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= p.L) return;
+  const uint32_t nl = g / p.BL, b = g - nl * p.BL;
+  const uint32_t tb = p.t0 + 32u * b;
+  const uint32_t live = p.mode == 0 ? 0u : target_mask(tb, p.n_targets);
+  const uint32_t acc = init_accept_block(p.seed, p.mode, p.param, p.n0 + nl, tb) & live;
+  St s;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    s.V[i] = 0u;
+    s.C[i] = ~live;
+    s.K[i] = 0u;
+  }
+  s.K[7] = ~live;
+  s.A = acc;
+  store_state(p.planes, g, s);
+}
+
+__global__ void k_init_pref(const InitParams p) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)p.n_nodes * p.BL) return;
+  const uint32_t node = (uint32_t)(i / p.BL), b = (uint32_t)(i - (size_t)node * p.BL);
+  const uint32_t tb = p.t0 + 32u * b;
+  uint32_t v;
+  if (is_byz(p.byz, node))
+    v = byz_pattern(p.round);
+  else
+    v = p.mode == 0 ? 0u : (init_accept_block(p.seed, p.mode, p.param, node, tb) & target_mask(tb, p.n_targets));
+  p.pref[i] = v;
+}
+
+__global__ void k_byz(uint32_t* byz, uint32_t n_nodes, uint64_t seed, uint32_t threshold) {
+  const uint32_t wi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (wi >= (n_nodes + 31u) / 32u) return;
+  uint32_t bits = 0;
+  for (uint32_t i = 0; i < 32u; ++i) {
+    const uint32_t node = wi * 32u + i;
+    if (node >= n_nodes) break;
+    uint32_t x[4];
+    philox(x, seed, node, 0u, 0u, kDomByz);
+    bits |= (x[0] < threshold ? 1u : 0u) << i;
+  }
+  byz[wi] = bits;
+}
+
+__global__ void k_read_records(const uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0,
+                               uint32_t tl1, uint32_t* out) {
+  const uint32_t W = tl1 - tl0;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)(nl1 - nl0) * W) return;
+  const uint32_t nl = nl0 + (uint32_t)(i / W), tl = tl0 + (uint32_t)(i % W);
+  const uint32_t g = nl * BL + (tl >> 5), bit = tl & 31u;
+  const uint32_t* t = tile_base(planes, g);
+  const uint32_t a = (t[kPA * 64] >> bit) & 1u;
+  if ((t[(kPK + 7) * 64] >> bit) & 1u) {
+    out[i] = 0xFFFE0000u | (a << 16);
+    return;
+  }
+  uint32_t v = 0, c = 0, k = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    v |= ((t[(kPV + q) * 64] >> bit) & 1u) << q;
+    c |= ((t[(kPC + q) * 64] >> bit) & 1u) << q;
+  }
+#pragma unroll
+  for (int q = 0; q < 7; ++q) k |= ((t[(kPK + q) * 64] >> bit) & 1u) << q;
+  out[i] = v | (c << 8) | (((k << 1) | a) << 16);
+}
+
+__global__ void k_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0,
+                                uint32_t tl1, const uint32_t* in) {
+  const uint32_t b0 = tl0 >> 5, b1 = (tl1 + 31u) >> 5, NB = b1 - b0, W = tl1 - tl0;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (nl1 - nl0) * NB) return;
+  const uint32_t nl = nl0 + i / NB, b = b0 + i % NB;
+  const uint32_t g = nl * BL + b;
+  St s;
+  load_state(planes, g, s);
+  for (uint32_t bit = 0; bit < 32u; ++bit) {
+    const uint32_t tl = b * 32u + bit;
+    if (tl < tl0 || tl >= tl1) continue;
+    const uint32_t w = in[(size_t)(nl - nl0) * W + (tl - tl0)];
+    const uint32_t m = 1u << bit;
+    const uint32_t conf = w >> 16;
+    const bool live = (conf >> 1) < 128u;
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t vb = live ? (w >> q) & 1u : 0u;
+      const uint32_t cb = live ? (w >> (8 + q)) & 1u : 1u;
+      const uint32_t kb = live ? ((conf >> 1) >> q) & 1u : (q == 7 ? 1u : 0u);
+      s.V[q] = (s.V[q] & ~m) | (vb << bit);
+      s.C[q] = (s.C[q] & ~m) | (cb << bit);
+      s.K[q] = (s.K[q] & ~m) | (kb << bit);
+    }
+    s.A = (s.A & ~m) | ((conf & 1u) << bit);
+  }
+  store_state(planes, g, s);
+}
+
+__global__ void k_refresh_pref(const uint32_t* planes, uint32_t* pref, const uint32_t* byz, uint32_t n0, uint32_t NL,
+                               uint32_t BL, uint32_t round) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= NL * BL) return;
+  const uint32_t nl = g / BL, b = g - nl * BL, node = n0 + nl;
+  pref[(size_t)node * BL + b] = is_byz(byz, node) ? byz_pattern(round) : tile_base(planes, g)[kPA * 64];
+}
+
+template <int K>
+__global__ void k_sample_peers(uint64_t seed, uint32_t n_nodes, uint32_t a, uint32_t b, uint32_t round, int mode,
+                               uint32_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (a + i >= b) return;
+  uint32_t peers[K];
+  sample_peers<K>(seed, a + i, round, n_nodes, mode, peers);
+#pragma unroll
+  for (int j = 0; j < K; ++j) out[(size_t)i * K + j] = peers[j];
+}
+
+// Synthetic replayed vote stream (C2): class per (node, round, slot, target)
+// from philox(node, round, t>>1, REPLAY | slot<<8); same definition as
+// avo_replay_err in the oracle. Output planes [slot][yes|consider][Lpad].
+__global__ void k_gen_replay(uint64_t seed, uint32_t n0, uint32_t BL, uint32_t L, uint32_t Lpad, uint32_t t0,
+                             uint32_t n_targets, uint32_t round, int k, uint32_t* out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= Lpad) return;
+  if (g >= L) {
+    for (int s = 0; s < k; ++s) {
+      out[(size_t)(2 * s) * Lpad + g] = 0u;
+      out[(size_t)(2 * s + 1) * Lpad + g] = 0u;
+    }
+    return;
+  }
+  const uint32_t nl = g / BL, b = g - nl * BL, node = n0 + nl;
+  const uint32_t tb = t0 + 32u * b;
+  const uint32_t tm = target_mask(tb, n_targets);
+  for (int s = 0; s < k; ++s) {
+    uint32_t y = 0, c = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      uint32_t x[4];
+      philox(x, seed, node, round, (tb >> 1) + q, kDomReplay | ((uint32_t)s << 8));
+      const uint32_t v0 = x[0], v1 = x[2];
+      y |= (v0 < kReplayYes ? 1u : 0u) << (2 * q);
+      c |= (v0 < kReplayNo ? 1u : 0u) << (2 * q);
+      y |= (v1 < kReplayYes ? 1u : 0u) << (2 * q + 1);
+      c |= (v1 < kReplayNo ? 1u : 0u) << (2 * q + 1);
+    }
+    out[(size_t)(2 * s) * Lpad + g] = y & tm;
+    out[(size_t)(2 * s + 1) * Lpad + g] = c & tm;
+  }
+}
+
+__global__ void k_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets, uint32_t log_cap,
+                              uint64_t* out) {
+  const uint32_t shard = blockIdx.x;
+  const uint32_t n = min(counts[shard], log_cap);
+  const uint64_t* src = log + (size_t)shard * log_cap;
+  uint64_t* dst = out + offsets[shard];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+template <int K>
+hipError_t launch_round_k(const RoundParams& p, bool replay, bool capped, hipStream_t s) {
+  if (capped) {
+    const uint32_t bt = ((p.BL + 63u) / 64u) * 64u;
+    if (replay)
+      hipLaunchKernelGGL((k_round_capped<K, true>), dim3(p.NL), dim3(bt), 0, s, p);
+    else
+      hipLaunchKernelGGL((k_round_capped<K, false>), dim3(p.NL), dim3(bt), 0, s, p);
+  } else {
+    const uint32_t blocks = (p.Lpad + 255u) / 256u;
+    if (replay)
+      hipLaunchKernelGGL((k_round_fast<K, true>), dim3(blocks), dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((k_round_fast<K, false>), dim3(blocks), dim3(256), 0, s, p);
+  }
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_sample_k(uint64_t seed, uint32_t n_nodes, uint32_t a, uint32_t b, uint32_t round, int mode,
+                           uint32_t* out, hipStream_t s) {
+  const uint32_t n = b - a;
+  hipLaunchKernelGGL((k_sample_peers<K>), dim3((n + 255) / 256), dim3(256), 0, s, seed, n_nodes, a, b, round, mode,
+                     out);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+#define AVK_K_SWITCH(k, CALL) \
+  switch (k) {                \
+    case 1: return CALL(1);   \
+    case 2: return CALL(2);   \
+    case 3: return CALL(3);   \
+    case 4: return CALL(4);   \
+    case 5: return CALL(5);   \
+    case 6: return CALL(6);   \
+    case 7: return CALL(7);   \
+    case 8: return CALL(8);   \
+    case 9: return CALL(9);   \
+    case 10: return CALL(10); \
+    case 11: return CALL(11); \
+    case 12: return CALL(12); \
+    case 13: return CALL(13); \
+    case 14: return CALL(14); \
+    case 15: return CALL(15); \
+    case 16: return CALL(16); \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t launch_round(const RoundParams& p, int k, bool replay, bool capped, hipStream_t s) {
+#define AVK_ROUND(K) launch_round_k<K>(p, replay, capped, s)
+  AVK_K_SWITCH(k, AVK_ROUND)
+#undef AVK_ROUND
+}
+
+hipError_t launch_sample_peers(uint64_t seed, uint32_t n_nodes, uint32_t a, uint32_t b, uint32_t round, int k,
+                               int mode, uint32_t* out, hipStream_t s) {
+  if (b <= a) return hipSuccess;
+#define AVK_SAMPLE(K) launch_sample_k<K>(seed, n_nodes, a, b, round, mode, out, s)
+  AVK_K_SWITCH(k, AVK_SAMPLE)
+#undef AVK_SAMPLE
+}
+
+hipError_t launch_init(const InitParams& p, hipStream_t s) {
+  if (p.L) hipLaunchKernelGGL(k_init_planes, dim3((p.L + 255) / 256), dim3(256), 0, s, p);
+  const size_t rows = (size_t)p.n_nodes * p.BL;
+  if (rows) hipLaunchKernelGGL(k_init_pref, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_byz(uint32_t* byz, uint32_t n_nodes, uint64_t seed, uint32_t threshold, hipStream_t s) {
+  const uint32_t words = (n_nodes + 31u) / 32u;
+  hipLaunchKernelGGL(k_byz, dim3((words + 255) / 256), dim3(256), 0, s, byz, n_nodes, seed, threshold);
+  return hipGetLastError();
+}
+
+hipError_t launch_register_votes(const DropInParams& p, hipStream_t s) {
+  if (!p.n_blocks) return hipSuccess;
+  hipLaunchKernelGGL(k_register_votes, dim3((p.n_blocks + 63) / 64), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_add_targets(const AddParams& p, hipStream_t s) {
+  if (!p.n) return hipSuccess;
+  hipLaunchKernelGGL(k_add_targets, dim3(1), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_read_records(const uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0,
+                               uint32_t tl1, uint32_t* out, hipStream_t s) {
+  const size_t n = (size_t)(nl1 - nl0) * (tl1 - tl0);
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_read_records, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, planes, BL, nl0, nl1, tl0,
+                     tl1, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0, uint32_t tl1,
+                                const uint32_t* in, hipStream_t s) {
+  const uint32_t nb = ((tl1 + 31u) >> 5) - (tl0 >> 5);
+  const uint32_t n = (nl1 - nl0) * nb;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_write_records, dim3((n + 255) / 256), dim3(256), 0, s, planes, BL, nl0, nl1, tl0, tl1, in);
+  return hipGetLastError();
+}
+
+hipError_t launch_refresh_pref(const uint32_t* planes, uint32_t* pref, const uint32_t* byz, uint32_t n0, uint32_t NL,
+                               uint32_t BL, uint32_t round, hipStream_t s) {
+  const uint32_t n = NL * BL;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_refresh_pref, dim3((n + 255) / 256), dim3(256), 0, s, planes, pref, byz, n0, NL, BL, round);
+  return hipGetLastError();
+}
+
+hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t BL, uint32_t L, uint32_t Lpad,
+                             uint32_t t0, uint32_t n_targets, uint32_t round, int k, uint32_t* out, hipStream_t s) {
+  (void)NL;
+  if (!Lpad) return hipSuccess;
+  hipLaunchKernelGGL(k_gen_replay, dim3((Lpad + 255) / 256), dim3(256), 0, s, seed, n0, BL, L, Lpad, t0, n_targets,
+                     round, k, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets, uint32_t log_cap,
+                              uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_compact_log, dim3(kLogShards), dim3(256), 0, s, log, counts, offsets, log_cap, out);
+  return hipGetLastError();
+}
+
+}  // namespace avk

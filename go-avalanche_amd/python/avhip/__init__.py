@@ -1,0 +1,334 @@
+"""ctypes binding of libavhip.so (include/avhip.h) — the MI355X batched
+Avalanche voting engine.
+
+This is a thin host-side mirror of the C ABI used by bench.py and the tests.
+It never falls back to anything else: if libavhip.so cannot be loaded, or a
+call fails, an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+try:  # share torch's HIP runtime (same soname) when torch is present
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the binding itself
+    torch = None
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libavhip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_PKG_ROOT), "include", "avhip.h")
+
+AV_OK = 0
+AV_ERR_NOT_FOUND = -4
+AV_ERR_OVERFLOW = -5
+
+STATUS_INVALID, STATUS_REJECTED, STATUS_ACCEPTED, STATUS_FINALIZED = 0, 1, 2, 3
+PEERS_RANDOM, PEERS_ROUND_ROBIN = 0, 1
+INIT_NONE, INIT_REJECTED, INIT_ACCEPTED, INIT_BERNOULLI, INIT_PAIRS = 0, 1, 2, 3, 4
+ABSENT_WORD = 0xFFFE0000
+FINALIZATION_SCORE = 128
+MAX_ELEMENT_POLL = 4096
+
+
+class AvError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"avhip error {code}: {msg}")
+        self.code = code
+
+
+class VoteRecordNotFound(AvError):
+    """The reference panics with "VoteRecord not found" (processor.go:136)."""
+
+
+class LogOverflow(AvError):
+    pass
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_int64),
+        ("n_targets", C.c_int64),
+        ("k", C.c_int32),
+        ("peer_mode", C.c_int32),
+        ("seed", C.c_uint64),
+        ("byz_threshold", C.c_uint32),
+        ("device", C.c_int32),
+        ("node_begin", C.c_int64),
+        ("node_end", C.c_int64),
+        ("target_begin", C.c_int64),
+        ("target_end", C.c_int64),
+        ("update_log_capacity", C.c_int64),
+    ]
+
+
+# every symbol declared in include/avhip.h (non-inline)
+EXPORTED = [
+    "av_abi_version", "av_config_init", "av_create", "av_destroy", "av_strerror", "av_last_error",
+    "av_init_records", "av_add_targets", "av_set_valid", "av_register_votes", "av_is_accepted",
+    "av_get_confidence", "av_get_invs", "av_run_rounds", "av_replay_round_errs", "av_replay_prepare",
+    "av_replay_rounds", "av_synchronize", "av_round_index", "av_updates_count", "av_fetch_updates",
+    "av_applied_votes", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
+    "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
+]
+
+_lib = None
+_vp = C.c_void_p
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"libavhip.so not built at {LIB_PATH} (run __graft_entry__.build() or make -C go-avalanche_amd)")
+    L = C.CDLL(LIB_PATH)
+    i64, i32, u32 = C.c_int64, C.c_int32, C.c_uint32
+    P = C.POINTER
+    sig = {
+        "av_abi_version": (i32, []),
+        "av_config_init": (None, [P(Config)]),
+        "av_create": (i32, [P(Config), P(_vp)]),
+        "av_destroy": (i32, [_vp]),
+        "av_strerror": (C.c_char_p, [i32]),
+        "av_last_error": (C.c_char_p, []),
+        "av_init_records": (i32, [_vp, i32, u32]),
+        "av_add_targets": (i32, [_vp, i64, _vp, _vp, i64, _vp]),
+        "av_set_valid": (i32, [_vp, i64, i32]),
+        "av_register_votes": (i32, [_vp, i64, _vp, _vp, i64, _vp]),
+        "av_is_accepted": (i32, [_vp, i64, i64, P(i32)]),
+        "av_get_confidence": (i32, [_vp, i64, i64, P(C.c_uint16)]),
+        "av_get_invs": (i32, [_vp, i64, _vp, i64, P(i64)]),
+        "av_run_rounds": (i32, [_vp, i32]),
+        "av_replay_round_errs": (i32, [_vp, _vp]),
+        "av_replay_prepare": (i32, [_vp, i32]),
+        "av_replay_rounds": (i32, [_vp, i32]),
+        "av_synchronize": (i32, [_vp]),
+        "av_round_index": (i32, [_vp, P(i64)]),
+        "av_updates_count": (i32, [_vp, P(i64)]),
+        "av_fetch_updates": (i32, [_vp, _vp, i64, P(i64)]),
+        "av_applied_votes": (i32, [_vp, P(i64)]),
+        "av_read_records": (i32, [_vp, i64, i64, i64, i64, _vp]),
+        "av_write_records": (i32, [_vp, i64, i64, i64, i64, _vp]),
+        "av_read_pref": (i32, [_vp, i64, i64, i64, i64, _vp]),
+        "av_sample_peers": (i32, [_vp, i64, i64, i64, _vp]),
+        "av_set_timing": (i32, [_vp, i32]),
+        "av_kernel_stats": (i32, [_vp, P(C.c_double), P(i64)]),
+        "av_layout_info": (i32, [_vp, P(i64), P(i64), P(i64), P(i32)]),
+        "av_comm_unique_id": (i32, [_vp]),
+        "av_comm_init": (i32, [_vp, i32, i32, _vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc == AV_OK:
+        return
+    msg = lib().av_last_error().decode(errors="replace")
+    if rc == AV_ERR_NOT_FOUND:
+        raise VoteRecordNotFound(rc, msg)
+    if rc == AV_ERR_OVERFLOW:
+        raise LogOverflow(rc, msg)
+    raise AvError(rc, msg)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_vp)
+
+
+def decode_updates(u: np.ndarray, base_round: int = 0) -> np.ndarray:
+    """Packed update words -> int64[n, 5] (round, node, slot, target, status)."""
+    u = np.asarray(u, np.uint64)
+    out = np.empty((u.size, 5), np.int64)
+    out[:, 0] = (u >> np.uint64(52)).astype(np.int64) + base_round
+    out[:, 1] = ((u >> np.uint64(28)) & np.uint64(0xFFFFFF)).astype(np.int64)
+    out[:, 2] = ((u >> np.uint64(24)) & np.uint64(0xF)).astype(np.int64)
+    out[:, 3] = ((u >> np.uint64(2)) & np.uint64(0x3FFFFF)).astype(np.int64)
+    out[:, 4] = (u & np.uint64(3)).astype(np.int64)
+    return out
+
+
+def comm_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    _check(lib().av_comm_unique_id(C.cast(buf, _vp)))
+    return bytes(buf)
+
+
+class Engine:
+    """One engine = N nodes x M targets of VoteRecords (or a shard) in HBM."""
+
+    def __init__(self, n_nodes, n_targets, k=8, seed=0xA7A1A9C4, peer_mode=PEERS_RANDOM, byz_threshold=0,
+                 device=0, node_range=None, target_range=None, log_capacity=0):
+        cfg = Config()
+        lib().av_config_init(C.byref(cfg))
+        cfg.n_nodes, cfg.n_targets, cfg.k = n_nodes, n_targets, k
+        cfg.peer_mode, cfg.seed, cfg.byz_threshold, cfg.device = peer_mode, seed, byz_threshold, device
+        if node_range is not None:
+            cfg.node_begin, cfg.node_end = node_range
+        if target_range is not None:
+            cfg.target_begin, cfg.target_end = target_range
+        cfg.update_log_capacity = log_capacity
+        h = _vp()
+        _check(lib().av_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.n_nodes, self.n_targets, self.k = n_nodes, n_targets, k
+        self.node_range = (cfg.node_begin, cfg.node_end) if node_range else (0, n_nodes)
+        self.target_range = (cfg.target_begin, cfg.target_end) if target_range else (0, n_targets)
+        self._log_base = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().av_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- population ----
+    def init_records(self, mode=INIT_BERNOULLI, param=0x80000000):
+        _check(lib().av_init_records(self._h, mode, param))
+
+    def add_targets(self, node, targets, accepted):
+        t = np.ascontiguousarray(targets, np.int64)
+        a = np.ascontiguousarray(accepted, np.uint8)
+        out = np.zeros(max(1, t.size), np.uint8)
+        _check(lib().av_add_targets(self._h, node, _ptr(t), _ptr(a), t.size, _ptr(out)))
+        return out[: t.size].astype(bool)
+
+    def set_valid(self, target, valid):
+        _check(lib().av_set_valid(self._h, target, int(bool(valid))))
+
+    # ---- one-node Processor methods ----
+    def register_votes(self, node, targets, errs):
+        t = np.ascontiguousarray(targets, np.int64)
+        e = np.ascontiguousarray(errs, np.uint32)
+        st = np.zeros(max(1, t.size), np.int32)
+        _check(lib().av_register_votes(self._h, node, _ptr(t), _ptr(e), t.size, _ptr(st)))
+        return st[: t.size]
+
+    def is_accepted(self, node, target):
+        out = C.c_int32(0)
+        _check(lib().av_is_accepted(self._h, node, target, C.byref(out)))
+        return bool(out.value)
+
+    def get_confidence(self, node, target):
+        out = C.c_uint16(0)
+        _check(lib().av_get_confidence(self._h, node, target, C.byref(out)))
+        return out.value
+
+    def get_invs(self, node):
+        buf = np.zeros(MAX_ELEMENT_POLL, np.int64)
+        n = C.c_int64(0)
+        _check(lib().av_get_invs(self._h, node, _ptr(buf), buf.size, C.byref(n)))
+        return buf[: n.value].copy()
+
+    # ---- rounds ----
+    def run_rounds(self, rounds=1):
+        _check(lib().av_run_rounds(self._h, rounds))
+
+    def replay_round_errs(self, errs):
+        e = np.ascontiguousarray(errs, np.uint32)
+        nl = self.node_range[1] - self.node_range[0]
+        tl = self.target_range[1] - self.target_range[0]
+        assert e.shape == (nl, self.k, tl), e.shape
+        _check(lib().av_replay_round_errs(self._h, _ptr(e)))
+
+    def replay_prepare(self, rounds):
+        _check(lib().av_replay_prepare(self._h, rounds))
+
+    def replay_rounds(self, rounds):
+        _check(lib().av_replay_rounds(self._h, rounds))
+
+    def synchronize(self):
+        _check(lib().av_synchronize(self._h))
+
+    @property
+    def round(self):
+        out = C.c_int64(0)
+        _check(lib().av_round_index(self._h, C.byref(out)))
+        return out.value
+
+    # ---- outputs ----
+    def updates_count(self):
+        out = C.c_int64(0)
+        _check(lib().av_updates_count(self._h, C.byref(out)))
+        return out.value
+
+    def fetch_updates(self, decode=True):
+        """All StatusUpdates since the previous fetch in canonical order."""
+        n = self.updates_count()
+        buf = np.zeros(max(1, n), np.uint64)
+        got = C.c_int64(0)
+        base = self._log_base
+        _check(lib().av_fetch_updates(self._h, _ptr(buf), buf.size, C.byref(got)))
+        self._log_base = self.round
+        buf = buf[: got.value]
+        return decode_updates(buf, base) if decode else buf
+
+    def applied_votes(self):
+        out = C.c_int64(0)
+        _check(lib().av_applied_votes(self._h, C.byref(out)))
+        return out.value
+
+    def read_records(self, n0=None, n1=None, t0=None, t1=None):
+        n0 = self.node_range[0] if n0 is None else n0
+        n1 = self.node_range[1] if n1 is None else n1
+        t0 = self.target_range[0] if t0 is None else t0
+        t1 = self.target_range[1] if t1 is None else t1
+        out = np.zeros((n1 - n0, t1 - t0), np.uint32)
+        _check(lib().av_read_records(self._h, n0, n1, t0, t1, _ptr(out)))
+        return out
+
+    def write_records(self, words, n0=None, t0=None):
+        w = np.ascontiguousarray(words, np.uint32)
+        n0 = self.node_range[0] if n0 is None else n0
+        t0 = self.target_range[0] if t0 is None else t0
+        _check(lib().av_write_records(self._h, n0, n0 + w.shape[0], t0, t0 + w.shape[1], _ptr(w)))
+
+    def read_pref(self, n0=0, n1=None, t0=None, t1=None):
+        n1 = self.n_nodes if n1 is None else n1
+        t0 = self.target_range[0] if t0 is None else t0
+        t1 = self.target_range[1] if t1 is None else t1
+        out = np.zeros((n1 - n0, t1 - t0), np.uint8)
+        _check(lib().av_read_pref(self._h, n0, n1, t0, t1, _ptr(out)))
+        return out
+
+    def sample_peers(self, rnd, n0=0, n1=None):
+        n1 = self.n_nodes if n1 is None else n1
+        out = np.zeros((n1 - n0, self.k), np.int32)
+        _check(lib().av_sample_peers(self._h, rnd, n0, n1, _ptr(out)))
+        return out
+
+    # ---- measurement ----
+    def set_timing(self, enable=True):
+        _check(lib().av_set_timing(self._h, int(enable)))
+
+    def kernel_stats(self):
+        ms, n = C.c_double(0), C.c_int64(0)
+        _check(lib().av_kernel_stats(self._h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def layout_info(self):
+        lanes, nl, bl, capped = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int32()
+        _check(lib().av_layout_info(self._h, C.byref(lanes), C.byref(nl), C.byref(bl), C.byref(capped)))
+        return {"lanes": lanes.value, "local_nodes": nl.value, "local_blocks": bl.value, "capped": bool(capped.value)}
+
+    def comm_init(self, world, rank, uid: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _check(lib().av_comm_init(self._h, world, rank, C.cast(buf, _vp)))

@@ -1,0 +1,179 @@
+/*
+ * avhip.h — C ABI of libavhip.so, the MI355X-native batched Avalanche voting
+ * engine (drop-in for go-avalanche's Processor/VoteRecord hot path).
+ *
+ * One engine = the VoteRecord state of a network of N simulated nodes x M
+ * targets (or one shard of it) held in HBM. Every function is plain C: opaque
+ * handle, plain pointers and sizes, int status codes, caller-owned host
+ * buffers that are not retained after the call returns (the cgo rule).
+ * Calls on one handle must be serialized by the caller (the reference
+ * Processor is not thread-safe either: processor.go:12-25, main.go:101,122,135).
+ *
+ * Reference interfaces replaced (itsdevbear/go-avalanche):
+ *   av_add_targets      <- (*Processor).AddTargetToReconcile   processor.go:45-58
+ *   av_register_votes   <- (*Processor).RegisterVotes           processor.go:61-122
+ *   av_is_accepted      <- (*Processor).IsAccepted              processor.go:125-130
+ *   av_get_confidence   <- (*Processor).GetConfidence           processor.go:133-140
+ *   av_get_invs         <- (*Processor).GetInvsForNextPoll      processor.go:144-170
+ *   av_round_index      <- (*Processor).GetRound                processor.go:40-42
+ *   av_set_valid        <- Target.IsValid / isWorthyPolling     avalanche.go:89-90, processor.go:185-187
+ *   av_run_rounds       <- the example's poll loop for every node at once
+ *                          (main.go:110-137 + responder main.go:168-192,
+ *                          peers from getSuitableNodeToQuery processor.go:173-182
+ *                          / Connman.NodesIDs net.go:25-31 replaced by
+ *                          counter-RNG k-peer sampling)
+ *   av_fetch_updates    <- the *[]StatusUpdate out-parameter     processor.go:61,111
+ */
+#ifndef AVHIP_H
+#define AVHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVHIP_ABI_VERSION 1
+
+/* return codes */
+#define AV_OK 0
+#define AV_ERR_INVALID_ARG (-1)
+#define AV_ERR_HIP (-2)
+#define AV_ERR_OOM (-3)
+#define AV_ERR_NOT_FOUND (-4)   /* GetConfidence's panic("VoteRecord not found") */
+#define AV_ERR_OVERFLOW (-5)    /* update log or caller buffer too small */
+#define AV_ERR_UNSUPPORTED (-6)
+#define AV_ERR_RCCL (-7)
+
+/* Status (avalanche.go:42-56, iota order) */
+#define AV_STATUS_INVALID 0
+#define AV_STATUS_REJECTED 1
+#define AV_STATUS_ACCEPTED 2
+#define AV_STATUS_FINALIZED 3
+
+#define AV_FINALIZATION_SCORE 128  /* avalanche.go:10 */
+#define AV_MAX_ELEMENT_POLL 4096   /* avalanche.go:17 */
+
+/* peer selection for av_run_rounds */
+#define AV_PEERS_RANDOM 0      /* k distinct uniform peers != self, Philox4x32-10 */
+#define AV_PEERS_ROUND_ROBIN 1 /* the example's i % N skipping self (main.go:110-116) */
+
+/* bulk population for av_init_records */
+#define AV_INIT_NONE 0      /* no records; add them with av_add_targets */
+#define AV_INIT_REJECTED 1  /* every node adds every target, IsAccepted() = false */
+#define AV_INIT_ACCEPTED 2  /* ... IsAccepted() = true */
+#define AV_INIT_BERNOULLI 3 /* IsAccepted() = philox(node, t) < init_param */
+#define AV_INIT_PAIRS 4     /* double-spend pairs (2p, 2p+1), complementary per node */
+
+/* Canonical record word used by av_read_records / av_write_records:
+ *   live record : votes | consider << 8 | confidence << 16  (vote.go:25-29,
+ *                 confidence >> 1 < 128)
+ *   no record   : 0xFFFE0000 | decision << 16  (deleted after finalization,
+ *                 processor.go:114-116, or never added; decision = 1 iff the
+ *                 record finalized accepted) */
+#define AV_ABSENT_WORD 0xFFFE0000u
+
+typedef struct av_engine av_engine;
+
+typedef struct {
+  int64_t n_nodes;       /* N, whole network */
+  int64_t n_targets;     /* M, whole network (target slots 0..M-1) */
+  int32_t k;             /* polls (Responses) per node per round, 1..16 */
+  int32_t peer_mode;     /* AV_PEERS_* */
+  uint64_t seed;         /* Philox key for peers / Byzantine set / init */
+  uint32_t byz_threshold;/* node j Byzantine iff philox(j) < threshold (0 = none) */
+  int32_t device;        /* HIP device ordinal */
+  int64_t node_begin;    /* this engine's node shard [node_begin, node_end) */
+  int64_t node_end;      /*   (0,0 = all nodes) */
+  int64_t target_begin;  /* this engine's target shard [target_begin, target_end), */
+  int64_t target_end;    /*   begin a multiple of 32 (0,0 = all targets) */
+  int64_t update_log_capacity; /* device StatusUpdate log entries (0 = default) */
+} av_config;
+
+/* Packed StatusUpdate as returned by av_fetch_updates (uint64):
+ *   [63:52] round - round of the previous fetch | [51:28] node |
+ *   [27:24] slot (poll index within the round)  | [23:2] target | [1:0] status
+ * Sorted ascending == (round, node, slot, target) == reference append order. */
+static inline int64_t av_update_round_rel(uint64_t u) { return (int64_t)(u >> 52); }
+static inline int64_t av_update_node(uint64_t u) { return (int64_t)((u >> 28) & 0xFFFFFFu); }
+static inline int32_t av_update_slot(uint64_t u) { return (int32_t)((u >> 24) & 0xFu); }
+static inline int64_t av_update_target(uint64_t u) { return (int64_t)((u >> 2) & 0x3FFFFFu); }
+static inline int32_t av_update_status(uint64_t u) { return (int32_t)(u & 3u); }
+
+/* ---- lifecycle ---- */
+int av_abi_version(void);
+void av_config_init(av_config* cfg);
+int av_create(const av_config* cfg, av_engine** out);
+int av_destroy(av_engine* e);
+const char* av_strerror(int code);
+const char* av_last_error(void); /* thread-local detail of the last failure */
+
+/* ---- population (processor.go:45-58) ---- */
+int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param);
+/* AddTargetToReconcile for targets[0..n) of one node, in order;
+ * added[i] = 1 iff a record was created (false if !IsValid or live record). */
+int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uint8_t* accepted, int64_t n,
+                   uint8_t* added);
+/* Target.IsValid() of a target for every node (isWorthyPolling). */
+int av_set_valid(av_engine* e, int64_t target, int32_t valid);
+
+/* ---- one-node Processor methods (drop-in path) ---- */
+/* RegisterVotes: votes (targets[i], errs[i]) applied in order. status_out[i] =
+ * Status of the StatusUpdate that vote appended, or -1 if none. Unknown
+ * targets (< 0 or >= M) and targets outside this shard are skipped as the
+ * reference skips unknown hashes. Always returns AV_OK on valid input
+ * (RegisterVotes returns true: processor.go:121). */
+int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const uint32_t* errs, int64_t n,
+                      int32_t* status_out);
+int av_is_accepted(av_engine* e, int64_t node, int64_t target, int32_t* out);
+/* AV_ERR_NOT_FOUND where the reference panics "VoteRecord not found". */
+int av_get_confidence(av_engine* e, int64_t node, int64_t target, uint16_t* out);
+/* Live valid targets in ascending index, truncated to 4096. */
+int av_get_invs(av_engine* e, int64_t node, int64_t* out_targets, int64_t cap, int64_t* n_out);
+
+/* ---- batched rounds: the hot path ---- */
+/* Enqueue `rounds` synchronous rounds: each node polls
+ * k peers; votes = peers' round-start published preference. Asynchronous. */
+int av_run_rounds(av_engine* e, int32_t rounds);
+/* One replayed round: errs is a HOST array [local nodes][k][local targets]
+ * of err words (vote.go:55-56 classes), consumed for the polled targets. */
+int av_replay_round_errs(av_engine* e, const uint32_t* errs);
+/* Synthetic replayed stream (C2 workload): generate the vote classes of the
+ * next `rounds` rounds on the device (avo_replay_err definition) ... */
+int av_replay_prepare(av_engine* e, int32_t rounds);
+/* ... and consume them (asynchronous). */
+int av_replay_rounds(av_engine* e, int32_t rounds);
+int av_synchronize(av_engine* e);
+int av_round_index(av_engine* e, int64_t* out);
+
+/* ---- outputs ---- */
+int av_updates_count(av_engine* e, int64_t* n);
+/* All StatusUpdates since the previous fetch, sorted canonical; clears the
+ * log. AV_ERR_OVERFLOW if the device log or `cap` overflowed (*n_out holds the
+ * required count when cap is too small). */
+int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out);
+/* Number of regsiterVote applications (vote.go:54) since creation. */
+int av_applied_votes(av_engine* e, int64_t* out);
+/* Canonical words for local nodes [n0,n1) x targets [t0,t1) (global ids). */
+int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint32_t* out);
+int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, const uint32_t* in);
+/* Round-start published preference (0/1) for nodes [n0,n1) x targets [t0,t1). */
+int av_read_pref(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint8_t* out);
+/* Device peer sampling dump: peers of nodes [n0,n1) in round `round`, [n][k]. */
+int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t* out);
+
+/* ---- measurement ---- */
+/* HIP-event timing of every round kernel launch on the engine stream. */
+int av_set_timing(av_engine* e, int32_t enable);
+int av_kernel_stats(av_engine* e, double* total_ms, int64_t* launches);
+/* Bytes per round of the round kernel's algorithmic traffic. */
+int av_layout_info(av_engine* e, int64_t* lanes, int64_t* local_nodes, int64_t* local_blocks, int32_t* capped);
+
+/* ---- multi-GPU (node-sharded engines exchange preferences over RCCL) ---- */
+int av_comm_unique_id(uint8_t out[128]);
+int av_comm_init(av_engine* e, int32_t world, int32_t rank, const uint8_t id[128]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

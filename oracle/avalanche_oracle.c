@@ -1,0 +1,479 @@
+/*
+ * avalanche_oracle.c — TEST INFRASTRUCTURE ONLY. See avalanche_oracle.h.
+ *
+ * Straight, per-record restatement of the reference semantics. Nothing here
+ * is bit-sliced or batched: every function follows the Go code it cites line
+ * by line so that it can serve as the parity checker for the HIP engine.
+ */
+#include "avalanche_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Philox4x32-10: round function and Weyl key schedule as published with   */
+/* Random123 (multipliers 0xD2511F53 / 0xCD9E8D57, bumps 0x9E3779B9 /       */
+/* 0xBB67AE85). Pinned by the Random123 known-answer vectors in tests/.    */
+/* ------------------------------------------------------------------------ */
+void avo_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    uint32_t n1 = (uint32_t)p1;
+    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    uint32_t n3 = (uint32_t)p0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static void philox_dom(uint64_t seed, uint32_t a, uint32_t b, uint32_t c, uint32_t dom, uint32_t out[4]) {
+  uint32_t ctr[4] = {a, b, c, dom};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  avo_philox4x32_10(ctr, key, out);
+}
+
+/* ------------------------------------------------------------------------ */
+/* VoteRecord — vote.go                                                      */
+/* ------------------------------------------------------------------------ */
+
+/* vote.go:93-98 countBits8 (Kernighan loop, kept literal) */
+static int count_bits8(uint8_t i) {
+  int count = 0;
+  for (; i > 0; i &= (uint8_t)(i - 1)) count++;
+  return count;
+}
+
+/* vote.go:33-35 NewVoteRecord: confidence = boolToUint16(accepted) */
+avo_vote_record avo_new_vote_record(int accepted) {
+  avo_vote_record vr;
+  vr.votes = 0;
+  vr.consider = 0;
+  vr.confidence = accepted ? 1 : 0;
+  return vr;
+}
+
+/* vote.go:38-40 */
+int avo_is_accepted_rec(const avo_vote_record* vr) { return (vr->confidence & 0x01) == 1; }
+/* vote.go:43-45 */
+uint16_t avo_get_confidence_rec(const avo_vote_record* vr) { return (uint16_t)(vr->confidence >> 1); }
+/* vote.go:48-50 */
+int avo_has_finalized(const avo_vote_record* vr) {
+  return avo_get_confidence_rec(vr) >= AVO_FINALIZATION_SCORE;
+}
+
+/* vote.go:54-75 regsiterVote */
+int avo_register_vote(avo_vote_record* vr, uint32_t err) {
+  /* :55-56 — u8 shift with wrap; neutral = int32(err) < 0 */
+  vr->votes = (uint8_t)((uint8_t)(vr->votes << 1) | (err == 0 ? 1 : 0));
+  vr->consider = (uint8_t)((uint8_t)(vr->consider << 1) | ((int32_t)err >= 0 ? 1 : 0));
+
+  /* :58 */
+  int yes = count_bits8((uint8_t)(vr->votes & vr->consider & 0xff)) > 6;
+
+  /* :61-63 — (-votes-1) is ^votes in uint8 arithmetic */
+  uint8_t not_votes = (uint8_t)(-(int)vr->votes - 1);
+  if (!yes && count_bits8((uint8_t)(not_votes & vr->consider & 0xff)) <= 6) {
+    return 0;
+  }
+
+  /* :66-69 */
+  if (avo_is_accepted_rec(vr) == yes) {
+    vr->confidence = (uint16_t)(vr->confidence + 2);
+    return avo_get_confidence_rec(vr) == AVO_FINALIZATION_SCORE;
+  }
+
+  /* :72-74 */
+  vr->confidence = yes ? 1 : 0;
+  return 1;
+}
+
+/* vote.go:77-91 */
+int avo_status(const avo_vote_record* vr) {
+  int finalized = avo_has_finalized(vr);
+  int accepted = avo_is_accepted_rec(vr);
+  if (!finalized && accepted) return AVO_STATUS_ACCEPTED;
+  if (!finalized && !accepted) return AVO_STATUS_REJECTED;
+  if (finalized && accepted) return AVO_STATUS_FINALIZED;
+  return AVO_STATUS_INVALID;
+}
+
+uint32_t avo_pack(avo_vote_record vr) {
+  return (uint32_t)vr.votes | ((uint32_t)vr.consider << 8) | ((uint32_t)vr.confidence << 16);
+}
+
+avo_vote_record avo_unpack(uint32_t w) {
+  avo_vote_record vr;
+  vr.votes = (uint8_t)(w & 0xff);
+  vr.consider = (uint8_t)((w >> 8) & 0xff);
+  vr.confidence = (uint16_t)(w >> 16);
+  return vr;
+}
+
+void avo_transition_batch(const uint32_t* words_in, const uint32_t* errs, int64_t n,
+                          uint32_t* words_out, uint8_t* changed, uint8_t* status) {
+  for (int64_t i = 0; i < n; ++i) {
+    avo_vote_record vr = avo_unpack(words_in[i]);
+    int c = avo_register_vote(&vr, errs[i]);
+    words_out[i] = avo_pack(vr);
+    if (changed) changed[i] = (uint8_t)c;
+    if (status) status[i] = (uint8_t)avo_status(&vr);
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Processor — processor.go. The Go maps keyed by Hash become dense arrays   */
+/* over target slots: present[t] <=> voteRecords[hash] exists.              */
+/* decision[t] remembers the finalized outcome of a deleted record so the   */
+/* harness can publish it (SURVEY.md §8(a) rule R2); the reference itself   */
+/* forgets it.                                                              */
+/* ------------------------------------------------------------------------ */
+struct avo_processor {
+  int64_t m;
+  uint8_t* present;
+  uint8_t* decision;
+  avo_vote_record* rec;
+};
+
+avo_processor* avo_processor_new(int64_t n_targets) {
+  avo_processor* p = (avo_processor*)calloc(1, sizeof(avo_processor));
+  p->m = n_targets;
+  p->present = (uint8_t*)calloc((size_t)n_targets, 1);
+  p->decision = (uint8_t*)calloc((size_t)n_targets, 1);
+  p->rec = (avo_vote_record*)calloc((size_t)n_targets, sizeof(avo_vote_record));
+  return p;
+}
+
+void avo_processor_free(avo_processor* p) {
+  if (!p) return;
+  free(p->present);
+  free(p->decision);
+  free(p->rec);
+  free(p);
+}
+
+/* processor.go:45-58 AddTargetToReconcile */
+int avo_processor_add(avo_processor* p, int64_t t, int accepted, int valid) {
+  if (t < 0 || t >= p->m) return 0;
+  if (!valid) return 0;              /* :46-48 isWorthyPolling */
+  if (p->present[t]) return 0;       /* :50-53 */
+  p->present[t] = 1;                 /* :55-56 */
+  p->rec[t] = avo_new_vote_record(accepted);
+  return 1;
+}
+
+/* processor.go:61-122 RegisterVotes (validation block :63-90 is `if false`) */
+int avo_processor_register_votes(avo_processor* p, const int64_t* targets, const uint32_t* errs,
+                                 int64_t n, const uint8_t* valid, int64_t* out_targets,
+                                 int32_t* out_status, int64_t* n_out) {
+  int64_t nu = 0;
+  for (int64_t i = 0; i < n; ++i) { /* :94 */
+    int64_t t = targets[i];
+    if (t < 0 || t >= p->m || !p->present[t]) continue; /* :95-99 */
+    if (!valid[t]) continue;                             /* :101-103 */
+    avo_vote_record* vr = &p->rec[t];
+    if (!avo_register_vote(vr, errs[i])) continue;       /* :105-108 */
+    if (out_targets) out_targets[nu] = t;                /* :111 */
+    if (out_status) out_status[nu] = avo_status(vr);
+    nu++;
+    if (avo_has_finalized(vr)) {                         /* :114-116 */
+      p->present[t] = 0;
+      p->decision[t] = (uint8_t)avo_is_accepted_rec(vr);
+    }
+  }
+  if (n_out) *n_out = nu;
+  return 1; /* :121 */
+}
+
+/* processor.go:125-130 */
+int avo_processor_is_accepted(const avo_processor* p, int64_t t) {
+  if (t >= 0 && t < p->m && p->present[t]) return avo_is_accepted_rec(&p->rec[t]);
+  return 0;
+}
+
+/* processor.go:133-140 ; -1 stands for panic("VoteRecord not found") */
+int avo_processor_get_confidence(const avo_processor* p, int64_t t, uint16_t* out) {
+  if (t < 0 || t >= p->m || !p->present[t]) return -1;
+  *out = avo_get_confidence_rec(&p->rec[t]);
+  return 0;
+}
+
+/* processor.go:144-170. Go map order is randomised; the harness fixes it to
+ * ascending target index. Truncated to cap (4096, :165-167). */
+int64_t avo_processor_get_invs(const avo_processor* p, const uint8_t* valid, int64_t* out, int64_t cap) {
+  int64_t n = 0;
+  for (int64_t t = 0; t < p->m; ++t) {
+    if (!p->present[t]) continue;
+    if (avo_has_finalized(&p->rec[t])) continue; /* :147-150 */
+    if (!valid[t]) continue;                     /* :155-157 */
+    if (n < cap) out[n] = t;
+    n++;
+    if (n >= cap) break; /* invs[:4096] keeps the first cap in this order */
+  }
+  return n < cap ? n : cap;
+}
+
+uint32_t avo_processor_dump_word(const avo_processor* p, int64_t t) {
+  if (p->present[t]) return avo_pack(p->rec[t]);
+  return AVO_ABSENT_WORD | ((uint32_t)p->decision[t] << 16);
+}
+
+static int published_pref(const avo_processor* p, int64_t t) {
+  if (p->present[t]) return avo_is_accepted_rec(&p->rec[t]);
+  return p->decision[t];
+}
+
+/* ------------------------------------------------------------------------ */
+/* Synthetic workload definition                                            */
+/* ------------------------------------------------------------------------ */
+
+/* k distinct peers != node, uniform over the other N-1 nodes by 32x32->hi
+ * multiply; Philox blocks of 4 draws, counter (node, round, block, PEERS). */
+void avo_sample_peers(uint64_t seed, int64_t node, int64_t round, int64_t n_nodes, int32_t k,
+                      int32_t mode, int64_t* out) {
+  uint64_t others = (uint64_t)(n_nodes - 1);
+  if (mode == AVO_PEERS_ROUND_ROBIN || (uint64_t)k >= others) {
+    /* main.go:110-116: round-robin over all other nodes, skipping self */
+    for (int32_t j = 0; j < k; ++j) {
+      uint64_t q = (mode == AVO_PEERS_ROUND_ROBIN) ? ((uint64_t)round * (uint64_t)k + (uint64_t)j)
+                                                    : (uint64_t)j;
+      uint64_t idx = q % others;
+      out[j] = (int64_t)(idx + (idx >= (uint64_t)node ? 1 : 0));
+    }
+    return;
+  }
+  int32_t cnt = 0;
+  uint32_t blk = 0;
+  while (cnt < k) {
+    uint32_t x[4];
+    philox_dom(seed, (uint32_t)node, (uint32_t)round, blk, AVO_DOM_PEERS, x);
+    for (int i = 0; i < 4 && cnt < k; ++i) {
+      uint64_t u = ((uint64_t)x[i] * others) >> 32;
+      int64_t p = (int64_t)(u + (u >= (uint64_t)node ? 1 : 0));
+      int dup = 0;
+      for (int32_t j = 0; j < cnt; ++j) dup |= (out[j] == p);
+      if (!dup) out[cnt++] = p;
+    }
+    blk++;
+  }
+}
+
+int avo_is_byzantine(uint64_t seed, int64_t node, uint32_t threshold) {
+  uint32_t x[4];
+  philox_dom(seed, (uint32_t)node, 0, 0, AVO_DOM_BYZ, x);
+  return x[0] < threshold;
+}
+
+int avo_initial_accept(uint64_t seed, int32_t mode, uint32_t param, int64_t node, int64_t t) {
+  uint32_t x[4];
+  switch (mode) {
+    case AVO_INIT_REJECTED: return 0;
+    case AVO_INIT_ACCEPTED: return 1;
+    case AVO_INIT_BERNOULLI:
+      philox_dom(seed, (uint32_t)node, (uint32_t)(t >> 2), 0, AVO_DOM_INIT, x);
+      return x[t & 3] < param;
+    case AVO_INIT_PAIRS: {
+      int64_t pair = t >> 1;
+      philox_dom(seed, (uint32_t)node, (uint32_t)(pair >> 2), 0, AVO_DOM_PAIRS, x);
+      return (int)((x[pair & 3] >> 31) ^ (uint32_t)(t & 1));
+    }
+    default: return 0;
+  }
+}
+
+/* Replayed vote stream (C2): P(yes)=0.70, P(no)=0.25, P(neutral)=0.05.
+ * no-errs {1, 2, 0x7FFFFFFF}; neutral errs {0x80000000, 0xFFFFFFFF}. */
+uint32_t avo_replay_err(uint64_t seed, int64_t node, int64_t round, int32_t slot, int64_t t) {
+  uint32_t x[4];
+  philox_dom(seed, (uint32_t)node, (uint32_t)round, (uint32_t)(t >> 1),
+             AVO_DOM_REPLAY | ((uint32_t)slot << 8), x);
+  uint32_t v = x[(t & 1) * 2];
+  uint32_t sel = x[(t & 1) * 2 + 1];
+  if (v < 3006477107u) return 0u;
+  if (v < 4080218931u) {
+    static const uint32_t no_errs[3] = {1u, 2u, 0x7FFFFFFFu};
+    return no_errs[sel % 3u];
+  }
+  return (sel & 1u) ? 0xFFFFFFFFu : 0x80000000u;
+}
+
+void avo_gen_replay_errs(uint64_t seed, int64_t round, int64_t n0, int64_t n1, int64_t n_targets,
+                         int32_t k, uint32_t* out) {
+  for (int64_t n = n0; n < n1; ++n)
+    for (int32_t s = 0; s < k; ++s)
+      for (int64_t t = 0; t < n_targets; ++t)
+        out[((n - n0) * k + s) * n_targets + t] = avo_replay_err(seed, n, round, s, t);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Batched-round harness                                                    */
+/* ------------------------------------------------------------------------ */
+struct avo_sim {
+  avo_sim_config cfg;
+  int64_t round;
+  avo_processor** procs;
+  uint8_t* valid; /* [M] Target.IsValid() */
+  uint8_t* pref;  /* [N][M] round-start published preference snapshot */
+  uint8_t* byz;   /* [N] */
+};
+
+avo_sim* avo_sim_new(const avo_sim_config* cfg) {
+  avo_sim* s = (avo_sim*)calloc(1, sizeof(avo_sim));
+  s->cfg = *cfg;
+  int64_t n = cfg->n_nodes, m = cfg->n_targets;
+  s->procs = (avo_processor**)calloc((size_t)n, sizeof(avo_processor*));
+  s->valid = (uint8_t*)malloc((size_t)m);
+  memset(s->valid, 1, (size_t)m);
+  s->pref = (uint8_t*)calloc((size_t)(n * m), 1);
+  s->byz = (uint8_t*)calloc((size_t)n, 1);
+  for (int64_t j = 0; j < n; ++j) {
+    s->procs[j] = avo_processor_new(m);
+    s->byz[j] = (uint8_t)avo_is_byzantine(cfg->seed, j, cfg->byz_threshold);
+    if (cfg->init_mode != AVO_INIT_NONE) {
+      for (int64_t t = 0; t < m; ++t) {
+        int acc = avo_initial_accept(cfg->seed, cfg->init_mode, cfg->init_param, j, t);
+        avo_processor_add(s->procs[j], t, acc, 1);
+        s->pref[j * m + t] = (uint8_t)acc;
+      }
+    }
+  }
+  return s;
+}
+
+void avo_sim_free(avo_sim* s) {
+  if (!s) return;
+  for (int64_t j = 0; j < s->cfg.n_nodes; ++j) avo_processor_free(s->procs[j]);
+  free(s->procs);
+  free(s->valid);
+  free(s->pref);
+  free(s->byz);
+  free(s);
+}
+
+void avo_sim_set_valid(avo_sim* s, int64_t t, int valid) { s->valid[t] = (uint8_t)(valid != 0); }
+int64_t avo_sim_round_index(const avo_sim* s) { return s->round; }
+int avo_sim_is_byzantine(const avo_sim* s, int64_t node) { return s->byz[node]; }
+
+static void refresh_pref(avo_sim* s) {
+  int64_t n = s->cfg.n_nodes, m = s->cfg.n_targets;
+  for (int64_t j = 0; j < n; ++j)
+    for (int64_t t = 0; t < m; ++t) s->pref[j * m + t] = (uint8_t)published_pref(s->procs[j], t);
+}
+
+int avo_sim_add(avo_sim* s, int64_t node, int64_t t, int accepted) {
+  int r = avo_processor_add(s->procs[node], t, accepted, s->valid[t]);
+  s->pref[node * s->cfg.n_targets + t] = (uint8_t)published_pref(s->procs[node], t);
+  return r;
+}
+
+int avo_sim_register_votes(avo_sim* s, int64_t node, const int64_t* targets, const uint32_t* errs,
+                           int64_t n, int64_t* out_targets, int32_t* out_status, int64_t* n_out) {
+  int r = avo_processor_register_votes(s->procs[node], targets, errs, n, s->valid, out_targets,
+                                       out_status, n_out);
+  for (int64_t t = 0; t < s->cfg.n_targets; ++t)
+    s->pref[node * s->cfg.n_targets + t] = (uint8_t)published_pref(s->procs[node], t);
+  return r;
+}
+
+typedef struct {
+  int64_t* rows; /* 5 columns */
+  int64_t n, cap;
+} upd_buf;
+
+static void upd_push(upd_buf* b, int64_t r, int64_t node, int64_t slot, int64_t t, int64_t st) {
+  if (b->n == b->cap) {
+    b->cap = b->cap ? b->cap * 2 : 64;
+    b->rows = (int64_t*)realloc(b->rows, (size_t)b->cap * 5 * sizeof(int64_t));
+  }
+  int64_t* row = b->rows + b->n * 5;
+  row[0] = r; row[1] = node; row[2] = slot; row[3] = t; row[4] = st;
+  b->n++;
+}
+
+/* One synchronous round (R1): every node draws k peers; for slot s it builds
+ * the capped poll set (GetInvsForNextPoll, ascending index) and registers one
+ * Response whose votes are the peer's round-start published preference
+ * (main.go:179-182: IsAccepted ? 0 : 1), Byzantine peers answering
+ * ((r ^ t) & 1) (R4), or the replayed err stream. */
+int avo_sim_round(avo_sim* s, const uint32_t* replay_errs, int64_t* updates, int64_t cap,
+                  int64_t* n_out, int32_t threads, int64_t* applied_votes) {
+  const int64_t n_nodes = s->cfg.n_nodes, m = s->cfg.n_targets;
+  const int32_t k = s->cfg.k;
+  const int64_t r = s->round;
+  upd_buf* bufs = (upd_buf*)calloc((size_t)n_nodes, sizeof(upd_buf));
+  int64_t applied = 0;
+  (void)threads;
+#ifdef _OPENMP
+  int nt = threads > 0 ? threads : 1;
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nt) reduction(+ : applied)
+#endif
+  for (int64_t node = 0; node < n_nodes; ++node) {
+    avo_processor* p = s->procs[node];
+    int64_t* peers = (int64_t*)malloc((size_t)k * sizeof(int64_t));
+    int64_t* invs = (int64_t*)malloc(AVO_MAX_ELEMENT_POLL * sizeof(int64_t));
+    uint32_t* errs = (uint32_t*)malloc(AVO_MAX_ELEMENT_POLL * sizeof(uint32_t));
+    int64_t* ut = (int64_t*)malloc(AVO_MAX_ELEMENT_POLL * sizeof(int64_t));
+    int32_t* us = (int32_t*)malloc(AVO_MAX_ELEMENT_POLL * sizeof(int32_t));
+    avo_sample_peers(s->cfg.seed, node, r, n_nodes, k, s->cfg.peer_mode, peers);
+    for (int32_t slot = 0; slot < k; ++slot) {
+      int64_t ni = avo_processor_get_invs(p, s->valid, invs, AVO_MAX_ELEMENT_POLL);
+      int64_t peer = peers[slot];
+      for (int64_t i = 0; i < ni; ++i) {
+        int64_t t = invs[i];
+        uint32_t err;
+        if (replay_errs) {
+          err = replay_errs[(node * k + slot) * m + t];
+        } else if (s->byz[peer]) {
+          err = ((uint64_t)(r ^ t) & 1u) ? 1u : 0u;
+        } else {
+          err = s->pref[peer * m + t] ? 0u : 1u;
+        }
+        errs[i] = err;
+      }
+      int64_t nu = 0;
+      applied += ni; /* every polled record is live and valid: one regsiterVote each */
+      avo_processor_register_votes(p, invs, errs, ni, s->valid, ut, us, &nu);
+      for (int64_t i = 0; i < nu; ++i) upd_push(&bufs[node], r, node, slot, ut[i], us[i]);
+    }
+    free(peers); free(invs); free(errs); free(ut); free(us);
+  }
+  int64_t total = 0;
+  for (int64_t node = 0; node < n_nodes; ++node) total += bufs[node].n;
+  int rc = 0;
+  if (n_out) *n_out = total;
+  if (updates && total <= cap) {
+    int64_t off = 0;
+    for (int64_t node = 0; node < n_nodes; ++node) {
+      memcpy(updates + off * 5, bufs[node].rows, (size_t)bufs[node].n * 5 * sizeof(int64_t));
+      off += bufs[node].n;
+    }
+  } else if (updates) {
+    rc = -1;
+  }
+  for (int64_t node = 0; node < n_nodes; ++node) free(bufs[node].rows);
+  free(bufs);
+  refresh_pref(s);
+  if (applied_votes) *applied_votes = applied;
+  s->round++;
+  return rc;
+}
+
+void avo_sim_dump(const avo_sim* s, uint32_t* out) {
+  int64_t n = s->cfg.n_nodes, m = s->cfg.n_targets;
+  for (int64_t j = 0; j < n; ++j)
+    for (int64_t t = 0; t < m; ++t) out[j * m + t] = avo_processor_dump_word(s->procs[j], t);
+}
+
+void avo_sim_pref(const avo_sim* s, uint8_t* out) {
+  memcpy(out, s->pref, (size_t)(s->cfg.n_nodes * s->cfg.n_targets));
+}

@@ -1,0 +1,288 @@
+"""GPU parity tests: the HIP engine (through the C ABI of libavhip.so) against
+the CPU oracle on identical seeded inputs, and against the golden vectors
+transcribed from the reference's tests. Bit-exact everywhere (integer path)."""
+import numpy as np
+import pytest
+
+import avhip
+from golden_ops import NotFound, run_processor
+
+pytestmark = pytest.mark.gpu
+
+BYZ20 = int(0.2 * 2**32)
+P80 = int(0.8 * 2**32)
+
+
+def rows(u):
+    return [tuple(int(v) for v in r) for r in np.asarray(u).tolist()]
+
+
+def make_pair(oracle, n, m, k, seed=7, peer_mode=0, byz=0, init_mode=3, init_param=P80):
+    eng = avhip.Engine(n, m, k=k, seed=seed, peer_mode=peer_mode, byz_threshold=byz)
+    eng.init_records(init_mode, init_param)
+    sim = oracle.Sim(n, m, k, seed=seed, peer_mode=peer_mode, byz_threshold=byz, init_mode=init_mode,
+                     init_param=init_param)
+    return eng, sim
+
+
+def assert_same_state(eng, sim, where=""):
+    got, exp = eng.read_records(), sim.dump()
+    if not np.array_equal(got, exp):
+        bad = np.argwhere(got != exp)[:5]
+        msg = [(int(a), int(b), hex(int(got[a, b])), hex(int(exp[a, b]))) for a, b in bad]
+        raise AssertionError(f"state mismatch {where}: {msg}")
+
+
+# ------------------------------------------------------------------ sampling / init
+@pytest.mark.parametrize("n,k,mode", [(1000, 8, 0), (12, 8, 0), (9, 8, 0), (7, 3, 1), (300, 16, 0), (3, 4, 0)])
+def test_sample_peers_parity(oracle, n, k, mode):
+    eng = avhip.Engine(n, 64, k=k, seed=11, peer_mode=mode)
+    for rnd in (0, 1, 17, 1000):
+        got = eng.sample_peers(rnd)
+        for node in range(n):
+            assert got[node].tolist() == oracle.sample_peers(11, node, rnd, n, k, mode).tolist(), (node, rnd)
+
+
+@pytest.mark.parametrize("mode,param", [(1, 0), (2, 0), (3, P80), (4, 0)])
+def test_init_parity(oracle, mode, param):
+    eng, sim = make_pair(oracle, 37, 150, 8, byz=BYZ20, init_mode=mode, init_param=param)
+    assert_same_state(eng, sim)
+    pref, exp = eng.read_pref(), sim.pref()
+    honest = [j for j in range(37) if not sim.is_byzantine(j)]
+    assert np.array_equal(pref[honest], exp[honest])
+
+
+# ------------------------------------------------------------------ rounds, sim mode
+SIM_CASES = [
+    dict(n=12, m=40, k=8, seed=7, init_mode=3),
+    dict(n=10, m=33, k=8, seed=9, init_mode=4, byz=BYZ20),
+    dict(n=6, m=20, k=3, seed=3, init_mode=2, peer_mode=1),
+    dict(n=8, m=70, k=5, seed=4, init_mode=1, byz=int(0.3 * 2**32)),
+    dict(n=64, m=200, k=8, seed=0xA7A1A9C4, init_mode=3, byz=BYZ20),
+    dict(n=300, m=517, k=8, seed=5, init_mode=4, byz=BYZ20),
+    dict(n=40, m=96, k=16, seed=8, init_mode=3),
+]
+
+
+@pytest.mark.parametrize("case", SIM_CASES, ids=lambda c: f"n{c['n']}m{c['m']}k{c['k']}")
+def test_sim_rounds_parity(oracle, case):
+    eng, sim = make_pair(oracle, case["n"], case["m"], case["k"], seed=case["seed"],
+                         peer_mode=case.get("peer_mode", 0), byz=case.get("byz", 0), init_mode=case["init_mode"])
+    total_applied = 0
+    for r in range(40):
+        if r == 5:  # target invalidated mid-run (avalanche_test.go:534 pattern), later revalidated
+            eng.set_valid(3, False)
+            sim.set_valid(3, False)
+        if r == 13:
+            eng.set_valid(3, True)
+            sim.set_valid(3, True)
+        eng.run_rounds(1)
+        exp_u, applied = sim.run_round()
+        total_applied += applied
+        got_u = eng.fetch_updates()
+        assert rows(got_u) == rows(exp_u), f"round {r}"
+        assert_same_state(eng, sim, f"round {r}")
+        assert eng.applied_votes() == total_applied
+    assert eng.round == 40
+
+
+def test_sim_capped_parity(oracle):
+    """M > 4096: the workgroup-scan path enforces the 4096 poll cap."""
+    eng, sim = make_pair(oracle, 20, 5000, 8, seed=3, byz=BYZ20, init_mode=3)
+    for r in range(6):
+        eng.run_rounds(1)
+        exp_u, applied = sim.run_round()
+        assert rows(eng.fetch_updates()) == rows(exp_u), r
+        assert_same_state(eng, sim, f"round {r}")
+    assert eng.layout_info()["capped"]
+
+
+# ------------------------------------------------------------------ rounds, replay mode
+@pytest.mark.parametrize("n,m,k", [(9, 300, 8), (6, 4500, 8), (5, 4097, 2), (4, 8300, 8)])
+def test_replay_parity(oracle, n, m, k):
+    eng, sim = make_pair(oracle, n, m, k, seed=21, init_mode=3)
+    applied_total = 0
+    for r in range(12):
+        errs = oracle.gen_replay_errs(21, r, 0, n, m, k)
+        eng.replay_round_errs(errs)
+        exp_u, applied = sim.run_round(errs)
+        applied_total += applied
+        assert rows(eng.fetch_updates()) == rows(exp_u), r
+        assert_same_state(eng, sim, f"round {r}")
+    assert eng.applied_votes() == applied_total
+
+
+def test_device_replay_generator_parity(oracle):
+    n, m, k, R = 10, 4300, 8, 6
+    eng, sim = make_pair(oracle, n, m, k, seed=0xA7A1A9C4, init_mode=3)
+    eng.replay_prepare(R)
+    eng.replay_rounds(R)
+    exp = []
+    for r in range(R):
+        u, _ = sim.run_round(oracle.gen_replay_errs(0xA7A1A9C4, r, 0, n, m, k))
+        exp += rows(u)
+    assert rows(eng.fetch_updates()) == exp
+    assert_same_state(eng, sim)
+
+
+# ------------------------------------------------------------------ exhaustive single-vote transitions
+def test_exhaustive_transitions_gpu(oracle):
+    """Every reachable live record (votes subset of consider: 6561 pairs x count
+    0..127 x accepted) receives one vote of each err class; result and emitted
+    StatusUpdate must equal the oracle's regsiterVote (vote.go:54-91)."""
+    v = np.arange(256, dtype=np.uint32)
+    vv, cc = np.meshgrid(v, v, indexing="ij")
+    ok = (vv & ~cc) == 0
+    vc = (vv[ok] | (cc[ok] << 8)).astype(np.uint32)  # 6561 nodes
+    t = np.arange(256, dtype=np.uint32)  # target t: count t>>1, accepted t&1
+    words = vc[:, None] | (((t >> 1) << 1 | (t & 1)) << 16)[None, :]
+    n, m = words.shape
+    for err in [0, 1, 2, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFF]:
+        eng = avhip.Engine(n, m, k=1, seed=1)
+        eng.init_records(avhip.INIT_REJECTED, 0)
+        eng.write_records(words)
+        assert np.array_equal(eng.read_records(), words)
+        eng.replay_round_errs(np.full((n, 1, m), err, np.uint32))
+        exp_w, changed, status = oracle.transition_batch(words.ravel(), np.full(words.size, err, np.uint32))
+        exp_w = exp_w.reshape(n, m)
+        fin = (exp_w >> 17) >= 128
+        exp_dump = np.where(fin, avhip.ABSENT_WORD | (((exp_w >> 16) & 1) << 16), exp_w).astype(np.uint32)
+        assert np.array_equal(eng.read_records(), exp_dump), hex(err)
+        idx = np.flatnonzero(changed)
+        exp_u = [(0, int(i // m), 0, int(i % m), int(status[i])) for i in idx]
+        assert rows(eng.fetch_updates()) == exp_u, hex(err)
+        eng.close()
+
+
+# ------------------------------------------------------------------ golden vectors through the C ABI
+class EngineProc:
+    def __init__(self, fx):
+        self.accepted = {int(h): v["accepted"] for h, v in fx["targets"].items()}
+        self.eng = avhip.Engine(2, max(self.accepted) + 1, k=1)
+
+    def add(self, h):
+        return bool(self.eng.add_targets(0, [h], [self.accepted[h]])[0])
+
+    def register(self, node, votes):
+        st = self.eng.register_votes(0, [h for _, h in votes], [e for e, _ in votes])
+        return [(h, int(s)) for (_, h), s in zip(votes, st) if s >= 0]
+
+    def is_accepted(self, h):
+        return self.eng.is_accepted(0, h)
+
+    def confidence(self, h):
+        try:
+            return self.eng.get_confidence(0, h)
+        except avhip.VoteRecordNotFound:
+            raise NotFound()
+
+    def invs(self):
+        return self.eng.get_invs(0).tolist()
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_processor_golden_gpu(golden, which):
+    fx = golden["processor"][which]
+    run_processor(fx, EngineProc(fx))
+
+
+def test_vote_record_golden_gpu(golden):
+    """TestVoteRecord (avalanche_test.go:13-91) through the engine. The bare
+    VoteRecord keeps voting after finalization; a Processor deletes it
+    (processor.go:114-116), so the engine runs the live stretches: up to the
+    first finalization, then from the flip at :70 (state rebuilt from the vote
+    history and the golden values) to the final finalization at :91."""
+    fx = golden["vote_record"]
+    steps = fx["steps"]
+    eng = avhip.Engine(2, 1, k=1)
+    assert eng.add_targets(0, [0], [fx["start_accepted"]])[0]
+    votes = cons = 0
+    resumed = False
+    for i, st in enumerate(steps):
+        err = st["err"]
+        votes = ((votes << 1) & 0xFF) | (err == 0)
+        cons = ((cons << 1) & 0xFF) | (err < 0x80000000)
+        exp = (st["accepted"], st["finalized"], st["confidence"])
+        dead = (int(eng.read_records()[0, 0]) >> 17) >= 128
+        if dead:
+            if st["finalized"]:
+                continue  # bare record past finalization: no Processor equivalent
+            # flip back to live (line 70): rebuild the bare record and resume
+            eng.write_records(np.array([[votes | (cons << 8) | ((st["confidence"] << 1 | st["accepted"]) << 16)]],
+                                       np.uint32))
+            resumed = True
+            continue
+        eng.register_votes(0, [0], [err])
+        w = int(eng.read_records()[0, 0])
+        if (w >> 17) >= 128:
+            got = (bool((w >> 16) & 1), True, 128)
+        else:
+            got = (bool((w >> 16) & 1), False, w >> 17)
+        assert got == exp, f"step {i} (line {st['line']}): {got} != {exp}"
+    assert resumed and (int(eng.read_records()[0, 0]) >> 17) >= 128
+
+
+# ------------------------------------------------------------------ sharding identities
+def test_target_shard_identity():
+    """Two target-sharded engines == one engine, bit for bit (the multi-GPU
+    target-sharding path, exercised on one device)."""
+    n, m, k, R = 500, 1000, 8, 30
+    full = avhip.Engine(n, m, k=k, seed=3, byz_threshold=BYZ20)
+    full.init_records(avhip.INIT_PAIRS, 0)
+    parts = [avhip.Engine(n, m, k=k, seed=3, byz_threshold=BYZ20, target_range=r) for r in [(0, 512), (512, 1000)]]
+    for p in parts:
+        p.init_records(avhip.INIT_PAIRS, 0)
+    full.run_rounds(R)
+    for p in parts:
+        p.run_rounds(R)
+    merged = np.concatenate([p.read_records() for p in parts], axis=1)
+    assert np.array_equal(full.read_records(), merged)
+    u = np.concatenate([p.fetch_updates() for p in parts])
+    u = u[np.lexsort((u[:, 3], u[:, 2], u[:, 1], u[:, 0]))]
+    assert np.array_equal(full.fetch_updates(), u)
+    assert full.applied_votes() == sum(p.applied_votes() for p in parts)
+
+
+def test_node_shard_needs_comm():
+    e = avhip.Engine(10, 64, node_range=(0, 5))
+    with pytest.raises(avhip.AvError):
+        e.run_rounds(1)
+
+
+# ------------------------------------------------------------------ full-size properties
+def test_c4_shape_properties():
+    """C4 shape at 1/10 scale (100k nodes x 1000 targets, k=8, Bernoulli(0.8)):
+    rounds 0-15 keep every record live (finalization needs >= 134 votes), so
+    applied votes == N*M*k per round; two runs are identical; the published
+    preference equals the records' accepted bit."""
+    n, m, k = 100_000, 1000, 8
+    digests = []
+    for _ in range(2):
+        e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4)
+        e.init_records(avhip.INIT_BERNOULLI, P80)
+        e.run_rounds(16)
+        assert e.applied_votes() == n * m * k * 16
+        u = e.fetch_updates()
+        assert not np.isin(u[:, 4], [avhip.STATUS_FINALIZED, avhip.STATUS_INVALID]).any()
+        recs = e.read_records(0, n, 0, m)
+        assert ((recs >> 17) < 128).all()
+        pref = e.read_pref(0, n, 0, m)
+        assert np.array_equal(pref, ((recs >> 16) & 1).astype(np.uint8))
+        digests.append((recs.tobytes().__hash__(), len(u)))
+        e.close()
+    assert digests[0] == digests[1]
+
+
+def test_run_to_finalization_properties(oracle):
+    """Honest network, all accepted: every record finalizes Finalized exactly
+    once, at vote 134 (round 16 at k=8), and then the engine goes quiet."""
+    n, m, k = 2000, 300, 8
+    e = avhip.Engine(n, m, k=k, seed=5)
+    e.init_records(avhip.INIT_ACCEPTED, 0)
+    e.run_rounds(20)
+    u = e.fetch_updates()
+    assert len(u) == n * m
+    assert (u[:, 4] == avhip.STATUS_FINALIZED).all()
+    assert (u[:, 0] == 16).all() and (u[:, 2] == 5).all()  # 16*8 + 6 = 134th vote
+    assert e.applied_votes() == n * m * 134
+    assert (e.read_records() == (avhip.ABSENT_WORD | 1 << 16)).all()

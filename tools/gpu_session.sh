@@ -1,0 +1,46 @@
+#!/bin/bash
+# Run GPU steps on the gpurun box; stop at the first crash-class exit status
+# (fault/abort/segv/timeout), keep going after ordinary test failures (rc 1).
+#   tools/gpu_session.sh smoke tests bench prof pmc
+# Outputs under gpurun_out/.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+OUT=gpurun_out
+
+step() {  # name, timeout-seconds, command...
+  local name=$1 secs=$2
+  shift 2
+  echo "=== $name: $*" | tee -a $OUT/session.log
+  local t0=$(date +%s)
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a $OUT/session.log
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "crash-class exit ($rc) in $name: stopping" | tee -a $OUT/session.log
+    exit $rc
+  fi
+  return 0
+}
+
+for s in "$@"; do
+  case $s in
+    smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step pytest_gpu 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench) step bench 900 python bench.py ;;
+    bench_c2) step bench_c2 900 python bench.py --workload c2 --no-cpu-baseline ;;
+    bench_c3) step bench_c3 900 python bench.py --workload c3 --no-cpu-baseline ;;
+    bench_c5) step bench_c5 900 python bench.py --workload c5 --no-cpu-baseline ;;
+    prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- \
+            python3 bench.py --no-cpu-baseline ;;
+    pmc_fetch) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o bench -- \
+            python3 bench.py --no-cpu-baseline ;;
+    pmc_write) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o bench -- \
+            python3 bench.py --no-cpu-baseline ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "=== session done" | tee -a $OUT/session.log
