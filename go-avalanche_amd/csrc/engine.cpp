@@ -69,6 +69,7 @@ struct av_engine {
   uint32_t* log_count = nullptr;
   uint32_t* log_overflow = nullptr;
   uint32_t log_cap = 0;
+  uint32_t log_shards = 1;
   unsigned long long* applied = nullptr;
   int64_t round = 0, log_base = 0;
   std::vector<uint32_t> valid_host;
@@ -140,6 +141,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   p.applied = e->applied;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
+  p.log_shards = e->log_shards;
   p.n_nodes = (uint32_t)e->N;
   p.n0 = (uint32_t)e->n0;
   p.NL = e->NL;
@@ -278,13 +280,16 @@ int av_create(const av_config* cfg, av_engine** out) {
   const size_t pref_words = (size_t)e->N * e->BL;
   int64_t cap = c.update_log_capacity;
   if (cap <= 0) cap = std::min<int64_t>(std::max<int64_t>((int64_t)L * 8, 1 << 20), 1ll << 28);
-  e->log_cap = (uint32_t)std::max<int64_t>((cap + avk::kLogShards - 1) / avk::kLogShards, 64);
+  // one shard per wave up to kLogShards: waves of the round kernel that runs
+  const uint64_t waves = e->capped ? (uint64_t)e->NL * ((e->BL + 63) / 64) : (uint64_t)(e->Lpad / 64);
+  e->log_shards = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(waves, avk::kLogShards));
+  e->log_cap = (uint32_t)std::max<int64_t>((cap + e->log_shards - 1) / e->log_shards, 64);
   if ((he = dev_alloc(&e->planes, plane_words)) != hipSuccess) return hip_fail(he, "alloc planes");
   if ((he = dev_alloc(&e->pref[0], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->pref[1], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->valid, e->BL)) != hipSuccess) return hip_fail(he, "alloc valid");
   if ((he = dev_alloc(&e->byz, (e->N + 31) / 32)) != hipSuccess) return hip_fail(he, "alloc byz");
-  if ((he = dev_alloc(&e->log, (size_t)e->log_cap * avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  if ((he = dev_alloc(&e->log, (size_t)e->log_cap * e->log_shards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->log_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->log_overflow, 1)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->applied, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
@@ -678,7 +683,7 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
     auto* dense = static_cast<uint64_t*>(s.p);
     auto* doffs = dense + total;
     AV_HIP(hipMemcpyAsync(doffs, offs.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
-    AV_HIP(avk::launch_compact_log(e->log, e->log_count, doffs, e->log_cap, dense, e->stream));
+    AV_HIP(avk::launch_compact_log(e->log, e->log_count, doffs, e->log_cap, e->log_shards, dense, e->stream));
     AV_HIP(hipMemcpyAsync(out, dense, (size_t)total * 8, hipMemcpyDeviceToHost, e->stream));
     AV_HIP(hipStreamSynchronize(e->stream));
     std::sort(out, out + total);

@@ -42,6 +42,7 @@ struct RoundParams {
   unsigned long long* applied;  // [kLogShards] regsiterVote applications
   uint64_t seed;
   uint32_t log_cap;          // entries per shard
+  uint32_t log_shards;       // shards in use (<= kLogShards; min(waves, kLogShards))
   uint32_t n_nodes;          // N (global)
   uint32_t n0;               // first local node (global id)
   uint32_t NL;               // local nodes
@@ -114,6 +115,6 @@ hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t B
                              uint32_t t0, uint32_t n_targets, uint32_t round, int k, uint32_t* out,
                              hipStream_t s);
 hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets,
-                              uint32_t log_cap, uint64_t* out, hipStream_t s);
+                              uint32_t log_cap, uint32_t shards, uint64_t* out, hipStream_t s);
 
 }  // namespace avk

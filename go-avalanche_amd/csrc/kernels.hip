@@ -251,7 +251,7 @@ __device__ __forceinline__ void emit_updates(const RoundParams& p, uint32_t wave
   if (__ballot(cnt != 0u) == 0ull) return;
   const uint32_t incl = wave_incl_scan(cnt, lane);
   const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
-  const uint32_t shard = wave_id & (kLogShards - 1u);
+  const uint32_t shard = wave_id % p.log_shards;
   uint32_t base = 0;
   if (lane == 0) base = atomicAdd(&p.log_count[shard], total);
   base = (uint32_t)__shfl((int)base, 0, 64);
@@ -286,7 +286,7 @@ __device__ __forceinline__ void emit_updates(const RoundParams& p, uint32_t wave
 
 __device__ __forceinline__ void count_applied(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied) {
   const uint32_t s = wave_sum(applied);
-  if (lane == 0 && s) atomicAdd(&p.applied[wave_id & (kLogShards - 1u)], (unsigned long long)s);
+  if (lane == 0 && s) atomicAdd(&p.applied[wave_id % p.log_shards], (unsigned long long)s);
 }
 
 // ---------------------------------------------------------------------------
@@ -831,8 +831,8 @@ hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t B
 }
 
 hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets, uint32_t log_cap,
-                              uint64_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_compact_log, dim3(kLogShards), dim3(256), 0, s, log, counts, offsets, log_cap, out);
+                              uint32_t shards, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_compact_log, dim3(shards), dim3(256), 0, s, log, counts, offsets, log_cap, out);
   return hipGetLastError();
 }
 
