@@ -83,7 +83,7 @@ def cpu_baseline(wl, seed, budget_s):
     n, m, k, init_mode, init_param, byz, replay, _ = WORKLOADS[wl]
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     threads = max(1, min(threads, 16))
-    ns = min(n, 8000 if wl != "c2" else 200)
+    ns = min(n, 40000 if wl != "c2" else 200)
     sim = cabi.Sim(ns, m, k, seed=seed, byz_threshold=byz, init_mode=init_mode, init_param=init_param)
     applied = 0
     dt = 0.0

@@ -232,14 +232,15 @@ def test_target_shard_identity():
     parts = [avhip.Engine(n, m, k=k, seed=3, byz_threshold=BYZ20, target_range=r) for r in [(0, 512), (512, 1000)]]
     for p in parts:
         p.init_records(avhip.INIT_PAIRS, 0)
-    full.run_rounds(R)
-    for p in parts:
-        p.run_rounds(R)
+    for r in range(R):
+        full.run_rounds(1)
+        for p in parts:
+            p.run_rounds(1)
+        u = np.concatenate([p.fetch_updates() for p in parts])
+        u = u[np.lexsort((u[:, 3], u[:, 2], u[:, 1], u[:, 0]))]
+        assert np.array_equal(full.fetch_updates(), u), r
     merged = np.concatenate([p.read_records() for p in parts], axis=1)
     assert np.array_equal(full.read_records(), merged)
-    u = np.concatenate([p.fetch_updates() for p in parts])
-    u = u[np.lexsort((u[:, 3], u[:, 2], u[:, 1], u[:, 0]))]
-    assert np.array_equal(full.fetch_updates(), u)
     assert full.applied_votes() == sum(p.applied_votes() for p in parts)
 
 
