@@ -53,7 +53,6 @@ WORKLOADS = {
            "C5: 10M nodes x 256 targets, k=8, Bernoulli(0.8), honest"),
 }
 
-BYTES_PER_LANE_PLANES = 25 * 4 * 2  # 25 u32 state planes read + written per 32-record block
 
 
 def parse():
@@ -142,6 +141,7 @@ def main():
     except avhip.LogOverflow:
         pass  # the log is cleared on overflow; warmup updates are not measured
     applied0 = eng.applied_votes()
+    bytes0 = eng.alg_bytes()
 
     # ---- timed region: K rounds
     eng.set_timing(True)
@@ -159,30 +159,26 @@ def main():
     kern_ms, launches = eng.kernel_stats()
     applied = eng.applied_votes() - applied0
     emitted = eng.updates_count()
+    # algorithmic bytes per launch, counted by the round kernel itself (planes
+    # actually streamed, gathered vote words, published words, StatusUpdates)
+    alg_bytes = (eng.alg_bytes() - bytes0) / max(launches, 1)
 
     stats = torch.tensor([elapsed, float(applied), float(emitted), kern_ms / max(launches, 1),
-                          float(info["lanes"])], dtype=torch.float64, device="cuda")
+                          float(alg_bytes)], dtype=torch.float64, device="cuda")
     if world > 1:
         tmax = stats[0].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tot = stats[1:3].clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        kavg = stats[3].clone()
-        dist.all_reduce(kavg, op=dist.ReduceOp.MAX)
-        elapsed, applied, emitted, kavg_ms = float(tmax), float(tot[0]), float(tot[1]), float(kavg)
-    else:
-        kavg_ms = float(stats[3])
-    lanes_local = info["lanes"]
+        elapsed, applied, emitted = float(tmax), float(tot[0]), float(tot[1])
+    kavg_ms = float(stats[3])  # this rank's (rank 0's) round-kernel average, HIP events on the engine stream
 
     if rank == 0:
         value = applied / elapsed
-        # algorithmic bytes of one round-kernel launch on one GPU (DESIGN.md "Roofline"):
-        #   per 32-record lane: 25 state planes read+written (200 B), k gathered
-        #   peer-preference words (4k B) or 2k replayed vote planes (8k B), one
-        #   published-preference word (4 B); + 8 B per emitted StatusUpdate.
-        per_lane = BYTES_PER_LANE_PLANES + (8 * k if replay else 4 * k) + 4
-        emitted_per_launch = emitted / max(args.steps, 1) / world
-        alg_bytes = lanes_local * per_lane + emitted_per_launch * 8
+        # roofline of rank 0's round kernel: its algorithmic bytes
+        # per launch (counted by the kernel: 236 B per 32-record lane at k=8, 176 B
+        # once the consider planes are warm, + 8 B per StatusUpdate) / its
+        # average launch time.
         achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")

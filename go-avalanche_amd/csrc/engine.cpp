@@ -71,7 +71,12 @@ struct av_engine {
   uint32_t log_cap = 0;
   uint32_t log_shards = 1;
   unsigned long long* applied = nullptr;
+  unsigned long long* bytes = nullptr;
   int64_t round = 0, log_base = 0;
+  // every consider bit ever shifted in was 1 (no replay, no neutral drop-in
+  // vote, no write_records): an all-ones oldest consider plane implies all
+  // consider planes are all-ones (lets k_round_fast skip them)
+  bool c_monotone = true;
   std::vector<uint32_t> valid_host;
   // replay stream
   uint32_t* replay = nullptr;
@@ -139,6 +144,8 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   p.log_count = e->log_count;
   p.log_overflow = e->log_overflow;
   p.applied = e->applied;
+  p.bytes = e->bytes;
+  p.warm_skip = e->c_monotone ? 1u : 0u;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
   p.log_shards = e->log_shards;
@@ -219,7 +226,7 @@ int av_destroy(av_engine* e) {
   }
   if (e->comm) (void)ncclCommDestroy(e->comm);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->valid, e->byz, e->log, e->log_count, e->log_overflow,
-                  e->applied, e->replay};
+                  e->applied, e->bytes, e->replay};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -293,6 +300,8 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->log_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->log_overflow, 1)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->applied, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
+  if ((he = dev_alloc(&e->bytes, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
+  (void)hipMemsetAsync(e->bytes, 0, avk::kLogShards * 8, e->stream);
   (void)hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
   (void)hipMemsetAsync(e->applied, 0, avk::kLogShards * 8, e->stream);
@@ -437,6 +446,7 @@ int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const 
     const int64_t tl = targets[i] - e->t0;
     const uint32_t b = (uint32_t)(tl >> 5);
     const uint32_t err = errs[i];
+    if ((int32_t)err < 0) e->c_monotone = false;  // neutral vote shifts in consider = 0
     const uint32_t meta = (uint32_t)(tl & 31) | ((err == 0u ? 1u : 0u) << 5) | (((int32_t)err >= 0 ? 1u : 0u) << 6);
     const uint32_t slot = start[b]++;
     entries[2 * (size_t)slot] = (uint32_t)i;
@@ -496,6 +506,7 @@ int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t
            AV_ERR_INVALID_ARG, "range outside this engine's shard");
   const size_t n = (size_t)(n1 - n0) * (size_t)(t1 - t0);
   if (!n) return AV_OK;
+  e->c_monotone = false;
   Scratch s;
   AV_HIP(s.ensure(n * 4));
   AV_HIP(hipMemcpyAsync(s.p, in, n * 4, hipMemcpyHostToDevice, e->stream));
@@ -563,6 +574,7 @@ int av_run_rounds(av_engine* e, int32_t rounds) {
 int av_replay_round_errs(av_engine* e, const uint32_t* errs) {
   AV_ENTER(e);
   AV_CHECK(errs, AV_ERR_INVALID_ARG, "null argument");
+  e->c_monotone = false;
   const int64_t TL = e->t1 - e->t0;
   std::vector<uint32_t> planes(e->round_replay_words(), 0u);
   for (uint32_t nl = 0; nl < e->NL; ++nl)
@@ -618,6 +630,7 @@ int av_replay_rounds(av_engine* e, int32_t rounds) {
   AV_CHECK(rounds >= 0, AV_ERR_INVALID_ARG, "rounds < 0");
   AV_CHECK(e->round >= e->replay_first && e->round + rounds <= e->replay_first + e->replay_ready,
            AV_ERR_INVALID_ARG, "replay stream not prepared for these rounds");
+  if (rounds > 0) e->c_monotone = false;
   const size_t per = e->round_replay_words();
   for (int32_t r = 0; r < rounds; ++r) {
     int rc = launch_one_round(e, e->replay + per * (size_t)(e->round - e->replay_first));
@@ -699,6 +712,18 @@ int av_applied_votes(av_engine* e, int64_t* out) {
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
   std::vector<unsigned long long> c(avk::kLogShards);
   AV_HIP(hipMemcpyAsync(c.data(), e->applied, avk::kLogShards * 8, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  unsigned long long t = 0;
+  for (auto v : c) t += v;
+  *out = (int64_t)t;
+  return AV_OK;
+}
+
+int av_alg_bytes(av_engine* e, int64_t* out) {
+  AV_ENTER(e);
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  std::vector<unsigned long long> c(avk::kLogShards);
+  AV_HIP(hipMemcpyAsync(c.data(), e->bytes, avk::kLogShards * 8, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
   unsigned long long t = 0;
   for (auto v : c) t += v;

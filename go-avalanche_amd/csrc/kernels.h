@@ -40,6 +40,7 @@ struct RoundParams {
   uint32_t* log_count;       // [kLogShards]
   uint32_t* log_overflow;    // [1]
   unsigned long long* applied;  // [kLogShards] regsiterVote applications
+  unsigned long long* bytes;    // [kLogShards] algorithmic bytes moved by the round kernel
   uint64_t seed;
   uint32_t log_cap;          // entries per shard
   uint32_t log_shards;       // shards in use (<= kLogShards; min(waves, kLogShards))
@@ -53,6 +54,7 @@ struct RoundParams {
   uint32_t round;            // global round index (RNG counter, byz pattern)
   uint32_t round_rel;        // round - log base (update key field)
   int32_t peer_mode;
+  uint32_t warm_skip;        // consider planes are monotone (sim votes only): skip all-ones planes
 };
 
 // Update-log entry (one StatusUpdate, avalanche.go:59-62):

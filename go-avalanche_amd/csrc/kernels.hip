@@ -242,20 +242,20 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // later slots) (only flips change A); a record finalized this round has a
 // single E bit (count 127 -> 128 cannot follow a flip within 16 votes).
 template <int K>
-__device__ __forceinline__ void emit_updates(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t node,
-                                             uint32_t tbase, const uint32_t (&E)[K], uint32_t A_final,
-                                             uint32_t died) {
+__device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t wave_id, uint32_t lane,
+                                                 uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
+                                                 uint32_t A_final, uint32_t died) {
   uint32_t cnt = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) cnt += __popc(E[j]);
-  if (__ballot(cnt != 0u) == 0ull) return;
+  if (__ballot(cnt != 0u) == 0ull) return 0u;
   const uint32_t incl = wave_incl_scan(cnt, lane);
   const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
   const uint32_t shard = wave_id % p.log_shards;
   uint32_t base = 0;
   if (lane == 0) base = atomicAdd(&p.log_count[shard], total);
   base = (uint32_t)__shfl((int)base, 0, 64);
-  if (cnt == 0u) return;
+  if (cnt == 0u) return total;
   uint32_t Aj[K];
   uint32_t par = 0;
 #pragma unroll
@@ -282,11 +282,21 @@ __device__ __forceinline__ void emit_updates(const RoundParams& p, uint32_t wave
     }
   }
   if (ovf) atomicOr(p.log_overflow, 1u);
+  return total;
 }
 
-__device__ __forceinline__ void count_applied(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied) {
+// Per-wave counters: regsiterVote applications (the metric numerator) and the
+// algorithmic bytes this wave moved (state planes actually read/written,
+// gathered vote words, the published word, 8 B per emitted StatusUpdate).
+__device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied,
+                                            bool active, uint32_t bytes_per_lane, uint32_t emitted) {
   const uint32_t s = wave_sum(applied);
-  if (lane == 0 && s) atomicAdd(&p.applied[wave_id % p.log_shards], (unsigned long long)s);
+  const uint32_t nact = (uint32_t)__popcll(__ballot(active));
+  if (lane == 0) {
+    const uint32_t shard = wave_id % p.log_shards;
+    if (s) atomicAdd(&p.applied[shard], (unsigned long long)s);
+    atomicAdd(&p.bytes[shard], (unsigned long long)nact * bytes_per_lane + 8ull * emitted);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -294,21 +304,29 @@ __device__ __forceinline__ void count_applied(const RoundParams& p, uint32_t wav
 // GetInvsForNextPoll never truncates: processor.go:165-167). One lane = one
 // 32-record block; no cross-lane dependence except the emission scan.
 // ---------------------------------------------------------------------------
-template <int K, bool REPLAY>
-__global__ __launch_bounds__(256) void k_round_fast(const RoundParams p) {
-  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63u;
-  if ((g & ~63u) >= p.L) return;  // whole wave beyond the last tile
-  const bool active = g < p.L;
-  const uint32_t nl = active ? g / p.BL : 0u;
-  const uint32_t b = active ? g - nl * p.BL : 0u;
-  const uint32_t node = p.n0 + nl;
-
+// WARM (sim mode only): every consider plane of the wave's blocks is all-ones
+// (each record has seen >= 8 votes and, with no replay / neutral vote ever
+// applied in this engine, every consider bit shifted in was 1). Then the 7
+// younger consider planes are neither loaded nor stored: 176 B per lane
+// instead of 236 B at k=8.
+template <int K, bool REPLAY, bool WARM>
+__device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g, uint32_t lane, bool active,
+                                                uint32_t b, uint32_t node) {
   St s;
-  if (active)
-    load_state(p.planes, g, s);
-  else
+  if (!active) {
     dead_state(s);
+  } else if (WARM) {
+    const uint32_t* t = tile_base(p.planes, g);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.V[i] = t[(kPV + i) * 64];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.C[i] = ~0u;
+    s.A = t[kPA * 64];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s.K[i] = t[(kPK + i) * 64];
+  } else {
+    load_state(p.planes, g, s);
+  }
 
   uint32_t w[K], cw[K];
   if (REPLAY) {
@@ -350,21 +368,51 @@ __global__ __launch_bounds__(256) void k_round_fast(const RoundParams p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         Vo[i] = t[(kPV + i) * 64];
-        Co[i] = t[(kPC + i) * 64];
+        if (!WARM) Co[i] = t[(kPC + i) * 64];
       }
     }
     const uint32_t dead = ~(alive | keep);
+    uint32_t* t = const_cast<uint32_t*>(tile_base(p.planes, g));
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      s.V[i] = (s.V[i] & alive) | (Vo[i] & keep);
-      s.C[i] = (s.C[i] & alive) | (Co[i] & keep) | dead;
+    for (int i = 0; i < 8; ++i) t[(kPV + i) * 64] = (s.V[i] & alive) | (Vo[i] & keep);
+    if (!WARM) {  // WARM: consider planes stay all-ones (dead records are canonical all-ones too)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[(kPC + i) * 64] = (s.C[i] & alive) | (Co[i] & keep) | dead;
     }
-    store_state(p.planes, g, s);
+    t[kPA * 64] = s.A;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[(kPK + i) * 64] = s.K[i];
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
   }
   const uint32_t wave_id = g >> 6;
-  count_applied(p, wave_id, lane, applied);
-  emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
+  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
+  constexpr uint32_t plane_bytes = WARM ? (18u + 17u) * 4u : 2u * kPlanes * 4u;
+  constexpr uint32_t bytes = plane_bytes + (REPLAY ? 8u : 4u) * K + 4u;
+  count_stats(p, wave_id, lane, applied, active, bytes, emitted);
+}
+
+// ---------------------------------------------------------------------------
+// Round kernel, uncapped path (every node has <= 4096 live valid targets, so
+// GetInvsForNextPoll never truncates: processor.go:165-167). One lane = one
+// 32-record block; no cross-lane dependence except the emission scan.
+// ---------------------------------------------------------------------------
+template <int K, bool REPLAY>
+__global__ __launch_bounds__(256) void k_round_fast(const RoundParams p) {
+  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  if ((g & ~63u) >= p.L) return;  // whole wave beyond the last tile
+  const bool active = g < p.L;
+  const uint32_t nl = active ? g / p.BL : 0u;
+  const uint32_t b = active ? g - nl * p.BL : 0u;
+  const uint32_t node = p.n0 + nl;
+  if (!REPLAY && p.warm_skip) {
+    const uint32_t c7 = active ? tile_base(p.planes, g)[(kPC + 7) * 64] : ~0u;
+    if (__all(c7 == ~0u)) {  // wave-uniform
+      round_fast_body<K, false, true>(p, g, lane, active, b, node);
+      return;
+    }
+  }
+  round_fast_body<K, REPLAY, false>(p, g, lane, active, b, node);
 }
 
 // ---------------------------------------------------------------------------
@@ -446,8 +494,8 @@ __global__ __launch_bounds__(1024) void k_round_capped(const RoundParams p) {
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
   }
   const uint32_t wave_id = blockIdx.x * 16u + wave;
-  count_applied(p, wave_id, lane, applied);
-  emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
+  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
+  count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted);
 }
 
 // ---------------------------------------------------------------------------

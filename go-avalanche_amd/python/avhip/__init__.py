@@ -70,7 +70,7 @@ EXPORTED = [
     "av_init_records", "av_add_targets", "av_set_valid", "av_register_votes", "av_is_accepted",
     "av_get_confidence", "av_get_invs", "av_run_rounds", "av_replay_round_errs", "av_replay_prepare",
     "av_replay_rounds", "av_synchronize", "av_round_index", "av_updates_count", "av_fetch_updates",
-    "av_applied_votes", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
+    "av_applied_votes", "av_alg_bytes", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
     "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
 ]
 
@@ -110,6 +110,7 @@ def lib():
         "av_updates_count": (i32, [_vp, P(i64)]),
         "av_fetch_updates": (i32, [_vp, _vp, i64, P(i64)]),
         "av_applied_votes": (i32, [_vp, P(i64)]),
+        "av_alg_bytes": (i32, [_vp, P(i64)]),
         "av_read_records": (i32, [_vp, i64, i64, i64, i64, _vp]),
         "av_write_records": (i32, [_vp, i64, i64, i64, i64, _vp]),
         "av_read_pref": (i32, [_vp, i64, i64, i64, i64, _vp]),
@@ -284,6 +285,11 @@ class Engine:
     def applied_votes(self):
         out = C.c_int64(0)
         _check(lib().av_applied_votes(self._h, C.byref(out)))
+        return out.value
+
+    def alg_bytes(self):
+        out = C.c_int64(0)
+        _check(lib().av_alg_bytes(self._h, C.byref(out)))
         return out.value
 
     def read_records(self, n0=None, n1=None, t0=None, t1=None):

@@ -154,6 +154,10 @@ int av_updates_count(av_engine* e, int64_t* n);
 int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out);
 /* Number of regsiterVote applications (vote.go:54) since creation. */
 int av_applied_votes(av_engine* e, int64_t* out);
+/* Algorithmic bytes moved by the round kernels since creation: state planes
+ * read/written, gathered vote words, published words, 8 B per StatusUpdate
+ * (DESIGN.md §3). */
+int av_alg_bytes(av_engine* e, int64_t* out);
 /* Canonical words for local nodes [n0,n1) x targets [t0,t1) (global ids). */
 int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint32_t* out);
 int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, const uint32_t* in);

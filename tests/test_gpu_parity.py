@@ -261,7 +261,12 @@ def test_c4_shape_properties():
     for _ in range(2):
         e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4)
         e.init_records(avhip.INIT_BERNOULLI, P80)
-        e.run_rounds(16)
+        lanes = e.layout_info()["lanes"]
+        e.run_rounds(1)  # round 0: consider planes fill up (236 B per 32-record lane)
+        assert e.alg_bytes() == lanes * 236 + 8 * e.updates_count()
+        b1, u1 = e.alg_bytes(), e.updates_count()
+        e.run_rounds(15)  # warm: the all-ones consider planes are skipped (176 B per lane)
+        assert e.alg_bytes() - b1 == 15 * lanes * 176 + 8 * (e.updates_count() - u1)
         assert e.applied_votes() == n * m * k * 16
         u = e.fetch_updates()
         assert not np.isin(u[:, 4], [avhip.STATUS_FINALIZED, avhip.STATUS_INVALID]).any()
