@@ -36,6 +36,7 @@ import torch  # noqa: E402  (device plumbing + torch.distributed only)
 import torch.distributed as dist  # noqa: E402
 
 import avhip  # noqa: E402
+from avhip import sharding  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 P80 = int(0.8 * 2**32)
@@ -66,12 +67,6 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     return ap.parse_args()
-
-
-def shard_targets(m, world, rank):
-    blocks = (m + 31) // 32
-    b0, b1 = rank * blocks // world, (rank + 1) * blocks // world
-    return b0 * 32, min(b1 * 32, m)
 
 
 def cpu_baseline(wl, seed, budget_s):
@@ -116,10 +111,9 @@ def main():
         raise SystemExit("target sharding needs M <= 4096 (poll cap couples targets); use --shard nodes")
     kw = dict(k=k, seed=args.seed, byz_threshold=byz, device=local_rank)
     if world > 1 and args.shard == "targets":
-        kw["target_range"] = shard_targets(m, world, rank)
+        kw["target_range"] = sharding.target_shard(m, world, rank)
     elif world > 1:
-        assert n % world == 0, "node sharding needs N % world == 0"
-        kw["node_range"] = (rank * n // world, (rank + 1) * n // world)
+        kw["node_range"] = sharding.node_shard(n, world, rank)
     total_rounds = args.warmup + args.steps
     est_updates = int(0.25 * n * m) + (1 << 20)
     eng = avhip.Engine(n, m, log_capacity=min(est_updates, 1 << 29), **kw)

@@ -364,12 +364,6 @@ void avo_sim_set_valid(avo_sim* s, int64_t t, int valid) { s->valid[t] = (uint8_
 int64_t avo_sim_round_index(const avo_sim* s) { return s->round; }
 int avo_sim_is_byzantine(const avo_sim* s, int64_t node) { return s->byz[node]; }
 
-static void refresh_pref(avo_sim* s) {
-  int64_t n = s->cfg.n_nodes, m = s->cfg.n_targets;
-  for (int64_t j = 0; j < n; ++j)
-    for (int64_t t = 0; t < m; ++t) s->pref[j * m + t] = (uint8_t)published_pref(s->procs[j], t);
-}
-
 int avo_sim_add(avo_sim* s, int64_t node, int64_t t, int accepted) {
   int r = avo_processor_add(s->procs[node], t, accepted, s->valid[t]);
   s->pref[node * s->cfg.n_targets + t] = (uint8_t)published_pref(s->procs[node], t);
@@ -407,6 +401,14 @@ static void upd_push(upd_buf* b, int64_t r, int64_t node, int64_t slot, int64_t 
  * ((r ^ t) & 1) (R4), or the replayed err stream. */
 int avo_sim_round(avo_sim* s, const uint32_t* replay_errs, int64_t* updates, int64_t cap,
                   int64_t* n_out, int32_t threads, int64_t* applied_votes) {
+  return avo_sim_round_range(s, 0, s->cfg.n_nodes, replay_errs, updates, cap, n_out, threads, applied_votes);
+}
+
+/* The same round for nodes [n0, n1) only (a node shard). Only those rows of
+ * the published snapshot are refreshed; the other rows are whatever the
+ * caller installed with avo_sim_set_pref_rows (the exchange step). */
+int avo_sim_round_range(avo_sim* s, int64_t n0, int64_t n1, const uint32_t* replay_errs, int64_t* updates,
+                        int64_t cap, int64_t* n_out, int32_t threads, int64_t* applied_votes) {
   const int64_t n_nodes = s->cfg.n_nodes, m = s->cfg.n_targets;
   const int32_t k = s->cfg.k;
   const int64_t r = s->round;
@@ -417,7 +419,7 @@ int avo_sim_round(avo_sim* s, const uint32_t* replay_errs, int64_t* updates, int
   int nt = threads > 0 ? threads : 1;
 #pragma omp parallel for schedule(dynamic, 4) num_threads(nt) reduction(+ : applied)
 #endif
-  for (int64_t node = 0; node < n_nodes; ++node) {
+  for (int64_t node = n0; node < n1; ++node) {
     avo_processor* p = s->procs[node];
     int64_t* peers = (int64_t*)malloc((size_t)k * sizeof(int64_t));
     int64_t* invs = (int64_t*)malloc(AVO_MAX_ELEMENT_POLL * sizeof(int64_t));
@@ -462,10 +464,15 @@ int avo_sim_round(avo_sim* s, const uint32_t* replay_errs, int64_t* updates, int
   }
   for (int64_t node = 0; node < n_nodes; ++node) free(bufs[node].rows);
   free(bufs);
-  refresh_pref(s);
+  for (int64_t j = n0; j < n1; ++j)
+    for (int64_t t = 0; t < m; ++t) s->pref[j * m + t] = (uint8_t)published_pref(s->procs[j], t);
   if (applied_votes) *applied_votes = applied;
   s->round++;
   return rc;
+}
+
+void avo_sim_set_pref_rows(avo_sim* s, int64_t n0, int64_t n1, const uint8_t* rows) {
+  memcpy(s->pref + n0 * s->cfg.n_targets, rows, (size_t)((n1 - n0) * s->cfg.n_targets));
 }
 
 void avo_sim_dump(const avo_sim* s, uint32_t* out) {

@@ -116,6 +116,11 @@ int64_t avo_sim_round_index(const avo_sim* s);
  * Returns 0, or -1 if cap was too small (n_out then holds the required count). */
 int avo_sim_round(avo_sim* s, const uint32_t* replay_errs, int64_t* updates, int64_t cap,
                   int64_t* n_out, int32_t threads, int64_t* applied_votes);
+/* Node-shard variant: processes nodes [n0, n1) only, refreshing only their
+ * published rows; other rows are installed with avo_sim_set_pref_rows. */
+int avo_sim_round_range(avo_sim* s, int64_t n0, int64_t n1, const uint32_t* replay_errs, int64_t* updates,
+                        int64_t cap, int64_t* n_out, int32_t threads, int64_t* applied_votes);
+void avo_sim_set_pref_rows(avo_sim* s, int64_t n0, int64_t n1, const uint8_t* rows);
 void avo_sim_dump(const avo_sim* s, uint32_t* out /* [N][M] canonical words */);
 void avo_sim_pref(const avo_sim* s, uint8_t* out /* [N][M] published preference */);
 int avo_sim_is_byzantine(const avo_sim* s, int64_t node);

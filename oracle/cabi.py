@@ -56,6 +56,9 @@ def lib():
         L.avo_sim_round_index.argtypes = [C.c_void_p]
         L.avo_sim_round.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                     C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_int64)]
+        L.avo_sim_round_range.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
+                                          C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_int64)]
+        L.avo_sim_set_pref_rows.argtypes = [C.c_void_p, C.c_int64, C.c_int64, u8p]
         L.avo_sim_dump.argtypes = [C.c_void_p, u32p]
         L.avo_sim_pref.argtypes = [C.c_void_p, u8p]
         L.avo_sim_is_byzantine.argtypes = [C.c_void_p, C.c_int64]
@@ -150,6 +153,21 @@ class Sim:
                                  C.byref(applied))
         assert rc == 0, "oracle update buffer too small"
         return buf[: n.value].copy(), applied.value
+
+    def run_round_range(self, n0, n1, threads=1):
+        """Sim-mode round for the node shard [n0, n1) only (node-sharded rehearsal)."""
+        n = C.c_int64(0)
+        applied = C.c_int64(0)
+        cap = (n1 - n0) * self.m * 2 + 16
+        buf = np.empty((cap, 5), np.int64)
+        rc = lib().avo_sim_round_range(self._h, n0, n1, None, buf.ctypes.data_as(C.c_void_p), cap, C.byref(n),
+                                       threads, C.byref(applied))
+        assert rc == 0
+        return buf[: n.value].copy(), applied.value
+
+    def set_pref_rows(self, n0, rows):
+        rows = np.ascontiguousarray(rows, np.uint8)
+        lib().avo_sim_set_pref_rows(self._h, n0, n0 + rows.shape[0], rows)
 
     def dump(self):
         out = np.empty((self.n, self.m), np.uint32)
