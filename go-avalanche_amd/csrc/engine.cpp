@@ -77,6 +77,7 @@ struct av_engine {
   // vote, no write_records): an all-ones oldest consider plane implies all
   // consider planes are all-ones (lets k_round_fast skip them)
   bool c_monotone = true;
+  bool plane_nt = false;  // tuning option "plane_nt"
   std::vector<uint32_t> valid_host;
   // replay stream
   uint32_t* replay = nullptr;
@@ -146,6 +147,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   p.applied = e->applied;
   p.bytes = e->bytes;
   p.warm_skip = e->c_monotone ? 1u : 0u;
+  p.plane_nt = e->plane_nt ? 1u : 0u;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
   p.log_shards = e->log_shards;
@@ -762,6 +764,19 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
                                   e->cfg.peer_mode, static_cast<uint32_t*>(s.p), e->stream));
   AV_HIP(hipMemcpyAsync(out, s.p, n * 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
+int av_set_option(av_engine* e, const char* name, int64_t value) {
+  AV_CHECK(e && name, AV_ERR_INVALID_ARG, "null argument");
+  const std::string n(name);
+  if (n == "plane_nt") {
+    e->plane_nt = value != 0;
+  } else if (n == "warm_skip") {  // may only be switched off (it is a proven invariant, not a hint)
+    if (!value) e->c_monotone = false;
+  } else {
+    return fail(AV_ERR_INVALID_ARG, "unknown option '%s'", name);
+  }
   return AV_OK;
 }
 

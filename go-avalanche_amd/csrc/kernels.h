@@ -55,6 +55,7 @@ struct RoundParams {
   uint32_t round_rel;        // round - log base (update key field)
   int32_t peer_mode;
   uint32_t warm_skip;        // consider planes are monotone (sim votes only): skip all-ones planes
+  uint32_t plane_nt;         // stream state planes with non-temporal loads/stores
 };
 
 // Update-log entry (one StatusUpdate, avalanche.go:59-62):

@@ -50,6 +50,22 @@ __device__ __forceinline__ void philox(uint32_t x[4], uint64_t seed, uint32_t a,
 
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
+// State-plane stream accessors. NT = non-temporal (global_load/store ... nt):
+// the planes are touched once per round, so keeping them out of L2 / the
+// Infinity Cache leaves room for the gathered preference table.
+template <bool NT>
+__device__ __forceinline__ uint32_t pld(const uint32_t* q) {
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  return *q;
+}
+template <bool NT>
+__device__ __forceinline__ void pst(uint32_t* q, uint32_t v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, q);
+  else
+    *q = v;
+}
+
 // Byzantine flip-flop answer: err = ((r ^ t) & 1) ? 1 : 0, so
 // "yes" on even targets in even rounds. Blocks start at multiples of 32.
 __device__ __forceinline__ uint32_t byz_pattern(uint32_t round) { return (round & 1u) ? 0xAAAAAAAAu : 0x55555555u; }
@@ -300,32 +316,28 @@ __device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_
 }
 
 // ---------------------------------------------------------------------------
-// Round kernel, uncapped path (every node has <= 4096 live valid targets, so
-// GetInvsForNextPoll never truncates: processor.go:165-167). One lane = one
-// 32-record block; no cross-lane dependence except the emission scan.
-// ---------------------------------------------------------------------------
+// Body of the uncapped round kernel for one lane (one 32-record block).
 // WARM (sim mode only): every consider plane of the wave's blocks is all-ones
 // (each record has seen >= 8 votes and, with no replay / neutral vote ever
 // applied in this engine, every consider bit shifted in was 1). Then the 7
 // younger consider planes are neither loaded nor stored: 176 B per lane
-// instead of 236 B at k=8.
-template <int K, bool REPLAY, bool WARM>
+// instead of 236 B at k=8. NT: non-temporal plane stream.
+// ---------------------------------------------------------------------------
+template <int K, bool REPLAY, bool WARM, bool NT>
 __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g, uint32_t lane, bool active,
                                                 uint32_t b, uint32_t node) {
   St s;
   if (!active) {
     dead_state(s);
-  } else if (WARM) {
+  } else {
     const uint32_t* t = tile_base(p.planes, g);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s.V[i] = t[(kPV + i) * 64];
+    for (int i = 0; i < 8; ++i) s.V[i] = pld<NT>(t + (kPV + i) * 64);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s.C[i] = ~0u;
-    s.A = t[kPA * 64];
+    for (int i = 0; i < 8; ++i) s.C[i] = WARM ? ~0u : pld<NT>(t + (kPC + i) * 64);
+    s.A = pld<NT>(t + kPA * 64);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s.K[i] = t[(kPK + i) * 64];
-  } else {
-    load_state(p.planes, g, s);
+    for (int i = 0; i < 8; ++i) s.K[i] = pld<NT>(t + (kPK + i) * 64);
   }
 
   uint32_t w[K], cw[K];
@@ -374,14 +386,14 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
     const uint32_t dead = ~(alive | keep);
     uint32_t* t = const_cast<uint32_t*>(tile_base(p.planes, g));
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t[(kPV + i) * 64] = (s.V[i] & alive) | (Vo[i] & keep);
+    for (int i = 0; i < 8; ++i) pst<NT>(t + (kPV + i) * 64, (s.V[i] & alive) | (Vo[i] & keep));
     if (!WARM) {  // WARM: consider planes stay all-ones (dead records are canonical all-ones too)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) t[(kPC + i) * 64] = (s.C[i] & alive) | (Co[i] & keep) | dead;
+      for (int i = 0; i < 8; ++i) pst<NT>(t + (kPC + i) * 64, (s.C[i] & alive) | (Co[i] & keep) | dead);
     }
-    t[kPA * 64] = s.A;
+    pst<NT>(t + kPA * 64, s.A);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t[(kPK + i) * 64] = s.K[i];
+    for (int i = 0; i < 8; ++i) pst<NT>(t + (kPK + i) * 64, s.K[i]);
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
   }
   const uint32_t wave_id = g >> 6;
@@ -408,11 +420,17 @@ __global__ __launch_bounds__(256) void k_round_fast(const RoundParams p) {
   if (!REPLAY && p.warm_skip) {
     const uint32_t c7 = active ? tile_base(p.planes, g)[(kPC + 7) * 64] : ~0u;
     if (__all(c7 == ~0u)) {  // wave-uniform
-      round_fast_body<K, false, true>(p, g, lane, active, b, node);
+      if (p.plane_nt)
+        round_fast_body<K, false, true, true>(p, g, lane, active, b, node);
+      else
+        round_fast_body<K, false, true, false>(p, g, lane, active, b, node);
       return;
     }
   }
-  round_fast_body<K, REPLAY, false>(p, g, lane, active, b, node);
+  if (p.plane_nt)
+    round_fast_body<K, REPLAY, false, true>(p, g, lane, active, b, node);
+  else
+    round_fast_body<K, REPLAY, false, false>(p, g, lane, active, b, node);
 }
 
 // ---------------------------------------------------------------------------

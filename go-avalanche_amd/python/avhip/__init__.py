@@ -71,7 +71,7 @@ EXPORTED = [
     "av_get_confidence", "av_get_invs", "av_run_rounds", "av_replay_round_errs", "av_replay_prepare",
     "av_replay_rounds", "av_synchronize", "av_round_index", "av_updates_count", "av_fetch_updates",
     "av_applied_votes", "av_alg_bytes", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
-    "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
+    "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
 ]
 
 _lib = None
@@ -115,6 +115,7 @@ def lib():
         "av_write_records": (i32, [_vp, i64, i64, i64, i64, _vp]),
         "av_read_pref": (i32, [_vp, i64, i64, i64, i64, _vp]),
         "av_sample_peers": (i32, [_vp, i64, i64, i64, _vp]),
+        "av_set_option": (i32, [_vp, C.c_char_p, i64]),
         "av_set_timing": (i32, [_vp, i32]),
         "av_kernel_stats": (i32, [_vp, P(C.c_double), P(i64)]),
         "av_layout_info": (i32, [_vp, P(i64), P(i64), P(i64), P(i32)]),
@@ -321,7 +322,10 @@ class Engine:
         _check(lib().av_sample_peers(self._h, rnd, n0, n1, _ptr(out)))
         return out
 
-    # ---- measurement ----
+    # ---- measurement / tuning ----
+    def set_option(self, name, value):
+        _check(lib().av_set_option(self._h, name.encode(), int(value)))
+
     def set_timing(self, enable=True):
         _check(lib().av_set_timing(self._h, int(enable)))
 

@@ -166,6 +166,11 @@ int av_read_pref(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, u
 /* Device peer sampling dump: peers of nodes [n0,n1) in round `round`, [n][k]. */
 int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t* out);
 
+/* ---- tuning ----
+ * "plane_nt"  (0/1): stream the state planes with non-temporal loads/stores.
+ * "warm_skip" (0)  : disable skipping all-ones consider planes (A/B only). */
+int av_set_option(av_engine* e, const char* name, int64_t value);
+
 /* ---- measurement ---- */
 /* HIP-event timing of every round kernel launch on the engine stream. */
 int av_set_timing(av_engine* e, int32_t enable);

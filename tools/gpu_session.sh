@@ -31,6 +31,7 @@ for s in "$@"; do
     tests) step pytest_gpu 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py ;;
+    ab) step ab 900 python tools/ab_tune.py --json $OUT/ab.json ;;
     bench_c2) step bench_c2 900 python bench.py --workload c2 --no-cpu-baseline ;;
     bench_c3) step bench_c3 900 python bench.py --workload c3 --no-cpu-baseline ;;
     bench_c5) step bench_c5 900 python bench.py --workload c5 --no-cpu-baseline ;;
