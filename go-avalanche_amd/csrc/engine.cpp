@@ -72,6 +72,8 @@ struct av_engine {
   uint32_t log_shards = 1;
   unsigned long long* applied = nullptr;
   unsigned long long* bytes = nullptr;
+  unsigned long long* finalized = nullptr;
+  unsigned long long* scratch_count = nullptr;
   int64_t round = 0, log_base = 0;
   // every consider bit ever shifted in was 1 (no replay, no neutral drop-in
   // vote, no write_records): an all-ones oldest consider plane implies all
@@ -146,6 +148,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   p.log_overflow = e->log_overflow;
   p.applied = e->applied;
   p.bytes = e->bytes;
+  p.finalized = e->finalized;
   p.warm_skip = e->c_monotone ? 1u : 0u;
   p.plane_nt = e->plane_nt ? 1u : 0u;
   p.seed = e->cfg.seed;
@@ -228,7 +231,7 @@ int av_destroy(av_engine* e) {
   }
   if (e->comm) (void)ncclCommDestroy(e->comm);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->valid, e->byz, e->log, e->log_count, e->log_overflow,
-                  e->applied, e->bytes, e->replay};
+                  e->applied, e->bytes, e->finalized, e->scratch_count, e->replay};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -304,6 +307,9 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->applied, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
   if ((he = dev_alloc(&e->bytes, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
   (void)hipMemsetAsync(e->bytes, 0, avk::kLogShards * 8, e->stream);
+  if ((he = dev_alloc(&e->finalized, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
+  (void)hipMemsetAsync(e->finalized, 0, avk::kLogShards * 8, e->stream);
+  if ((he = dev_alloc(&e->scratch_count, 1)) != hipSuccess) return hip_fail(he, "alloc counters");
   (void)hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
   (void)hipMemsetAsync(e->applied, 0, avk::kLogShards * 8, e->stream);
@@ -718,6 +724,44 @@ int av_applied_votes(av_engine* e, int64_t* out) {
   unsigned long long t = 0;
   for (auto v : c) t += v;
   *out = (int64_t)t;
+  return AV_OK;
+}
+
+static int sum_counter(av_engine* e, const unsigned long long* dev, int64_t* out) {
+  std::vector<unsigned long long> c(avk::kLogShards);
+  AV_HIP(hipMemcpyAsync(c.data(), dev, avk::kLogShards * 8, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  unsigned long long t = 0;
+  for (auto v : c) t += v;
+  *out = (int64_t)t;
+  return AV_OK;
+}
+
+int av_finalized_count(av_engine* e, int64_t* out) {
+  AV_ENTER(e);
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  return sum_counter(e, e->finalized, out);
+}
+
+int av_live_records(av_engine* e, int32_t honest_only, int64_t* out) {
+  AV_ENTER(e);
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  AV_HIP(hipMemsetAsync(e->scratch_count, 0, 8, e->stream));
+  AV_HIP(avk::launch_count_live(e->planes, e->valid, e->byz, (uint32_t)e->n0, e->BL, e->L, honest_only,
+                                e->scratch_count, e->stream));
+  unsigned long long v = 0;
+  AV_HIP(hipMemcpyAsync(&v, e->scratch_count, 8, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  *out = (int64_t)v;
+  return AV_OK;
+}
+
+int av_discard_updates(av_engine* e) {
+  AV_ENTER(e);
+  AV_HIP(hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream));
+  AV_HIP(hipMemsetAsync(e->log_overflow, 0, 4, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  e->log_base = e->round;
   return AV_OK;
 }
 

@@ -41,6 +41,7 @@ struct RoundParams {
   uint32_t* log_overflow;    // [1]
   unsigned long long* applied;  // [kLogShards] regsiterVote applications
   unsigned long long* bytes;    // [kLogShards] algorithmic bytes moved by the round kernel
+  unsigned long long* finalized;  // [kLogShards] records finalized (deleted, processor.go:114-116)
   uint64_t seed;
   uint32_t log_cap;          // entries per shard
   uint32_t log_shards;       // shards in use (<= kLogShards; min(waves, kLogShards))
@@ -117,6 +118,8 @@ hipError_t launch_sample_peers(uint64_t seed, uint32_t n_nodes, uint32_t a, uint
 hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t BL, uint32_t L, uint32_t Lpad,
                              uint32_t t0, uint32_t n_targets, uint32_t round, int k, uint32_t* out,
                              hipStream_t s);
+hipError_t launch_count_live(const uint32_t* planes, const uint32_t* valid, const uint32_t* byz, uint32_t n0,
+                             uint32_t BL, uint32_t L, int honest_only, unsigned long long* out, hipStream_t s);
 hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets,
                               uint32_t log_cap, uint32_t shards, uint64_t* out, hipStream_t s);
 

@@ -13,6 +13,8 @@
 // kernels are HBM-bound streaming kernels (DESIGN.md "Roofline").
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace avk {
@@ -305,12 +307,14 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
 // algorithmic bytes this wave moved (state planes actually read/written,
 // gathered vote words, the published word, 8 B per emitted StatusUpdate).
 __device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied,
-                                            bool active, uint32_t bytes_per_lane, uint32_t emitted) {
+                                            bool active, uint32_t bytes_per_lane, uint32_t emitted, uint32_t died) {
   const uint32_t s = wave_sum(applied);
+  const uint32_t f = wave_sum(__popc(died));
   const uint32_t nact = (uint32_t)__popcll(__ballot(active));
   if (lane == 0) {
     const uint32_t shard = wave_id % p.log_shards;
     if (s) atomicAdd(&p.applied[shard], (unsigned long long)s);
+    if (f) atomicAdd(&p.finalized[shard], (unsigned long long)f);
     atomicAdd(&p.bytes[shard], (unsigned long long)nact * bytes_per_lane + 8ull * emitted);
   }
 }
@@ -400,7 +404,7 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
   const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
   constexpr uint32_t plane_bytes = WARM ? (18u + 17u) * 4u : 2u * kPlanes * 4u;
   constexpr uint32_t bytes = plane_bytes + (REPLAY ? 8u : 4u) * K + 4u;
-  count_stats(p, wave_id, lane, applied, active, bytes, emitted);
+  count_stats(p, wave_id, lane, applied, active, bytes, emitted, died);
 }
 
 // ---------------------------------------------------------------------------
@@ -513,7 +517,7 @@ __global__ __launch_bounds__(1024) void k_round_capped(const RoundParams p) {
   }
   const uint32_t wave_id = blockIdx.x * 16u + wave;
   const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
-  count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted);
+  count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted, died);
 }
 
 // ---------------------------------------------------------------------------
@@ -763,6 +767,23 @@ __global__ void k_gen_replay(uint64_t seed, uint32_t n0, uint32_t BL, uint32_t L
   }
 }
 
+// Live valid records (optionally of honest nodes only): the convergence
+// measure for rounds-to-finalization. Grid-stride, one atomic per block.
+__global__ void k_count_live(const uint32_t* planes, const uint32_t* valid, const uint32_t* byz, uint32_t n0,
+                             uint32_t BL, uint32_t L, int honest_only, unsigned long long* out) {
+  __shared__ unsigned long long part[4];
+  unsigned long long c = 0;
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < L; g += gridDim.x * blockDim.x) {
+    const uint32_t nl = g / BL, b = g - nl * BL;
+    if (honest_only && is_byz(byz, n0 + nl)) continue;
+    c += __popc(~tile_base(planes, g)[(kPK + 7) * 64] & valid[b]);
+  }
+  const uint32_t w = wave_sum((uint32_t)c);  // <= 32 * 64 per wave per pass: fits u32
+  if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
+}
+
 __global__ void k_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets, uint32_t log_cap,
                               uint64_t* out) {
   const uint32_t shard = blockIdx.x;
@@ -893,6 +914,14 @@ hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t B
   if (!Lpad) return hipSuccess;
   hipLaunchKernelGGL(k_gen_replay, dim3((Lpad + 255) / 256), dim3(256), 0, s, seed, n0, BL, L, Lpad, t0, n_targets,
                      round, k, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_count_live(const uint32_t* planes, const uint32_t* valid, const uint32_t* byz, uint32_t n0,
+                             uint32_t BL, uint32_t L, int honest_only, unsigned long long* out, hipStream_t s) {
+  if (!L) return hipSuccess;
+  const uint32_t blocks = std::min<uint32_t>(2048u, (L + 255u) / 256u);
+  hipLaunchKernelGGL(k_count_live, dim3(blocks), dim3(256), 0, s, planes, valid, byz, n0, BL, L, honest_only, out);
   return hipGetLastError();
 }
 

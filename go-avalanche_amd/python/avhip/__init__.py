@@ -70,7 +70,7 @@ EXPORTED = [
     "av_init_records", "av_add_targets", "av_set_valid", "av_register_votes", "av_is_accepted",
     "av_get_confidence", "av_get_invs", "av_run_rounds", "av_replay_round_errs", "av_replay_prepare",
     "av_replay_rounds", "av_synchronize", "av_round_index", "av_updates_count", "av_fetch_updates",
-    "av_applied_votes", "av_alg_bytes", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
+    "av_applied_votes", "av_alg_bytes", "av_finalized_count", "av_live_records", "av_discard_updates", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
 ]
 
@@ -111,6 +111,9 @@ def lib():
         "av_fetch_updates": (i32, [_vp, _vp, i64, P(i64)]),
         "av_applied_votes": (i32, [_vp, P(i64)]),
         "av_alg_bytes": (i32, [_vp, P(i64)]),
+        "av_finalized_count": (i32, [_vp, P(i64)]),
+        "av_live_records": (i32, [_vp, i32, P(i64)]),
+        "av_discard_updates": (i32, [_vp]),
         "av_read_records": (i32, [_vp, i64, i64, i64, i64, _vp]),
         "av_write_records": (i32, [_vp, i64, i64, i64, i64, _vp]),
         "av_read_pref": (i32, [_vp, i64, i64, i64, i64, _vp]),
@@ -287,6 +290,20 @@ class Engine:
         out = C.c_int64(0)
         _check(lib().av_applied_votes(self._h, C.byref(out)))
         return out.value
+
+    def finalized_count(self):
+        out = C.c_int64(0)
+        _check(lib().av_finalized_count(self._h, C.byref(out)))
+        return out.value
+
+    def live_records(self, honest_only=False):
+        out = C.c_int64(0)
+        _check(lib().av_live_records(self._h, int(honest_only), C.byref(out)))
+        return out.value
+
+    def discard_updates(self):
+        _check(lib().av_discard_updates(self._h))
+        self._log_base = self.round
 
     def alg_bytes(self):
         out = C.c_int64(0)

@@ -154,6 +154,12 @@ int av_updates_count(av_engine* e, int64_t* n);
 int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out);
 /* Number of regsiterVote applications (vote.go:54) since creation. */
 int av_applied_votes(av_engine* e, int64_t* out);
+/* Records deleted after finalization by round kernels since creation. */
+int av_finalized_count(av_engine* e, int64_t* out);
+/* Live valid records now (honest_only: skip Byzantine nodes). */
+int av_live_records(av_engine* e, int32_t honest_only, int64_t* out);
+/* Drop pending StatusUpdates without copying them (long convergence runs). */
+int av_discard_updates(av_engine* e);
 /* Algorithmic bytes moved by the round kernels since creation: state planes
  * read/written, gathered vote words, published words, 8 B per StatusUpdate
  * (DESIGN.md §3). */

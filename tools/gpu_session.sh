@@ -32,6 +32,9 @@ for s in "$@"; do
     testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py ;;
     ab) step ab 900 python tools/ab_tune.py --json $OUT/ab.json ;;
+    conv_c3) step conv_c3 900 python tools/run_to_finalization.py --workload c3 --json $OUT/conv_c3.json ;;
+    conv_c5) step conv_c5 900 python tools/run_to_finalization.py --workload c5 --max-rounds 64 --json $OUT/conv_c5.json ;;
+    conv_c4) step conv_c4 900 python tools/run_to_finalization.py --workload c4 --max-rounds 64 --json $OUT/conv_c4.json ;;
     bench_c2) step bench_c2 900 python bench.py --workload c2 --no-cpu-baseline ;;
     bench_c3) step bench_c3 900 python bench.py --workload c3 --no-cpu-baseline ;;
     bench_c5) step bench_c5 900 python bench.py --workload c5 --no-cpu-baseline ;;
