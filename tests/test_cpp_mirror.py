@@ -14,6 +14,15 @@ def test_cpp_mirror_binary_built():
 
 
 @pytest.mark.gpu
+def test_example_basic_preconsensus():
+    """examples/basic-preconcensus (C1) on the engine: every node finalizes every tx."""
+    exe = os.path.join(ROOT, "go-avalanche_amd", "bin", "basic_preconsensus")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Nodes fully finalized: 100" in r.stdout
+
+
+@pytest.mark.gpu
 def test_cpp_mirror_reference_tests():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     print(r.stdout, r.stderr)
