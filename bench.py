@@ -7,18 +7,19 @@
 One *step* = one synchronous round of go-avalanche's poll loop for every
 simulated node: k peers sampled per node, k Responses
 registered, VoteRecord updates (vote.go:54-91) and StatusUpdate emission
-(processor.go:111). Inputs (records, preferences) are resident in HBM before
-the timed region starts.
+(processor.go:111). Inputs (records, preferences, replayed votes) are resident
+in HBM before the timed region starts.
 
 metric : vote-record updates/s = regsiterVote applications on live records
          (vote.go:54) per second, whole job (all ranks). triples/s (node, target,
          round) = updates/s / k is reported beside it.
-workload (N=1 default) : C4 of BASELINE.json — 1M nodes x 1000 targets, k=8,
+workload : C4 of BASELINE.json (the north_star's 1M nodes x 1k targets) — k=8,
          IsAccepted() ~ Bernoulli(0.8), honest, synthetic (seeded), rounds
-         W..W+K-1 (< 17: every record stays live). With N GPUs the same
-         network is split by target blocks (no per-round exchange; strong
-         scaling) or, with --shard nodes, by nodes with an RCCL all-gather of
-         the published preferences every round.
+         W..W+K-1 (< 17: every record stays live). With N GPUs the same network
+         is split by target blocks (no per-round exchange; strong scaling) or,
+         with --shard nodes, by nodes with an RCCL all-gather of the published
+         preferences every round. At N=1 the line also carries configs[1] (C2:
+         replayed vote streams, 4096 poll cap binding) under "secondary".
 """
 from __future__ import annotations
 
@@ -55,7 +56,6 @@ WORKLOADS = {
 }
 
 
-
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -65,7 +65,9 @@ def parse():
     ap.add_argument("--shard", default="targets", choices=["targets", "nodes"])
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xA7A1A9C4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--plane-nt", type=int, default=None, help="override the plane_nt tuning option")
     return ap.parse_args()
 
 
@@ -95,18 +97,11 @@ def cpu_baseline(wl, seed, budget_s):
                       f"({applied} regsiterVote applications, {dt:.1f}s, OpenMP over nodes)"}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
-    n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[args.workload]
+def measure(wl, args, world, rank, local_rank, steps, warmup):
+    """Build the workload's engine (this rank's shard), run `warmup` untimed and
+    `steps` timed rounds; return whole-job numbers (max time, summed work) and
+    rank-local kernel numbers."""
+    n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
     if args.shard == "targets" and world > 1 and m > 4096:
         raise SystemExit("target sharding needs M <= 4096 (poll cap couples targets); use --shard nodes")
     kw = dict(k=k, seed=args.seed, byz_threshold=byz, device=local_rank)
@@ -114,36 +109,36 @@ def main():
         kw["target_range"] = sharding.target_shard(m, world, rank)
     elif world > 1:
         kw["node_range"] = sharding.node_shard(n, world, rank)
-    total_rounds = args.warmup + args.steps
     est_updates = int(0.25 * n * m) + (1 << 20)
     eng = avhip.Engine(n, m, log_capacity=min(est_updates, 1 << 29), **kw)
+    if args.plane_nt is not None:
+        eng.set_option("plane_nt", args.plane_nt)
     eng.init_records(init_mode, init_param)
     if world > 1 and args.shard == "nodes":
         obj = [avhip.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(world, rank, obj[0])
     if replay:
-        eng.replay_prepare(total_rounds)
+        eng.replay_prepare(warmup + steps)
     run = eng.replay_rounds if replay else eng.run_rounds
     info = eng.layout_info()
 
     # ---- warmup (untimed), then drain the StatusUpdate log
-    run(args.warmup)
+    run(warmup)
     eng.synchronize()
     try:  # drain what the warmup emitted (the timed region starts with an empty log)
         eng.fetch_updates(decode=False)
     except avhip.LogOverflow:
         pass  # the log is cleared on overflow; warmup updates are not measured
-    applied0 = eng.applied_votes()
-    bytes0 = eng.alg_bytes()
+    applied0, bytes0 = eng.applied_votes(), eng.alg_bytes()
 
-    # ---- timed region: K rounds
+    # ---- timed region
     eng.set_timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.steps)
+    run(steps)
     eng.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -156,24 +151,55 @@ def main():
     # algorithmic bytes per launch, counted by the round kernel itself (planes
     # actually streamed, gathered vote words, published words, StatusUpdates)
     alg_bytes = (eng.alg_bytes() - bytes0) / max(launches, 1)
+    kavg_ms = kern_ms / max(launches, 1)
+    eng.close()
 
-    stats = torch.tensor([elapsed, float(applied), float(emitted), kern_ms / max(launches, 1),
-                          float(alg_bytes)], dtype=torch.float64, device="cuda")
     if world > 1:
-        tmax = stats[0].clone()
+        st = torch.tensor([elapsed, float(applied), float(emitted)], dtype=torch.float64, device="cuda")
+        tmax = st[0:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tot = stats[1:3].clone()
+        tot = st[1:3].clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         elapsed, applied, emitted = float(tmax), float(tot[0]), float(tot[1])
-    kavg_ms = float(stats[3])  # this rank's (rank 0's) round-kernel average, HIP events on the engine stream
+    value = applied / elapsed
+    # roofline of this rank's round kernel: algorithmic bytes per
+    # launch (236 B per 32-record lane at k=8, 176 B once the consider planes
+    # are warm, + 8 B per StatusUpdate) / its HIP-event average launch time.
+    achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
+    kname = ("k_round_capped" if info["capped"] else "k_round_fast") + f"<{k},{'true' if replay else 'false'}>"
+    return {
+        "desc": desc, "n": n, "m": m, "k": k, "value": value, "elapsed": elapsed, "applied": applied,
+        "emitted": emitted, "info": info, "kavg_ms": kavg_ms, "alg_bytes": alg_bytes, "achieved": achieved,
+        "kernel": kname,
+    }
+
+
+def roofline(r, traffic=None):
+    return {"bound": "hbm", "achieved": r["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": r["achieved"] / HBM_PEAK_GBS, "traffic": traffic, "kernel": r["kernel"],
+            "kernel_ms_avg": r["kavg_ms"], "alg_bytes_per_launch": r["alg_bytes"]}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    r = measure(args.workload, args, world, rank, local_rank, args.steps, args.warmup)
+    secondary = None
+    if world == 1 and not args.no_secondary and args.workload != "c2":
+        c2 = measure("c2", args, world, rank, local_rank, 14, 2)
+        secondary = {"c2": {"workload": c2["desc"], "value": c2["value"], "unit": "vote-record updates/s",
+                            "ms_per_step": c2["elapsed"] / 14 * 1e3, "rounds": "2..15",
+                            "roofline": roofline(c2)}}
 
     if rank == 0:
-        value = applied / elapsed
-        # roofline of rank 0's round kernel: its algorithmic bytes
-        # per launch (counted by the kernel: 236 B per 32-record lane at k=8, 176 B
-        # once the consider planes are warm, + 8 B per StatusUpdate) / its
-        # average launch time.
-        achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
         if world == 1 and os.path.exists(pmc_path):
@@ -181,44 +207,34 @@ def main():
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         line = {
             "metric": "vote-record updates/sec (node·target·round) at 1/2/4/8 GPU; % HBM roofline",
-            "value": value,
+            "value": r["value"],
             "unit": "vote-record updates/s (1 update = 1 regsiterVote on a live record; k=8 per node·target·round)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": r["elapsed"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (seeded Philox4x32-10 network; no dataset)",
             "config": {
-                "workload": desc,
-                "n_nodes": n, "n_targets": m, "k": k,
-                "rounds": f"{args.warmup}..{total_rounds - 1}",
+                "workload": r["desc"],
+                "n_nodes": r["n"], "n_targets": r["m"], "k": r["k"],
+                "rounds": f"{args.warmup}..{args.warmup + args.steps - 1}",
                 "parallelism": f"{args.shard}-sharded x{world}" if world > 1 else "single GPU",
                 "layout": "bit-sliced: 25 u32 planes per 32 records; tile of 64 lanes contiguous",
-                "capped_poll_path": info["capped"],
+                "capped_poll_path": r["info"]["capped"],
             },
-            "triples_per_s": value / k,
-            "updates_emitted": int(emitted),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "kernel": "k_round_fast<8,%s>" % ("true" if replay else "false") if not info["capped"] else
-                          "k_round_capped<8,%s>" % ("true" if replay else "false"),
-                "kernel_ms_avg": kavg_ms,
-                "alg_bytes_per_launch": alg_bytes,
-            },
+            "triples_per_s": r["value"] / r["k"],
+            "updates_emitted": int(r["emitted"]),
+            "roofline": roofline(r, traffic),
         }
+        if secondary:
+            line["secondary"] = secondary
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args.workload, args.seed, args.cpu_seconds)
         print(json.dumps(line), flush=True)
-    eng.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
