@@ -20,8 +20,10 @@ namespace avk {
 //           never added). A dead record keeps A = published decision.
 // A *lane* is one (local node, local block) pair, g = node_local * BL + b.
 // Lanes are grouped in tiles of 64 (one wavefront); a tile stores its 25
-// planes contiguously: word(g, p) = planes[((g >> 6) * 25 + p) * 64 + (g & 63)]
-// so one wave reads/writes one contiguous 6400-byte span per round.
+// planes in one contiguous 6400-byte span (plane_off() in kernels.hip):
+// V0-3, V4-7, K0-3, K4-7 as lane-interleaved 16-byte groups (one dwordx4 per
+// lane = 1 KiB contiguous per wave-instruction), then C0..C7 and A as dword
+// planes (256 B per wave-instruction).
 // ---------------------------------------------------------------------------
 constexpr int kPlanes = 25;
 constexpr int kPV = 0, kPC = 8, kPA = 16, kPK = 17;

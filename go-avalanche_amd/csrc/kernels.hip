@@ -67,6 +67,19 @@ __device__ __forceinline__ void pst(uint32_t* q, uint32_t v) {
   else
     *q = v;
 }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ u32x4 pld4(const u32x4* q) {
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  return *q;
+}
+template <bool NT>
+__device__ __forceinline__ void pst4(u32x4* q, u32x4 v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, q);
+  else
+    *q = v;
+}
 
 // Byzantine flip-flop answer: err = ((r ^ t) & 1) ? 1 : 0, so
 // "yes" on even targets in even rounds. Blocks start at multiples of 32.
@@ -78,30 +91,46 @@ struct St {
   uint32_t V[8], C[8], A, K[8];
 };
 
-__device__ __forceinline__ const uint32_t* tile_base(const uint32_t* planes, uint32_t g) {
-  return planes + (size_t)(g >> 6) * (kPlanes * 64) + (g & 63u);
+// Tile layout (1600 words = 6400 B per 64 lanes), see kernels.h:
+//   [0,1024)    V0-3 | V4-7 | K0-3 | K4-7 as 16-byte groups, lane-interleaved:
+//               group q, lane l, plane i -> q*256 + l*4 + i  (one dwordx4 per
+//               lane, 1 KiB contiguous per wave-instruction)
+//   [1024,1536) C0..C7 dword planes: 1024 + c*64 + l
+//   [1536,1600) A dword plane:       1536 + l
+__host__ __device__ constexpr uint32_t plane_off(int p, uint32_t lane) {
+  return p < kPC ? (uint32_t)(p >> 2) * 256u + lane * 4u + (uint32_t)(p & 3)
+       : p < kPA ? 1024u + (uint32_t)(p - kPC) * 64u + lane
+       : p == kPA ? 1536u + lane
+       : (uint32_t)(2 + ((p - kPK) >> 2)) * 256u + lane * 4u + (uint32_t)((p - kPK) & 3);
+}
+
+__device__ __forceinline__ uint32_t* tile_of(const uint32_t* planes, uint32_t g) {
+  return const_cast<uint32_t*>(planes) + (size_t)(g >> 6) * (kPlanes * 64);
+}
+
+// pointer to the word of plane p for lane g
+__device__ __forceinline__ uint32_t* pw(const uint32_t* planes, uint32_t g, int p) {
+  return tile_of(planes, g) + plane_off(p, g & 63u);
 }
 
 __device__ __forceinline__ void load_state(const uint32_t* planes, uint32_t g, St& s) {
-  const uint32_t* t = tile_base(planes, g);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s.V[i] = t[(kPV + i) * 64];
+  for (int i = 0; i < 8; ++i) s.V[i] = *pw(planes, g, kPV + i);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s.C[i] = t[(kPC + i) * 64];
-  s.A = t[kPA * 64];
+  for (int i = 0; i < 8; ++i) s.C[i] = *pw(planes, g, kPC + i);
+  s.A = *pw(planes, g, kPA);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s.K[i] = t[(kPK + i) * 64];
+  for (int i = 0; i < 8; ++i) s.K[i] = *pw(planes, g, kPK + i);
 }
 
 __device__ __forceinline__ void store_state(uint32_t* planes, uint32_t g, const St& s) {
-  uint32_t* t = const_cast<uint32_t*>(tile_base(planes, g));
 #pragma unroll
-  for (int i = 0; i < 8; ++i) t[(kPV + i) * 64] = s.V[i];
+  for (int i = 0; i < 8; ++i) *pw(planes, g, kPV + i) = s.V[i];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) t[(kPC + i) * 64] = s.C[i];
-  t[kPA * 64] = s.A;
+  for (int i = 0; i < 8; ++i) *pw(planes, g, kPC + i) = s.C[i];
+  *pw(planes, g, kPA) = s.A;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) t[(kPK + i) * 64] = s.K[i];
+  for (int i = 0; i < 8; ++i) *pw(planes, g, kPK + i) = s.K[i];
 }
 
 // No live record in any of the 32 slots (canonical dead form).
@@ -331,17 +360,22 @@ template <int K, bool REPLAY, bool WARM, bool NT>
 __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g, uint32_t lane, bool active,
                                                 uint32_t b, uint32_t node) {
   St s;
+  uint32_t* const tile = tile_of(p.planes, g);
+  u32x4* const grp = reinterpret_cast<u32x4*>(tile) + lane;  // V0-3, V4-7, K0-3, K4-7 at +0, +64, +128, +192
   if (!active) {
     dead_state(s);
   } else {
-    const uint32_t* t = tile_base(p.planes, g);
+    const u32x4 v0 = pld4<NT>(grp), v1 = pld4<NT>(grp + 64), k0 = pld4<NT>(grp + 128), k1 = pld4<NT>(grp + 192);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s.V[i] = pld<NT>(t + (kPV + i) * 64);
+    for (int i = 0; i < 4; ++i) {
+      s.V[i] = v0[i];
+      s.V[4 + i] = v1[i];
+      s.K[i] = k0[i];
+      s.K[4 + i] = k1[i];
+    }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s.C[i] = WARM ? ~0u : pld<NT>(t + (kPC + i) * 64);
-    s.A = pld<NT>(t + kPA * 64);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s.K[i] = pld<NT>(t + (kPK + i) * 64);
+    for (int i = 0; i < 8; ++i) s.C[i] = WARM ? ~0u : pld<NT>(tile + plane_off(kPC + i, lane));
+    s.A = pld<NT>(tile + plane_off(kPA, lane));
   }
 
   uint32_t w[K], cw[K];
@@ -380,24 +414,30 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
 #pragma unroll
     for (int i = 0; i < 8; ++i) Vo[i] = Co[i] = 0u;
     if (keep) {
-      const uint32_t* t = tile_base(p.planes, g);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        Vo[i] = t[(kPV + i) * 64];
-        if (!WARM) Co[i] = t[(kPC + i) * 64];
+        Vo[i] = tile[plane_off(kPV + i, lane)];
+        if (!WARM) Co[i] = tile[plane_off(kPC + i, lane)];
       }
     }
     const uint32_t dead = ~(alive | keep);
-    uint32_t* t = const_cast<uint32_t*>(tile_base(p.planes, g));
+    u32x4 v0, v1, k0, k1;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) pst<NT>(t + (kPV + i) * 64, (s.V[i] & alive) | (Vo[i] & keep));
+    for (int i = 0; i < 4; ++i) {
+      v0[i] = (s.V[i] & alive) | (Vo[i] & keep);
+      v1[i] = (s.V[4 + i] & alive) | (Vo[4 + i] & keep);
+      k0[i] = s.K[i];
+      k1[i] = s.K[4 + i];
+    }
+    pst4<NT>(grp, v0);
+    pst4<NT>(grp + 64, v1);
+    pst4<NT>(grp + 128, k0);
+    pst4<NT>(grp + 192, k1);
     if (!WARM) {  // WARM: consider planes stay all-ones (dead records are canonical all-ones too)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) pst<NT>(t + (kPC + i) * 64, (s.C[i] & alive) | (Co[i] & keep) | dead);
+      for (int i = 0; i < 8; ++i) pst<NT>(tile + plane_off(kPC + i, lane), (s.C[i] & alive) | (Co[i] & keep) | dead);
     }
-    pst<NT>(t + kPA * 64, s.A);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) pst<NT>(t + (kPK + i) * 64, s.K[i]);
+    pst<NT>(tile + plane_off(kPA, lane), s.A);
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
   }
   const uint32_t wave_id = g >> 6;
@@ -422,7 +462,7 @@ __global__ __launch_bounds__(256) void k_round_fast(const RoundParams p) {
   const uint32_t b = active ? g - nl * p.BL : 0u;
   const uint32_t node = p.n0 + nl;
   if (!REPLAY && p.warm_skip) {
-    const uint32_t c7 = active ? tile_base(p.planes, g)[(kPC + 7) * 64] : ~0u;
+    const uint32_t c7 = active ? *pw(p.planes, g, kPC + 7) : ~0u;
     if (__all(c7 == ~0u)) {  // wave-uniform
       if (p.plane_nt)
         round_fast_body<K, false, true, true>(p, g, lane, active, b, node);
@@ -563,21 +603,21 @@ __global__ void k_add_targets(const AddParams p) {
     const uint32_t t = p.targets[i];
     const uint32_t b = t >> 5, m = 1u << (t & 31u);
     const uint32_t g = p.node_local * p.BL + b;
-    uint32_t* base = const_cast<uint32_t*>(tile_base(p.planes, g));
-    const bool valid = (p.valid[b] & m) != 0u;       // isWorthyPolling (:46-48)
-    const bool exists = (base[(kPK + 7) * 64] & m) == 0u;  // record present (:50-53)
+    const bool valid = (p.valid[b] & m) != 0u;               // isWorthyPolling (:46-48)
+    const bool exists = (*pw(p.planes, g, kPK + 7) & m) == 0u;  // record present (:50-53)
     if (!valid || exists) {
       p.added[i] = 0;
       continue;
     }
     for (int q = 0; q < 8; ++q) {  // NewVoteRecord(t.IsAccepted()) (vote.go:33-35)
-      base[(kPV + q) * 64] &= ~m;
-      base[(kPC + q) * 64] &= ~m;
-      base[(kPK + q) * 64] &= ~m;
+      *pw(p.planes, g, kPV + q) &= ~m;
+      *pw(p.planes, g, kPC + q) &= ~m;
+      *pw(p.planes, g, kPK + q) &= ~m;
     }
-    base[kPA * 64] = p.accepted[i] ? (base[kPA * 64] | m) : (base[kPA * 64] & ~m);
+    uint32_t* a = pw(p.planes, g, kPA);
+    *a = p.accepted[i] ? (*a | m) : (*a & ~m);
     p.added[i] = 1;
-    p.pref[(size_t)p.node * p.BL + b] = is_byz(p.byz, p.node) ? byz_pattern(p.round) : base[kPA * 64];
+    p.pref[(size_t)p.node * p.BL + b] = is_byz(p.byz, p.node) ? byz_pattern(p.round) : *a;
   }
 }
 
@@ -668,20 +708,19 @@ __global__ void k_read_records(const uint32_t* planes, uint32_t BL, uint32_t nl0
   if (i >= (size_t)(nl1 - nl0) * W) return;
   const uint32_t nl = nl0 + (uint32_t)(i / W), tl = tl0 + (uint32_t)(i % W);
   const uint32_t g = nl * BL + (tl >> 5), bit = tl & 31u;
-  const uint32_t* t = tile_base(planes, g);
-  const uint32_t a = (t[kPA * 64] >> bit) & 1u;
-  if ((t[(kPK + 7) * 64] >> bit) & 1u) {
+  const uint32_t a = (*pw(planes, g, kPA) >> bit) & 1u;
+  if ((*pw(planes, g, kPK + 7) >> bit) & 1u) {
     out[i] = 0xFFFE0000u | (a << 16);
     return;
   }
   uint32_t v = 0, c = 0, k = 0;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    v |= ((t[(kPV + q) * 64] >> bit) & 1u) << q;
-    c |= ((t[(kPC + q) * 64] >> bit) & 1u) << q;
+    v |= ((*pw(planes, g, kPV + q) >> bit) & 1u) << q;
+    c |= ((*pw(planes, g, kPC + q) >> bit) & 1u) << q;
   }
 #pragma unroll
-  for (int q = 0; q < 7; ++q) k |= ((t[(kPK + q) * 64] >> bit) & 1u) << q;
+  for (int q = 0; q < 7; ++q) k |= ((*pw(planes, g, kPK + q) >> bit) & 1u) << q;
   out[i] = v | (c << 8) | (((k << 1) | a) << 16);
 }
 
@@ -719,7 +758,7 @@ __global__ void k_refresh_pref(const uint32_t* planes, uint32_t* pref, const uin
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= NL * BL) return;
   const uint32_t nl = g / BL, b = g - nl * BL, node = n0 + nl;
-  pref[(size_t)node * BL + b] = is_byz(byz, node) ? byz_pattern(round) : tile_base(planes, g)[kPA * 64];
+  pref[(size_t)node * BL + b] = is_byz(byz, node) ? byz_pattern(round) : *pw(planes, g, kPA);
 }
 
 template <int K>
@@ -776,7 +815,7 @@ __global__ void k_count_live(const uint32_t* planes, const uint32_t* valid, cons
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < L; g += gridDim.x * blockDim.x) {
     const uint32_t nl = g / BL, b = g - nl * BL;
     if (honest_only && is_byz(byz, n0 + nl)) continue;
-    c += __popc(~tile_base(planes, g)[(kPK + 7) * 64] & valid[b]);
+    c += __popc(~*pw(planes, g, kPK + 7) & valid[b]);
   }
   const uint32_t w = wave_sum((uint32_t)c);  // <= 32 * 64 per wave per pass: fits u32
   if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = w;
