@@ -65,7 +65,7 @@ def main():
     warm.close()
     cold.close()
 
-    # --- per-rank kernel time at G-way target sharding (rank 0's shard, warm, default options)
+    # --- per-rank kernel time at G-way target sharding (rank 0's shard, warm), nt on/off interleaved
     for g in (1, 2, 4, 8):
         t0, t1 = sharding.target_shard(M, g, 0)
         e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, target_range=(t0, t1), log_capacity=1 << 27)
@@ -76,12 +76,18 @@ def main():
             e.fetch_updates(decode=False)
         except avhip.LogOverflow:
             pass
+        ts = {0: [], 1: []}
         b0 = e.alg_bytes()
-        ts = [one_round_ms(e) for _ in range(args.rounds)]
-        med = statistics.median(ts)
-        bpl = (e.alg_bytes() - b0) / args.rounds
-        out[f"shard{g}"] = {"targets": [t0, t1], "median_ms": med, "alg_GBs": bpl / (med * 1e-3) / 1e9,
-                            "updates_per_s_per_gpu": N * (t1 - t0) * K / (med * 1e-3)}
+        for _ in range(args.rounds):
+            for nt in (0, 1):
+                e.set_option("plane_nt", nt)
+                ts[nt].append(one_round_ms(e))
+        bpl = (e.alg_bytes() - b0) / (2 * args.rounds)
+        for nt in (0, 1):
+            med = statistics.median(ts[nt])
+            out[f"shard{g}" + ("+nt" if nt else "")] = {
+                "targets": [t0, t1], "median_ms": med, "alg_GBs": bpl / (med * 1e-3) / 1e9,
+                "updates_per_s_per_gpu": N * (t1 - t0) * K / (med * 1e-3)}
         e.close()
     print(json.dumps(out, indent=1))
     if args.json:

@@ -41,9 +41,15 @@ for s in "$@"; do
     prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- \
             python3 bench.py --no-cpu-baseline ;;
     pmc_fetch) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o bench -- \
-            python3 bench.py --no-cpu-baseline ;;
+            python3 bench.py --no-cpu-baseline --no-secondary ;;
     pmc_write) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o bench -- \
-            python3 bench.py --no-cpu-baseline ;;
+            python3 bench.py --no-cpu-baseline --no-secondary ;;
+    calib_fetch) step calib_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib_fetch -o calib -- \
+            go-avalanche_amd/bin/pmc_calib ;;
+    calib_write) step calib_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/calib_write -o calib -- \
+            go-avalanche_amd/bin/pmc_calib ;;
+    pmc_sum) step pmc_sum 120 python tools/pmc_summary.py --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write \
+            --fetch $OUT/pmc_fetch --write $OUT/pmc_write --out $OUT/pmc_traffic_c4.json ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
