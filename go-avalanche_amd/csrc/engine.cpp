@@ -80,6 +80,7 @@ struct av_engine {
   // consider planes are all-ones (lets k_round_fast skip them)
   bool c_monotone = true;
   bool plane_nt = true;  // tuning option "plane_nt" (A/B on MI355X: -8 % kernel time warm, -16 % cold)
+  bool ablate_gather = false;  // diagnostics option "ablate_gather" (invalid results)
   std::vector<uint32_t> valid_host;
   // replay stream
   uint32_t* replay = nullptr;
@@ -151,6 +152,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   p.finalized = e->finalized;
   p.warm_skip = e->c_monotone ? 1u : 0u;
   p.plane_nt = e->plane_nt ? 1u : 0u;
+  p.ablate_gather = e->ablate_gather ? 1u : 0u;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
   p.log_shards = e->log_shards;
@@ -816,6 +818,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   const std::string n(name);
   if (n == "plane_nt") {
     e->plane_nt = value != 0;
+  } else if (n == "ablate_gather") {
+    e->ablate_gather = value != 0;
   } else if (n == "warm_skip") {  // may only be switched off (it is a proven invariant, not a hint)
     if (!value) e->c_monotone = false;
   } else {

@@ -59,6 +59,7 @@ struct RoundParams {
   int32_t peer_mode;
   uint32_t warm_skip;        // consider planes are monotone (sim votes only): skip all-ones planes
   uint32_t plane_nt;         // stream state planes with non-temporal loads/stores
+  uint32_t ablate_gather;    // diagnostics only: gather the node's own row (wrong results)
 };
 
 // Update-log entry (one StatusUpdate, avalanche.go:59-62):

@@ -390,8 +390,11 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
     sample_peers<K>(p.seed, node, p.round, p.n_nodes, p.peer_mode, peers);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      w[j] = active ? p.pref_in[(size_t)peers[j] * p.BL + b] : 0u;  // peer's published preference
-      cw[j] = ~0u;                                                  // honest/Byzantine votes are 0 or 1
+      // peer's published preference; the ablation (timing diagnostics only,
+      // results invalid) reads the node's own row instead: coalesced, same count
+      const uint32_t src = p.ablate_gather ? (node ^ (uint32_t)j) % p.n_nodes : peers[j];
+      w[j] = active ? p.pref_in[(size_t)src * p.BL + b] : 0u;
+      cw[j] = ~0u;  // honest/Byzantine votes are 0 or 1
     }
   }
   const uint32_t vmask = active ? p.valid[b] : 0u;

@@ -76,16 +76,19 @@ def main():
             e.fetch_updates(decode=False)
         except avhip.LogOverflow:
             pass
-        ts = {0: [], 1: []}
+        variants = {"": (0, 0), "+nt": (1, 0), "+nt+ablate_gather": (1, 1)}
+        ts = {v: [] for v in variants}
         b0 = e.alg_bytes()
         for _ in range(args.rounds):
-            for nt in (0, 1):
+            for v, (nt, abl) in variants.items():
                 e.set_option("plane_nt", nt)
-                ts[nt].append(one_round_ms(e))
-        bpl = (e.alg_bytes() - b0) / (2 * args.rounds)
-        for nt in (0, 1):
-            med = statistics.median(ts[nt])
-            out[f"shard{g}" + ("+nt" if nt else "")] = {
+                e.set_option("ablate_gather", abl)
+                ts[v].append(one_round_ms(e))
+        e.set_option("ablate_gather", 0)
+        bpl = (e.alg_bytes() - b0) / (len(variants) * args.rounds)
+        for v in variants:
+            med = statistics.median(ts[v])
+            out[f"shard{g}{v}"] = {
                 "targets": [t0, t1], "median_ms": med, "alg_GBs": bpl / (med * 1e-3) / 1e9,
                 "updates_per_s_per_gpu": N * (t1 - t0) * K / (med * 1e-3)}
         e.close()
