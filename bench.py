@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--plane-nt", type=int, default=None, help="override the plane_nt tuning option")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N>1 rehearsal on a 1-GPU box: every rank on device 0, gloo for the host-side "
+                         "barrier/reductions (target sharding only; not a measurement)")
     return ap.parse_args()
 
 
@@ -155,7 +158,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     eng.close()
 
     if world > 1:
-        st = torch.tensor([elapsed, float(applied), float(emitted)], dtype=torch.float64, device="cuda")
+        st = torch.tensor([elapsed, float(applied), float(emitted)], dtype=torch.float64,
+                          device="cpu" if args.rehearse_one_gpu else "cuda")
         tmax = st[0:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tot = st[1:3].clone()
@@ -187,8 +191,14 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.rehearse_one_gpu:
+        if args.shard != "targets":
+            raise SystemExit("--rehearse-one-gpu supports target sharding only (RCCL needs distinct GPUs)")
+        local_rank = 0
     torch.cuda.set_device(local_rank)
-    if world > 1:
+    if world > 1 and args.rehearse_one_gpu:
+        dist.init_process_group("gloo")
+    elif world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     r = measure(args.workload, args, world, rank, local_rank, args.steps, args.warmup)

@@ -125,6 +125,23 @@ def test_device_replay_generator_parity(oracle):
     assert_same_state(eng, sim)
 
 
+def test_c2_full_size_replay_parity(oracle):
+    """configs[1] at full size (1k nodes x 10k targets, k=8, replayed streams,
+    4096 poll cap binding): device-generated stream, bit-exact vs the oracle."""
+    n, m, k, R, seed = 1000, 10_000, 8, 4, 0xA7A1A9C4
+    eng, sim = make_pair(oracle, n, m, k, seed=seed, init_mode=3, init_param=0x80000000)
+    eng.replay_prepare(R)
+    threads = min(8, __import__("os").cpu_count() or 1)
+    applied = 0
+    for r in range(R):
+        eng.replay_rounds(1)
+        exp_u, a = sim.run_round(oracle.gen_replay_errs(seed, r, 0, n, m, k), threads=threads)
+        applied += a
+        assert np.array_equal(eng.fetch_updates(), exp_u), r
+    assert_same_state(eng, sim)
+    assert eng.applied_votes() == applied == R * n * k * 4096
+
+
 # ------------------------------------------------------------------ exhaustive single-vote transitions
 def test_exhaustive_transitions_gpu(oracle):
     """Every reachable live record (votes subset of consider: 6561 pairs x count

@@ -31,6 +31,10 @@ for s in "$@"; do
     tests) step pytest_gpu 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py ;;
+    rehearse2) step rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --rehearse-one-gpu --no-secondary ;;
+    rehearse4) step rehearse4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+            --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 4 --rehearse-one-gpu --no-secondary ;;
     ab) step ab 900 python tools/ab_tune.py --json $OUT/ab.json ;;
     conv_c3) step conv_c3 900 python tools/run_to_finalization.py --workload c3 --json $OUT/conv_c3.json ;;
     conv_c5) step conv_c5 900 python tools/run_to_finalization.py --workload c5 --max-rounds 64 --json $OUT/conv_c5.json ;;
