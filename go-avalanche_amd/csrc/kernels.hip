@@ -558,7 +558,7 @@ __global__ __launch_bounds__(1024) void k_round_capped(const RoundParams p) {
     store_state(p.planes, g, s);
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
   }
-  const uint32_t wave_id = blockIdx.x * 16u + wave;
+  const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
   const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
   count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted, died);
 }

@@ -17,8 +17,8 @@ def rows(u):
     return [tuple(int(v) for v in r) for r in np.asarray(u).tolist()]
 
 
-def make_pair(oracle, n, m, k, seed=7, peer_mode=0, byz=0, init_mode=3, init_param=P80):
-    eng = avhip.Engine(n, m, k=k, seed=seed, peer_mode=peer_mode, byz_threshold=byz)
+def make_pair(oracle, n, m, k, seed=7, peer_mode=0, byz=0, init_mode=3, init_param=P80, log_capacity=0):
+    eng = avhip.Engine(n, m, k=k, seed=seed, peer_mode=peer_mode, byz_threshold=byz, log_capacity=log_capacity)
     eng.init_records(init_mode, init_param)
     sim = oracle.Sim(n, m, k, seed=seed, peer_mode=peer_mode, byz_threshold=byz, init_mode=init_mode,
                      init_param=init_param)
@@ -129,7 +129,7 @@ def test_c2_full_size_replay_parity(oracle):
     """configs[1] at full size (1k nodes x 10k targets, k=8, replayed streams,
     4096 poll cap binding): device-generated stream, bit-exact vs the oracle."""
     n, m, k, R, seed = 1000, 10_000, 8, 4, 0xA7A1A9C4
-    eng, sim = make_pair(oracle, n, m, k, seed=seed, init_mode=3, init_param=0x80000000)
+    eng, sim = make_pair(oracle, n, m, k, seed=seed, init_mode=3, init_param=0x80000000, log_capacity=1 << 24)
     eng.replay_prepare(R)
     threads = min(8, __import__("os").cpu_count() or 1)
     applied = 0
