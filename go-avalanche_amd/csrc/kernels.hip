@@ -302,7 +302,6 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
   uint32_t base = 0;
   if (lane == 0) base = atomicAdd(&p.log_count[shard], total);
   base = (uint32_t)__shfl((int)base, 0, 64);
-  if (cnt == 0u) return total;
   uint32_t Aj[K];
   uint32_t par = 0;
 #pragma unroll
@@ -328,7 +327,7 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
       ++pos;
     }
   }
-  if (ovf) atomicOr(p.log_overflow, 1u);
+  if (__ballot(ovf) != 0ull && lane == 0) atomicOr(p.log_overflow, 1u);  // one atomic per wave
   return total;
 }
 

@@ -30,7 +30,10 @@ def main():
     args = ap.parse_args()
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[args.workload]
     assert not replay
-    e = avhip.Engine(n, m, k=k, seed=args.seed, byz_threshold=byz, log_capacity=1 << 20)
+    # log sized for the heaviest round (every record can emit up to 2 updates per round at k=8);
+    # capped at 2^31 entries (16 GB) — a round beyond that is reported as overflow
+    log_cap = min(2 * n * m + (1 << 20), 1 << 31)
+    e = avhip.Engine(n, m, k=k, seed=args.seed, byz_threshold=byz, log_capacity=log_cap)
     e.init_records(init_mode, init_param)
     honest_records = e.live_records(honest_only=True)
     per_round = []
@@ -42,10 +45,11 @@ def main():
         e.run_rounds(1)
         ms, _ = e.kernel_stats()
         e.set_timing(False)
+        emitted = e.updates_count()  # StatusUpdates this round (log sized for the heaviest round)
         e.discard_updates()  # convergence only needs the counters
         live = e.live_records(honest_only=True)
         per_round.append({"round": r, "kernel_ms": ms, "applied": e.applied_votes() - a0,
-                          "finalized": e.finalized_count() - f0, "honest_live": live})
+                          "finalized": e.finalized_count() - f0, "emitted": emitted, "honest_live": live})
         if live == 0:
             done_round = r
             break
