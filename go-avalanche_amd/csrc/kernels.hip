@@ -283,11 +283,15 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 }
 
 // End-of-round StatusUpdate emission (processor.go:111) for one wave: one
-// atomic per emitting wave on a sharded log counter, entries in
-// (slot, lane, target) order inside the wave's reservation. Status is
-// derived from the final A plane: after slot j, A_j = A_final ^ parity(E at
-// later slots) (only flips change A); a record finalized this round has a
-// single E bit (count 127 -> 128 cannot follow a flip within 16 votes).
+// atomic per emitting wave on a sharded log counter reserves the wave's
+// total; then, per slot, every iteration lets each lane with updates left
+// emit one entry into consecutive log slots (mbcnt over the active lanes),
+// so every store instruction writes one contiguous run. The log order is
+// irrelevant: the packed key sorts to the canonical (round, node, slot,
+// target) order on fetch. Status is derived from the final A plane: after
+// slot j, A_j = A_final ^ parity(E at later slots) (only flips change A); a
+// record finalized this round has a single E bit (count 127 -> 128 cannot
+// follow a flip within 16 votes).
 template <int K>
 __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t wave_id, uint32_t lane,
                                                  uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
@@ -296,8 +300,7 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
 #pragma unroll
   for (int j = 0; j < K; ++j) cnt += __popc(E[j]);
   if (__ballot(cnt != 0u) == 0ull) return 0u;
-  const uint32_t incl = wave_incl_scan(cnt, lane);
-  const uint32_t total = (uint32_t)__shfl((int)incl, 63, 64);
+  const uint32_t total = wave_sum(cnt);
   const uint32_t shard = wave_id % p.log_shards;
   uint32_t base = 0;
   if (lane == 0) base = atomicAdd(&p.log_count[shard], total);
@@ -310,21 +313,27 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
     par ^= E[j];
   }
   uint64_t* dst = p.log + (size_t)shard * p.log_cap;
-  uint32_t pos = base + incl - cnt;
+  uint32_t run = base;  // wave-uniform
   bool ovf = false;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     uint32_t e = E[j];
-    while (e) {
-      const uint32_t bit = (uint32_t)__ffs(e) - 1u;
-      e &= e - 1u;
-      const uint32_t a = (Aj[j] >> bit) & 1u;
-      const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
-      if (pos < p.log_cap)
-        dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
-      else
-        ovf = true;
-      ++pos;
+    for (;;) {
+      const uint64_t act = __ballot(e != 0u);
+      if (act == 0ull) break;
+      if (e) {
+        const uint32_t bit = (uint32_t)__ffs(e) - 1u;
+        e &= e - 1u;
+        const uint32_t a = (Aj[j] >> bit) & 1u;
+        const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
+        const uint32_t pos =
+            run + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+        if (pos < p.log_cap)
+          dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
+        else
+          ovf = true;
+      }
+      run += (uint32_t)__popcll(act);
     }
   }
   if (__ballot(ovf) != 0ull && lane == 0) atomicOr(p.log_overflow, 1u);  // one atomic per wave
