@@ -315,8 +315,7 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
   uint64_t* dst = p.log + (size_t)shard * p.log_cap;
   uint32_t run = base;  // wave-uniform
   bool ovf = false;
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
+  for (int j = 0; j < K; ++j) {  // not unrolled (data-dependent inner loop); E/Aj stay in VGPRs
     uint32_t e = E[j];
     for (;;) {
       const uint64_t act = __ballot(e != 0u);
