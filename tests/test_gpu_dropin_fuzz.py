@@ -1,0 +1,88 @@
+"""Randomised op sequences on the one-node Processor surface (drop-in path) and
+interleaved batched rounds, engine vs oracle, bit-exact after every op.
+
+Covers what the reference's RegisterVotes loop does with messy input
+(processor.go:92-117): duplicate hashes inside one Response (applied in order),
+unknown hashes (skipped), invalid targets (skipped), votes on records deleted
+earlier in the same Response, re-adding after finalization (:45-58)."""
+import numpy as np
+import pytest
+
+import avhip
+
+pytestmark = pytest.mark.gpu
+
+ERRS = np.array([0, 0, 0, 0, 1, 2, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFF], np.uint32)
+
+
+def check(eng, sim, where):
+    got, exp = eng.read_records(), sim.dump()
+    assert np.array_equal(got, exp), where
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_dropin_fuzz(oracle, seed):
+    rng = np.random.default_rng(seed)
+    n, m = 5, 150
+    eng = avhip.Engine(n, m, k=4, seed=seed)  # no records (AV_INIT_NONE)
+    sim = oracle.Sim(n, m, 4, seed=seed, init_mode=0)
+    valid = np.ones(m, bool)
+    for step in range(400):
+        op = rng.integers(0, 10)
+        node = int(rng.integers(0, n))
+        if op < 2:  # AddTargetToReconcile, list with duplicates
+            ts = rng.integers(0, m, size=int(rng.integers(1, 20)))
+            acc = rng.integers(0, 2, size=ts.size)
+            got = eng.add_targets(node, ts, acc)
+            exp = [sim.add(node, int(t), int(a)) for t, a in zip(ts, acc)]
+            assert got.tolist() == exp, (step, "add")
+        elif op < 8:  # RegisterVotes, long Responses with duplicates and unknown hashes
+            size = int(rng.integers(1, 600))
+            ts = rng.integers(-5, m + 5, size=size)
+            ts[rng.random(size) < 0.3] = int(rng.integers(0, m))  # hammer one record
+            errs = rng.choice(ERRS, size)
+            st = eng.register_votes(node, ts, errs)
+            known = (ts >= 0) & (ts < m)
+            exp = sim.register_votes(node, ts[known], errs[known])
+            got = [(int(t), int(s)) for t, s in zip(ts, st) if s >= 0]
+            assert got == exp, (step, "register")
+        elif op == 8:  # Target.IsValid flips
+            t = int(rng.integers(0, m))
+            v = bool(rng.integers(0, 2))
+            eng.set_valid(t, v)
+            sim.set_valid(t, v)
+            valid[t] = v
+        else:  # a batched round in between (published preferences must be consistent)
+            eng.run_rounds(1)
+            exp_u, _ = sim.run_round()
+            got_u = eng.fetch_updates()
+            assert np.array_equal(got_u, exp_u), (step, "round")
+        check(eng, sim, step)
+        if step % 50 == 0:
+            for t in range(0, m, 7):
+                w = int(sim.dump()[node, t])
+                live = (w >> 17) < 128
+                assert eng.is_accepted(node, t) == (live and bool((w >> 16) & 1))
+                if live:
+                    assert eng.get_confidence(node, t) == w >> 17
+                else:
+                    with pytest.raises(avhip.VoteRecordNotFound):
+                        eng.get_confidence(node, t)
+            dump = sim.dump()[node]
+            exp_invs = [t for t in range(m) if (int(dump[t]) >> 17) < 128 and valid[t]][:4096]
+            assert eng.get_invs(node).tolist() == exp_invs, (step, "invs")
+
+
+def test_node_sharded_rccl_world1(oracle):
+    """The node-sharded RCCL path (av_comm_init + in-place ncclAllGather every
+    round) with a single rank equals the plain engine bit for bit."""
+    n, m, k, R = 64, 200, 8, 20
+    plain = avhip.Engine(n, m, k=k, seed=9, byz_threshold=int(0.2 * 2**32))
+    comm = avhip.Engine(n, m, k=k, seed=9, byz_threshold=int(0.2 * 2**32), node_range=(0, n))
+    for e in (plain, comm):
+        e.init_records(avhip.INIT_PAIRS, 0)
+    comm.comm_init(1, 0, avhip.comm_unique_id())
+    plain.run_rounds(R)
+    comm.run_rounds(R)
+    assert np.array_equal(plain.read_records(), comm.read_records())
+    assert np.array_equal(plain.fetch_updates(), comm.fetch_updates())

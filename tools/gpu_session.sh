@@ -31,6 +31,7 @@ for s in "$@"; do
     tests) step pytest_gpu 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
     testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py ;;
+    rccl2) step rccl2 240 python tools/rccl_two_rank_probe.py ;;
     rehearse2) step rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
             --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --rehearse-one-gpu --no-secondary ;;
     rehearse4) step rehearse4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
