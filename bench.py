@@ -82,7 +82,7 @@ def cpu_baseline(wl, seed, budget_s):
     n, m, k, init_mode, init_param, byz, replay, _ = WORKLOADS[wl]
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     threads = max(1, min(threads, 16))
-    ns = min(n, 40000 if wl != "c2" else 200)
+    ns = min(n, 80000 if wl != "c2" else 400)
     sim = cabi.Sim(ns, m, k, seed=seed, byz_threshold=byz, init_mode=init_mode, init_param=init_param)
     applied = 0
     dt = 0.0
@@ -170,7 +170,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     # launch (236 B per 32-record lane at k=8, 176 B once the consider planes
     # are warm, + 8 B per StatusUpdate) / its HIP-event average launch time.
     achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
-    kname = ("k_round_capped" if info["capped"] else "k_round_fast") + f"<{k},{'true' if replay else 'false'}>"
+    kname = ("k_round_capped" if info["capped"] else "k_round_sweep" if k <= 8 else "k_round_fast") + \
+        f"<{k},{'true' if replay else 'false'}>"
     return {
         "desc": desc, "n": n, "m": m, "k": k, "value": value, "elapsed": elapsed, "applied": applied,
         "emitted": emitted, "info": info, "kavg_ms": kavg_ms, "alg_bytes": alg_bytes, "achieved": achieved,

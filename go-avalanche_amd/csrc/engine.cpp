@@ -81,6 +81,15 @@ struct av_engine {
   bool c_monotone = true;
   bool plane_nt = true;  // tuning option "plane_nt" (A/B on MI355X: -8 % kernel time warm, -16 % cold)
   bool ablate_gather = false;  // diagnostics option "ablate_gather" (invalid results)
+  // round kernel: 2 = k_round_sweep (persistent, k <= 8, uncapped), 1 = k_round_fast (option "kernel")
+  int kernel = 2;
+  uint32_t sweep_blocks = 0;  // resident workgroups of the sweep grid (option "sweep_blocks"; 0 = one wave per tile)
+  // every consider plane of every lane is all-ones: set after a sim round with k >= 8 in which every
+  // live record was polled (all targets valid, uncapped); cleared by anything that can write a 0
+  // consider bit (init, add, write_records, drop-in votes, replay)
+  bool warm_all = false;
+  uint32_t bl_magic = 1, bl_sh1 = 0, bl_sh2 = 0;
+  uint32_t store_policy = 0;  // option "store_policy": 2 = sc1 (write-through) plane stores, 3 = nt sc1
   std::vector<uint32_t> valid_host;
   // replay stream
   uint32_t* replay = nullptr;
@@ -166,13 +175,32 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   p.round = (uint32_t)e->round;
   p.round_rel = (uint32_t)(e->round - e->log_base);
   p.peer_mode = e->cfg.peer_mode;
+  p.warm_all = e->warm_all ? 1u : 0u;
+  p.store_policy = e->store_policy;
+  p.bl_magic = e->bl_magic;
+  p.bl_sh1 = e->bl_sh1;
+  p.bl_sh2 = e->bl_sh2;
+  const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped;
+  bool all_valid = true;
+  for (uint32_t b = 0; b < e->BL; ++b) {
+    const int64_t tb = e->t0 + 32ll * b;
+    const int64_t r = std::min<int64_t>(e->t1 - tb, 32);
+    all_valid &= e->valid_host[b] == (r >= 32 ? ~0u : ((1u << r) - 1u));
+  }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (e->timing) {
     AV_HIP(hipEventCreate(&ev0));
     AV_HIP(hipEventCreate(&ev1));
     AV_HIP(hipEventRecord(ev0, e->stream));
   }
-  AV_HIP(avk::launch_round(p, e->k, replay != nullptr, e->capped, e->stream));
+  if (sweep)
+    AV_HIP(avk::launch_round_sweep(p, e->k, replay != nullptr, e->sweep_blocks, e->stream));
+  else
+    AV_HIP(avk::launch_round(p, e->k, replay != nullptr, e->capped, e->stream));
+  if (replay)
+    e->warm_all = false;
+  else if (e->c_monotone && e->k >= 8 && !e->capped && all_valid)
+    e->warm_all = true;  // every live record was polled and shifted in 8 considered votes
   if (e->timing) {
     AV_HIP(hipEventRecord(ev1, e->stream));
     e->events.emplace_back(ev0, ev1);
@@ -186,6 +214,19 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   e->cur ^= 1;
   e->round++;
   return AV_OK;
+}
+
+// Sweep grid (0 = one wave per tile). Measured on MI355X (tools/ab_tune.py):
+// one wave per tile is fastest for large tile counts (C4 on 1-4 GPUs: the
+// dispatcher keeps the active tiles in a narrow, DRAM-friendly window); a
+// resident grid that walks the tiles wins slightly once there are only a few
+// tiles per resident wave (C4 8-way target shard: 62.5k tiles, ~9 per wave).
+uint32_t default_sweep_blocks(const av_engine* e) {
+  if (e->k > 8 || e->capped) return 0;
+  int bpc = 0, cus = 0;
+  if (avk::round_sweep_occupancy(e->k, false, &bpc, &cus) != hipSuccess || bpc <= 0 || cus <= 0) return 0;
+  const uint64_t resident_waves = (uint64_t)bpc * cus * 4;
+  return (uint64_t)(e->Lpad / 64) <= 12 * resident_waves ? (uint32_t)(bpc * cus) : 0u;
 }
 
 int refresh_pref(av_engine* e) {
@@ -280,6 +321,7 @@ int av_create(const av_config* cfg, av_engine** out) {
   if (L >= (1ull << 31)) return bad("too many lanes for one engine: shard further");
   e->L = (uint32_t)L;
   e->Lpad = (uint32_t)((L + 63) / 64 * 64);
+  avk::bl_divider(e->BL, e->bl_magic, e->bl_sh1, e->bl_sh2);
 
   int rc = AV_OK;
   auto hip_fail = [&](hipError_t he, const char* what) {
@@ -328,6 +370,7 @@ int av_create(const av_config* cfg, av_engine** out) {
     return hip_fail(he, "upload valid");
   if ((he = avk::launch_byz(e->byz, (uint32_t)e->N, c.seed, c.byz_threshold, e->stream)) != hipSuccess)
     return hip_fail(he, "byz kernel");
+  e->sweep_blocks = default_sweep_blocks(e);
   *out = e;
   rc = av_init_records(e, AV_INIT_NONE, 0);
   if (rc != AV_OK) {
@@ -340,6 +383,7 @@ int av_create(const av_config* cfg, av_engine** out) {
 
 int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
   AV_ENTER(e);
+  e->warm_all = false;
   AV_CHECK(init_mode >= AV_INIT_NONE && init_mode <= AV_INIT_PAIRS, AV_ERR_INVALID_ARG, "bad init_mode");
   avk::InitParams p{};
   p.planes = e->planes;
@@ -383,6 +427,7 @@ int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uin
   AV_ENTER(e);
   AV_CHECK(n >= 0 && (n == 0 || (targets && accepted && added)), AV_ERR_INVALID_ARG, "null argument");
   AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
+  e->warm_all = false;
   std::vector<uint32_t> tl;
   std::vector<uint8_t> acc;
   std::vector<int64_t> pos;
@@ -820,6 +865,20 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->plane_nt = value != 0;
   } else if (n == "ablate_gather") {
     e->ablate_gather = value != 0;
+  } else if (n == "kernel") {  // 2 = k_round_sweep (default where it applies), 1 = k_round_fast
+    AV_CHECK(value == 1 || value == 2, AV_ERR_INVALID_ARG, "kernel must be 1 or 2");
+    e->kernel = (int)value;
+  } else if (n == "store_policy") {
+    AV_CHECK(value >= 0 && value <= 3, AV_ERR_INVALID_ARG, "store_policy must be in [0, 3]");
+    e->store_policy = (uint32_t)value;
+  } else if (n == "sweep_blocks") {  // 0 = one wave per tile, -1 = every resident workgroup once (default)
+    AV_CHECK(value >= -1 && value < (1ll << 31), AV_ERR_INVALID_ARG, "bad sweep_blocks");
+    if (value < 0) {
+      AV_ENTER(e);
+      e->sweep_blocks = default_sweep_blocks(e);
+    } else {
+      e->sweep_blocks = (uint32_t)value;
+    }
   } else if (n == "warm_skip") {  // may only be switched off (it is a proven invariant, not a hint)
     if (!value) e->c_monotone = false;
   } else {

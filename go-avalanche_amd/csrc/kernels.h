@@ -60,7 +60,21 @@ struct RoundParams {
   uint32_t warm_skip;        // consider planes are monotone (sim votes only): skip all-ones planes
   uint32_t plane_nt;         // stream state planes with non-temporal loads/stores
   uint32_t ablate_gather;    // diagnostics only: gather the node's own row (wrong results)
+  // k_round_sweep only
+  uint32_t warm_all;         // every consider plane of every lane is all-ones (no per-tile check)
+  uint32_t store_policy;     // 0/1: per plane_nt; 2: sc1 plane/pref stores; 3: nt sc1 (k = 8)
+  uint32_t bl_magic, bl_sh1, bl_sh2;  // n / BL = (t + ((n - t) >> sh1)) >> sh2, t = mulhi(n, magic)
 };
+
+// Division by the (runtime) block count BL without a hardware divide:
+// Granlund-Montgomery round-up magic, exact for every 32-bit n.
+inline void bl_divider(uint32_t d, uint32_t& magic, uint32_t& sh1, uint32_t& sh2) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  magic = (uint32_t)((((1ull << l) - d) << 32) / d + 1);
+  sh1 = l < 1 ? l : 1;
+  sh2 = l > 1 ? l - 1 : 0;
+}
 
 // Update-log entry (one StatusUpdate, avalanche.go:59-62):
 //   [63:52] round - log_base | [51:28] node | [27:24] slot | [23:2] target | [1:0] status
@@ -72,6 +86,11 @@ __host__ __device__ inline uint64_t pack_update(uint32_t round_rel, uint32_t nod
 }
 
 hipError_t launch_round(const RoundParams& p, int k, bool replay, bool capped, hipStream_t s);
+// Persistent streaming round kernel (round_sweep.hip), uncapped path, k <= 8:
+// `blocks` workgroups of 256 threads sweep the tiles; 0 = one wave per tile.
+hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s);
+// Resident 256-thread workgroups per CU for the sweep kernel and the CU count.
+hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cus);
 
 struct InitParams {
   uint32_t* planes;

@@ -16,345 +16,10 @@
 #include <algorithm>
 
 #include "kernels.h"
+#include "round_common.h"
 
 namespace avk {
 namespace {
-
-constexpr uint32_t kDomPeers = 1u, kDomByz = 2u, kDomInit = 3u, kDomPairs = 4u, kDomReplay = 5u;
-// replay class thresholds: P(yes)=0.70, P(no)=0.25, P(neutral)=0.05
-constexpr uint32_t kReplayYes = 3006477107u, kReplayNo = 4080218931u;
-
-// ---------------------------------------------------------------------------
-// Philox4x32-10 (Salmon et al. SC'11), same counter/key conventions as the
-// oracle's restatement (oracle/avalanche_oracle.c) and Random123's KATs.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void philox(uint32_t x[4], uint64_t seed, uint32_t a, uint32_t b, uint32_t c,
-                                       uint32_t dom) {
-  uint32_t c0 = a, c1 = b, c2 = c, c3 = dom;
-  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r) {
-      k0 += 0x9E3779B9u;
-      k1 += 0xBB67AE85u;
-    }
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-    c1 = (uint32_t)p1;
-    c3 = (uint32_t)p0;
-    c0 = n0;
-    c2 = n2;
-  }
-  x[0] = c0; x[1] = c1; x[2] = c2; x[3] = c3;
-}
-
-__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
-
-// State-plane stream accessors. NT = non-temporal (global_load/store ... nt):
-// the planes are touched once per round, so keeping them out of L2 / the
-// Infinity Cache leaves room for the gathered preference table.
-template <bool NT>
-__device__ __forceinline__ uint32_t pld(const uint32_t* q) {
-  if constexpr (NT) return __builtin_nontemporal_load(q);
-  return *q;
-}
-template <bool NT>
-__device__ __forceinline__ void pst(uint32_t* q, uint32_t v) {
-  if constexpr (NT)
-    __builtin_nontemporal_store(v, q);
-  else
-    *q = v;
-}
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-template <bool NT>
-__device__ __forceinline__ u32x4 pld4(const u32x4* q) {
-  if constexpr (NT) return __builtin_nontemporal_load(q);
-  return *q;
-}
-template <bool NT>
-__device__ __forceinline__ void pst4(u32x4* q, u32x4 v) {
-  if constexpr (NT)
-    __builtin_nontemporal_store(v, q);
-  else
-    *q = v;
-}
-
-// Byzantine flip-flop answer: err = ((r ^ t) & 1) ? 1 : 0, so
-// "yes" on even targets in even rounds. Blocks start at multiples of 32.
-__device__ __forceinline__ uint32_t byz_pattern(uint32_t round) { return (round & 1u) ? 0xAAAAAAAAu : 0x55555555u; }
-
-__device__ __forceinline__ bool is_byz(const uint32_t* byz, uint32_t node) { return (byz[node >> 5] >> (node & 31u)) & 1u; }
-
-struct St {
-  uint32_t V[8], C[8], A, K[8];
-};
-
-// Tile layout (1600 words = 6400 B per 64 lanes), see kernels.h:
-//   [0,1024)    V0-3 | V4-7 | K0-3 | K4-7 as 16-byte groups, lane-interleaved:
-//               group q, lane l, plane i -> q*256 + l*4 + i  (one dwordx4 per
-//               lane, 1 KiB contiguous per wave-instruction)
-//   [1024,1536) C0..C7 dword planes: 1024 + c*64 + l
-//   [1536,1600) A dword plane:       1536 + l
-__host__ __device__ constexpr uint32_t plane_off(int p, uint32_t lane) {
-  return p < kPC ? (uint32_t)(p >> 2) * 256u + lane * 4u + (uint32_t)(p & 3)
-       : p < kPA ? 1024u + (uint32_t)(p - kPC) * 64u + lane
-       : p == kPA ? 1536u + lane
-       : (uint32_t)(2 + ((p - kPK) >> 2)) * 256u + lane * 4u + (uint32_t)((p - kPK) & 3);
-}
-
-__device__ __forceinline__ uint32_t* tile_of(const uint32_t* planes, uint32_t g) {
-  return const_cast<uint32_t*>(planes) + (size_t)(g >> 6) * (kPlanes * 64);
-}
-
-// pointer to the word of plane p for lane g
-__device__ __forceinline__ uint32_t* pw(const uint32_t* planes, uint32_t g, int p) {
-  return tile_of(planes, g) + plane_off(p, g & 63u);
-}
-
-__device__ __forceinline__ void load_state(const uint32_t* planes, uint32_t g, St& s) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s.V[i] = *pw(planes, g, kPV + i);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s.C[i] = *pw(planes, g, kPC + i);
-  s.A = *pw(planes, g, kPA);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s.K[i] = *pw(planes, g, kPK + i);
-}
-
-__device__ __forceinline__ void store_state(uint32_t* planes, uint32_t g, const St& s) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) *pw(planes, g, kPV + i) = s.V[i];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) *pw(planes, g, kPC + i) = s.C[i];
-  *pw(planes, g, kPA) = s.A;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) *pw(planes, g, kPK + i) = s.K[i];
-}
-
-// No live record in any of the 32 slots (canonical dead form).
-__device__ __forceinline__ void dead_state(St& s) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    s.V[i] = 0u;
-    s.C[i] = ~0u;
-    s.K[i] = 0u;
-  }
-  s.K[7] = ~0u;
-  s.A = 0u;
-}
-
-// Bit-sliced "popcount of 8 > 6" (vote.go:58,61): at most one zero among x[].
-__device__ __forceinline__ uint32_t atleast7(const uint32_t (&x)[8]) {
-  uint32_t t = x[0], u = ~0u;
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    u = (u & x[i]) | t;
-    t &= x[i];
-  }
-  return u;
-}
-
-// One regsiterVote (vote.go:54-75) applied to the records of `part`.
-//   yw : err == 0            (vote.go:55)
-//   cw : int32(err) >= 0     (vote.go:56)
-// MASKED=false shifts every bit (caller restores non-participants at the end
-// of the round); MASKED=true leaves non-participating records untouched.
-// Outputs E = records whose regsiterVote returned true, fin = finalized now.
-template <bool MASKED>
-__device__ __forceinline__ void vote_step(St& s, uint32_t yw, uint32_t cw, uint32_t part, uint32_t& E,
-                                          uint32_t& fin) {
-  yw &= cw;
-  if (MASKED) {
-#pragma unroll
-    for (int i = 7; i > 0; --i) {
-      s.V[i] = bfi(part, s.V[i - 1], s.V[i]);
-      s.C[i] = bfi(part, s.C[i - 1], s.C[i]);
-    }
-    s.V[0] = bfi(part, yw, s.V[0]);
-    s.C[0] = bfi(part, cw, s.C[0]);
-  } else {
-#pragma unroll
-    for (int i = 7; i > 0; --i) {
-      s.V[i] = s.V[i - 1];
-      s.C[i] = s.C[i - 1];
-    }
-    s.V[0] = yw;
-    s.C[0] = cw;
-  }
-  uint32_t y[8], n[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    y[i] = s.V[i] & s.C[i];   // votes & consider            (vote.go:58)
-    n[i] = ~s.V[i] & s.C[i];  // (-votes-1) & consider        (vote.go:61)
-  }
-  const uint32_t yes = atleast7(y);
-  const uint32_t no = atleast7(n);
-  const uint32_t concl = (yes | no) & part;  // conclusive     (vote.go:61-63)
-  const uint32_t flip = concl & (s.A ^ yes);  // disagrees      (vote.go:72-74)
-  uint32_t carry = concl ^ flip;              // agrees: conf+=2 (vote.go:66-69)
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    const uint32_t c2 = s.K[i] & carry;
-    s.K[i] = (s.K[i] ^ carry) & ~flip;  // flip resets the count
-    carry = c2;
-  }
-  s.K[7] |= carry;  // count reached exactly 128 (vote.go:68), record deleted
-  s.A = bfi(flip, yes, s.A);
-  E = flip | carry;
-  fin = carry;
-}
-
-// k distinct peers != node, uniform over the other N-1 nodes (first K
-// distinct values of the Philox candidate stream; same definition as
-// avo_sample_peers in the oracle). Fast path = the first ceil(K/4) Philox
-// blocks give K distinct candidates; otherwise a rarely taken general loop.
-template <int K>
-__device__ __forceinline__ void sample_peers(uint64_t seed, uint32_t node, uint32_t round, uint32_t n_nodes,
-                                             int mode, uint32_t (&out)[K]) {
-  const uint32_t others = n_nodes - 1u;
-  if (mode == 1 || (uint32_t)K >= others) {
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const uint64_t q = (mode == 1) ? (uint64_t)round * (uint64_t)K + (uint64_t)j : (uint64_t)j;
-      const uint32_t idx = (uint32_t)(q % others);
-      out[j] = idx + (idx >= node ? 1u : 0u);
-    }
-    return;
-  }
-  constexpr int NB = (K + 3) / 4;
-  uint32_t cand[NB * 4];
-#pragma unroll
-  for (int blk = 0; blk < NB; ++blk) {
-    uint32_t x[4];
-    philox(x, seed, node, round, (uint32_t)blk, kDomPeers);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t u = (uint32_t)(((uint64_t)x[i] * others) >> 32);
-      cand[blk * 4 + i] = u + (u >= node ? 1u : 0u);
-    }
-  }
-  bool distinct = true;
-#pragma unroll
-  for (int i = 1; i < K; ++i)
-#pragma unroll
-    for (int j = 0; j < i; ++j) distinct &= cand[i] != cand[j];
-  if (distinct) {
-#pragma unroll
-    for (int j = 0; j < K; ++j) out[j] = cand[j];
-    return;
-  }
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) out[j] = 0u;
-  for (uint32_t blk = 0; cnt < (uint32_t)K; ++blk) {
-    uint32_t x[4];
-    philox(x, seed, node, round, blk, kDomPeers);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t u = (uint32_t)(((uint64_t)x[i] * others) >> 32);
-      const uint32_t pp = u + (u >= node ? 1u : 0u);
-      bool dup = false;
-#pragma unroll
-      for (int j = 0; j < K; ++j) dup |= ((uint32_t)j < cnt) && (out[j] == pp);
-      if (!dup && cnt < (uint32_t)K) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) out[j] = ((uint32_t)j == cnt) ? pp : out[j];
-        ++cnt;
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)v, (unsigned)d, 64);
-    if (lane >= (uint32_t)d) v += t;
-  }
-  return v;
-}
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d, 64);
-  return v;
-}
-
-// End-of-round StatusUpdate emission (processor.go:111) for one wave: one
-// atomic per emitting wave on a sharded log counter reserves the wave's
-// total; then, per slot, every iteration lets each lane with updates left
-// emit one entry into consecutive log slots (mbcnt over the active lanes),
-// so every store instruction writes one contiguous run. The log order is
-// irrelevant: the packed key sorts to the canonical (round, node, slot,
-// target) order on fetch. Status is derived from the final A plane: after
-// slot j, A_j = A_final ^ parity(E at later slots) (only flips change A); a
-// record finalized this round has a single E bit (count 127 -> 128 cannot
-// follow a flip within 16 votes).
-template <int K>
-__device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t wave_id, uint32_t lane,
-                                                 uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
-                                                 uint32_t A_final, uint32_t died) {
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) cnt += __popc(E[j]);
-  if (__ballot(cnt != 0u) == 0ull) return 0u;
-  const uint32_t total = wave_sum(cnt);
-  const uint32_t shard = wave_id % p.log_shards;
-  uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(&p.log_count[shard], total);
-  base = (uint32_t)__shfl((int)base, 0, 64);
-  uint32_t Aj[K];
-  uint32_t par = 0;
-#pragma unroll
-  for (int j = K - 1; j >= 0; --j) {
-    Aj[j] = A_final ^ par;
-    par ^= E[j];
-  }
-  uint64_t* dst = p.log + (size_t)shard * p.log_cap;
-  uint32_t run = base;  // wave-uniform
-  bool ovf = false;
-  for (int j = 0; j < K; ++j) {  // not unrolled (data-dependent inner loop); E/Aj stay in VGPRs
-    uint32_t e = E[j];
-    for (;;) {
-      const uint64_t act = __ballot(e != 0u);
-      if (act == 0ull) break;
-      if (e) {
-        const uint32_t bit = (uint32_t)__ffs(e) - 1u;
-        e &= e - 1u;
-        const uint32_t a = (Aj[j] >> bit) & 1u;
-        const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
-        const uint32_t pos =
-            run + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-        if (pos < p.log_cap)
-          dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
-        else
-          ovf = true;
-      }
-      run += (uint32_t)__popcll(act);
-    }
-  }
-  if (__ballot(ovf) != 0ull && lane == 0) atomicOr(p.log_overflow, 1u);  // one atomic per wave
-  return total;
-}
-
-// Per-wave counters: regsiterVote applications (the metric numerator) and the
-// algorithmic bytes this wave moved (state planes actually read/written,
-// gathered vote words, the published word, 8 B per emitted StatusUpdate).
-__device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied,
-                                            bool active, uint32_t bytes_per_lane, uint32_t emitted, uint32_t died) {
-  const uint32_t s = wave_sum(applied);
-  const uint32_t f = wave_sum(__popc(died));
-  const uint32_t nact = (uint32_t)__popcll(__ballot(active));
-  if (lane == 0) {
-    const uint32_t shard = wave_id % p.log_shards;
-    if (s) atomicAdd(&p.applied[shard], (unsigned long long)s);
-    if (f) atomicAdd(&p.finalized[shard], (unsigned long long)f);
-    atomicAdd(&p.bytes[shard], (unsigned long long)nact * bytes_per_lane + 8ull * emitted);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Body of the uncapped round kernel for one lane (one 32-record block).
 // WARM (sim mode only): every consider plane of the wave's blocks is all-ones

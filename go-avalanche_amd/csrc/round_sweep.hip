@@ -1,0 +1,470 @@
+// Persistent streaming round kernel (uncapped path, k <= 8): the hot path of
+// the engine. One round of go-avalanche's poll loop for every simulated node
+// (processor.go:92-117 driven by main.go:110-136, rules R1-R4 of SURVEY.md
+// §8): peer draw (processor.go:173-182 replaced by a Philox k-peer draw),
+// gather of each peer's published IsAccepted word (main.go:168-192 responder),
+// k regsiterVote steps (vote.go:54-75) on 32 bit-sliced VoteRecords per lane,
+// StatusUpdate emission (processor.go:111) and deletion on finalization
+// (:114-116).
+//
+// Same HBM layout, outputs and counters as k_round_fast (kernels.hip); what
+// differs is how the work maps onto CDNA4:
+//  * a fixed grid of resident waves sweeps the 64-lane tiles, so the per-wave
+//    counters are reduced and flushed once per wave, not once per tile;
+//  * the Philox peer draw runs once per (node, Philox block) across the
+//    wave's lanes and is handed to the node's lanes with ds_bpermute, instead
+//    of every lane of a node redrawing the same peers;
+//  * the ">6 of 8" thresholds of vote.go:58,61 are evaluated for all k slots
+//    at once as sliding windows over [old planes | new votes] (prefix
+//    aggregates on both sides of the boundary, 2 VALU ops per window);
+//  * when no record of the wave can reach count 128 this round (count < 120,
+//    k <= 8), the confidence update is a bit-sliced popcount of the agreeing
+//    votes after the last flip added once, not a 7-plane ripple per vote;
+//    otherwise the exact per-vote ripple with deletion runs;
+//  * once every consider plane is known to be all-ones (sim votes only, the
+//    engine tracks it), the consider planes are neither read nor written and
+//    the per-tile check load disappears.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "kernels.h"
+#include "round_common.h"
+
+namespace avk {
+namespace {
+
+__device__ __forceinline__ uint32_t div_bl(const RoundParams& p, uint32_t n) {
+  const uint32_t t = __umulhi(n, p.bl_magic);
+  return (t + ((n - t) >> p.bl_sh1)) >> p.bl_sh2;
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// Thresholds of vote.go:58,61 at slot j. The 8-vote window after slot j is
+// seq[j .. j+7] of the sequence seq = [V_6 .. V_0, w_0 .. w_{K-1}] (old
+// shift-register planes, oldest first, then this round's votes). y = votes &
+// consider, n = ^votes & consider (vote.go:58, :61); "popcount > 6" of 8
+// planes = at most one zero = a 14-op bit-sliced network (u | t folds into
+// one v_bitop3 per plane).
+template <int J, int K, bool NEG = false>
+__device__ __forceinline__ uint32_t atleast7_window(const uint32_t (&seq)[7 + K]) {
+  uint32_t t = NEG ? ~seq[J] : seq[J], u = ~0u;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    const uint32_t x = NEG ? ~seq[J + i] : seq[J + i];
+    u = (u & x) | t;
+    t &= x;
+  }
+  return u;
+}
+
+// yes / no thresholds of slot J; SYM: n == ~y on the whole window (sim votes
+// on warm planes), so the no side runs on the complement of ys in place
+template <int J, int K, bool SYM>
+__device__ __forceinline__ void thresholds(const uint32_t (&ys)[7 + K], const uint32_t (&ns)[7 + K], uint32_t& yes,
+                                           uint32_t& no) {
+  yes = atleast7_window<J, K>(ys);
+  no = SYM ? atleast7_window<J, K, true>(ys) : atleast7_window<J, K>(ns);
+}
+
+// The rarely taken peer draws (round-robin mode, N - 1 <= k, one block per
+// node, or a repeated candidate) out of line, so their registers do not
+// weigh on the hot path.
+template <int K>
+struct PeerList {
+  uint32_t v[K];
+};
+template <int K>
+__device__ __forceinline__ PeerList<K> sample_peers_general(uint64_t seed, uint32_t node, uint32_t round,
+                                                         uint32_t n_nodes, int mode) {
+  PeerList<K> r;
+  sample_peers<K>(seed, node, round, n_nodes, mode, r.v);
+  return r;
+}
+
+struct SweepAcc {
+  uint32_t applied = 0, died = 0, lane_bytes = 0;
+  uint32_t emitted = 0;  // wave-uniform
+};
+
+enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3 };
+
+// Per-slot step of the round. The count update is deferred: c (4 planes)
+// counts the agreeing conclusive votes since the last flip (vote.go:66-69),
+// F marks records that flipped (vote.go:72-74; count reset to 0), and at the
+// end count_new = F ? c : count + c. det (some polled record of the wave has
+// count >= 120, wave-uniform): also detect the vote that takes a record from 127 to 128 —
+// an agreement with no flip before it in the round and low3 + c == 8, where
+// low3 = count & 7 (count >= 120 means bits 3..6 are set) — which finalizes
+// and deletes it (vote.go:68, processor.go:114-116); later slots skip it.
+template <int K, bool SYM, int J = 0>
+__device__ __forceinline__ void round_slots(const uint32_t (&ys)[7 + K], const uint32_t (&ns)[7 + K],
+                                            const uint32_t (&low3)[3], uint32_t nearfin, bool det, uint32_t& alive,
+                                            uint32_t& A, uint32_t (&E)[K], uint32_t (&c)[4], uint32_t& F,
+                                            uint32_t& applied) {
+  if constexpr (J < K) {
+    uint32_t yes, no;
+    thresholds<J, K, SYM>(ys, ns, yes, no);
+    applied += (uint32_t)__popc(alive);
+    const uint32_t concl = (yes | no) & alive;  // conclusive (vote.go:61-63)
+    const uint32_t flip = concl & (A ^ yes);    // disagrees: reset to yes?1:0 (vote.go:72-74)
+    const uint32_t agree = concl ^ flip;        // agrees: confidence += 2 (vote.go:66-69)
+    uint32_t carry = agree;
+    A ^= flip;
+    constexpr int planes = J < 1 ? 1 : J < 3 ? 2 : J < 7 ? 3 : 4;  // c <= J + 1
+#pragma unroll
+    for (int i = 0; i < planes; ++i) {
+      const uint32_t ci = J == 0 ? 0u : c[i] & ~flip;
+      c[i] = ci ^ carry;
+      carry &= ci;
+    }
+    uint32_t e = flip;
+    if (det) {  // wave-uniform
+      // low3 + c == 8 (c <= 8, low3 <= 7): sum bits 0..2 clear, bit 3 set
+      const uint32_t c3 = planes > 3 ? c[3] : 0u;
+      const uint32_t c2 = planes > 2 ? c[2] : 0u;
+      const uint32_t s0 = low3[0] ^ c[0], k0 = low3[0] & c[0];
+      const uint32_t t1 = low3[1] ^ c[1], s1 = t1 ^ k0, k1 = bfi(t1, k0, low3[1]);
+      const uint32_t t2 = low3[2] ^ c2, s2 = t2 ^ k1, k2 = bfi(t2, k1, low3[2]);
+      const uint32_t s3 = c3 ^ k2;
+      const uint32_t fin = agree & ~F & nearfin & ~(s0 | s1 | s2) & s3;
+      e |= fin;
+      alive &= ~fin;
+    }
+    F |= flip;
+    E[J] = e;
+    round_slots<K, SYM, J + 1>(ys, ns, low3, nearfin, det, alive, A, E, c, F, applied);
+  }
+}
+
+// Plane-stream cache policy POL: 0 = default loads/stores, 1 = non-temporal
+// loads and stores, 2 = non-temporal loads + sc1 stores (write-through, the
+// line leaves the XCD's L2), 3 = non-temporal loads + nt sc1 stores. 2/3 keep
+// the streamed state out of L2 so that more of the gathered preference table
+// stays there (MI355X_MICROARCH.md: plain/nt stores keep the line in L2, sc1
+// stores drop it).
+constexpr int32_t kRsrcWord3 = 0x00020000;  // raw 32-bit buffer (gfx9 family)
+template <int POL>
+__device__ __forceinline__ u32x4 ld4(const u32x4* q) {
+  return pld4<(POL > 0)>(q);
+}
+template <int POL>
+__device__ __forceinline__ uint32_t ld1(const uint32_t* q) {
+  return pld<(POL > 0)>(q);
+}
+template <int POL>
+__device__ __forceinline__ void st4(__amdgpu_buffer_rsrc_t r, u32x4* q, uint32_t off, u32x4 v) {
+  if constexpr (POL < 2)
+    pst4<(POL > 0)>(q, v);
+  else
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, POL == 2 ? 16 : 18);
+}
+template <int POL>
+__device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, uint32_t* q, uint32_t off, uint32_t v) {
+  if constexpr (POL < 2)
+    pst<(POL > 0)>(q, v);
+  else
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, POL == 2 ? 16 : 18);
+}
+
+// One 64-lane tile of the round. WARM: consider planes all-ones (neither
+// loaded nor stored; sim votes only). POL: plane-stream cache policy.
+template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE>
+__device__ __forceinline__ void sweep_tile(const RoundParams& p, uint32_t tile, uint32_t lane, uint32_t extra_bytes,
+                                           SweepAcc& acc) {
+  const uint32_t g = tile * 64u + lane;
+  const bool active = g < p.L;
+  const uint32_t gc = active ? g : p.L - 1u;  // inactive lanes read a valid lane, never store
+  const uint32_t nl = div_bl(p, gc);
+  const uint32_t b = gc - nl * p.BL;
+  const uint32_t node = p.n0 + nl;
+
+  // ---- state planes (vote.go:25-29): V0-7 and K0-7 as dwordx4 groups, A, C0-7 unless warm
+  uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
+  u32x4* const grp = reinterpret_cast<u32x4*>(tp) + lane;
+  const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(tp, 0, kPlanes * 64 * 4, kRsrcWord3);
+  const u32x4 v0 = ld4<POL>(grp), v1 = ld4<POL>(grp + 64), k0 = ld4<POL>(grp + 128), k1 = ld4<POL>(grp + 192);
+  uint32_t A = ld1<POL>(tp + 1536u + lane);
+  uint32_t C[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) C[i] = WARM ? ~0u : ld1<POL>(tp + 1024u + (uint32_t)i * 64u + lane);
+  const uint32_t vmask = active ? p.valid[b] : 0u;
+
+  // ---- this round's votes: ys/ns hold y/n of [V_6..V_0, w_0..w_{K-1}]
+  constexpr bool SYM = WARM && !REPLAY;  // n == ~y everywhere: ns is never read
+  uint32_t ys[7 + K], ns[7 + K], cwv[K];
+  if constexpr (REPLAY) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t cw = p.replay[(size_t)(2 * j + 1) * p.Lpad + gc];
+      const uint32_t yw = p.replay[(size_t)(2 * j) * p.Lpad + gc] & cw;  // err == 0 implies considered
+      ys[7 + j] = yw;
+      ns[7 + j] = ~yw & cw;
+      cwv[j] = cw;
+    }
+  } else {
+    uint32_t peers[K];
+    const uint32_t others = p.n_nodes - 1u;
+    constexpr uint32_t NB = (K + 3) / 4;
+    const uint32_t nlA = uni(nl);                                                      // lane 0 is always active
+    const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)nl, 63) - nlA + 1u;  // nodes in this tile
+    bool general = p.peer_mode == 1 || (uint32_t)K >= others || nn * NB > 64u;
+    if (!general) {
+      // producer lane q draws Philox block q % NB of the tile's node q / NB ...
+      const uint32_t q = lane;
+      const uint32_t pnode = p.n0 + nlA + min(q / NB, nn - 1u);
+      uint32_t x[4];
+      philox(x, p.seed, pnode, p.round, q % NB, kDomPeers);
+      uint32_t prod[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t u = __umulhi(x[i], others);
+        prod[i] = u + (u >= pnode ? 1u : 0u);
+      }
+      // ... and every lane of that node takes its candidates with ds_bpermute
+      const uint32_t base = (nl - nlA) * NB;
+      bool distinct = true;
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        peers[c] = (uint32_t)__shfl((int)prod[c & 3], (int)(base + (uint32_t)c / 4u), 64);
+#pragma unroll
+        for (int d = 0; d < c; ++d) distinct &= peers[c] != peers[d];
+      }
+      general = !distinct;
+    }
+    if (general) {
+      const PeerList<K> r = sample_peers_general<K>(p.seed, node, p.round, p.n_nodes, p.peer_mode);
+#pragma unroll
+      for (int j = 0; j < K; ++j) peers[j] = r.v[j];
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      // ABLATE (timing diagnostics only, results invalid): the node's own row, coalesced
+      const uint32_t src = ABLATE ? node : peers[j];
+      const uint32_t w = p.pref_in[src * p.BL + b];  // < N * BL < 2^31 (engine check)
+      ys[7 + j] = w;  // honest or Byzantine answers: never neutral
+      ns[7 + j] = SYM ? 0u : ~w;
+      cwv[j] = ~0u;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {  // old planes V_6..V_0
+    const uint32_t vi = (6 - i) < 4 ? v0[6 - i] : v1[2 - i];
+    ys[i] = WARM ? vi : (vi & C[6 - i]);
+    ns[i] = SYM ? 0u : WARM ? ~vi : (~vi & C[6 - i]);
+  }
+
+  const uint32_t live0 = ~k1[3];                         // K7 = no live record
+  const uint32_t P0 = live0 & vmask;                     // polled: live and IsValid (processor.go:95-103)
+  const uint32_t keep = active ? (live0 & ~vmask) : 0u;  // live but !IsValid: untouched (processor.go:101-103)
+
+  // ---- the shift-register planes after K votes are final for every record
+  // that survives the round: store them now (a record deleted this round is
+  // rewritten below)
+  if (active) {
+    const uint32_t dead0 = ~(P0 | keep);
+    u32x4 o0, o1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t vi = i < 4 ? v0[i] : v1[i - 4];
+      const uint32_t vs = i < K ? ys[6 + K - i] : (i - K < 4 ? v0[i - K] : v1[i - K - 4]);
+      const uint32_t vn = (vs & P0) | (vi & keep);
+      if (i < 4)
+        o0[i] = vn;
+      else
+        o1[i - 4] = vn;
+    }
+    st4<POL>(tr, grp, lane * 16u, o0);
+    st4<POL>(tr, grp + 64, 1024u + lane * 16u, o1);
+    if (!WARM) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t cs = i < K ? cwv[K - 1 - i] : C[i - K];
+        st1<POL>(tr, tp + 1024u + (uint32_t)i * 64u + lane, (1024u + (uint32_t)i * 64u + lane) * 4u,
+                 (cs & P0) | (C[i] & keep) | dead0);
+      }
+    }
+  }
+
+  uint32_t Kp[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    Kp[i] = k0[i];
+    Kp[4 + i] = k1[i];
+  }
+  uint32_t E[K], alive = P0, applied = 0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u;
+  const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
+  const uint32_t nearfin = P0 & Kp[6] & Kp[5] & Kp[4] & Kp[3];  // count >= 120: may reach 128 (K <= 8)
+  const bool det = __ballot(nearfin != 0u) != 0ull;
+  round_slots<K, SYM>(ys, ns, low3, nearfin, det, alive, A, E, c, F, applied);
+  // count_new = F ? c : count + c on planes 0..6 (survivors stay <= 127); deleted: count 128 (K7 set)
+  const uint32_t died = P0 & ~alive;
+  {
+    uint32_t cy = 0u;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const uint32_t ci = i < 4 ? c[i] : 0u;
+      const uint32_t t = Kp[i] ^ ci;
+      const uint32_t si = t ^ cy;
+      cy = (t & cy) | (Kp[i] & ci);
+      Kp[i] = ((F & ci) | (~F & si)) & ~died;
+    }
+    Kp[7] |= died;
+  }
+
+  if (active) {
+    u32x4 o2, o3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o2[i] = Kp[i];
+      o3[i] = Kp[4 + i];
+    }
+    st4<POL>(tr, grp + 128, 2048u + lane * 16u, o2);
+    st4<POL>(tr, grp + 192, 3072u + lane * 16u, o3);
+    st1<POL>(tr, tp + 1536u + lane, (1536u + lane) * 4u, A);
+    const uint32_t prow = node * p.BL + b;  // < N * BL < 2^31
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, 0x7FFFFFFF, kRsrcWord3);
+    st1<POL>(pr, p.pref_out + prow, prow * 4u, is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A);
+    if (died) {  // deleted records: canonical votes 0 / consider all-ones (rare; same lane, same addresses)
+      u32x4 d0 = pld4<false>(grp), d1 = pld4<false>(grp + 64);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        d0[i] &= ~died;
+        d1[i] &= ~died;
+      }
+      pst4<false>(grp, d0);
+      pst4<false>(grp + 64, d1);
+      if (!WARM) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) tp[1024u + (uint32_t)i * 64u + lane] |= died;
+      }
+    }
+  }
+  const uint32_t emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died);
+
+  constexpr uint32_t plane_bytes = WARM ? 2u * 17u * 4u : 2u * kPlanes * 4u;
+  constexpr uint32_t lane_bytes = plane_bytes + (REPLAY ? 8u : 4u) * K + 4u;
+  acc.applied += applied;
+  acc.died += (uint32_t)__popc(died);
+  acc.lane_bytes += active ? lane_bytes + extra_bytes : 0u;
+  acc.emitted += emitted;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum64(uint32_t v) {
+  unsigned long long x = v;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x += (unsigned long long)__shfl_xor((long long)x, d, 64);
+  return x;
+}
+
+// MODE: kModeWarm (sim, every consider plane all-ones), kModeCheck (sim, per
+// tile: the oldest consider plane decides), kModeReplay (replayed votes),
+// kModeAblate (kModeCheck with the peer gather replaced by a coalesced read of
+// the node's own row: timing diagnostics only, results invalid).
+template <int K, int MODE, int POL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeReplay ? 6 : 7))) void k_round_sweep(const RoundParams p) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave0 = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * 4u;
+  const uint32_t tiles = p.Lpad >> 6;
+  SweepAcc acc;
+  for (uint32_t tile = wave0; tile < tiles; tile += nwaves) {
+    constexpr bool AB = MODE == kModeAblate;
+    if constexpr (MODE == kModeReplay) {
+      sweep_tile<K, true, false, POL, false>(p, tile, lane, 0u, acc);
+    } else if constexpr (MODE == kModeWarm) {
+      sweep_tile<K, false, true, POL, false>(p, tile, lane, 0u, acc);
+    } else {
+      bool warm = false;
+      if (p.warm_skip) {
+        // all-ones oldest consider plane <=> all consider planes all-ones (monotone sim votes)
+        const uint32_t g = tile * 64u + lane;
+        const uint32_t c7 = g < p.L ? p.planes[(size_t)tile * (kPlanes * 64u) + 1024u + 7u * 64u + lane] : ~0u;
+        warm = __all(c7 == ~0u);
+      }
+      if (warm)
+        sweep_tile<K, false, true, POL, AB>(p, tile, lane, 4u, acc);
+      else
+        sweep_tile<K, false, false, POL, AB>(p, tile, lane, 0u, acc);
+    }
+  }
+  // one flush per wave (shard = wave index)
+  const unsigned long long s = wave_sum64(acc.applied);
+  const unsigned long long f = wave_sum64(acc.died);
+  const unsigned long long by = wave_sum64(acc.lane_bytes) + 8ull * acc.emitted;
+  if (lane == 0) {
+    const uint32_t shard = wave0 % p.log_shards;
+    if (s) atomicAdd(&p.applied[shard], s);
+    if (f) atomicAdd(&p.finalized[shard], f);
+    if (by) atomicAdd(&p.bytes[shard], by);
+  }
+}
+
+template <int K, int MODE>
+hipError_t launch_mode(const RoundParams& p, uint32_t grid, hipStream_t s) {
+  // write-through store policies are built for k = 8 only (the measured workloads)
+  const uint32_t pol = (K == 8 && p.store_policy >= 2) ? p.store_policy : (p.plane_nt ? 1u : 0u);
+  switch (pol) {
+    case 0: hipLaunchKernelGGL((k_round_sweep<K, MODE, 0>), dim3(grid), dim3(256), 0, s, p); break;
+    case 1: hipLaunchKernelGGL((k_round_sweep<K, MODE, 1>), dim3(grid), dim3(256), 0, s, p); break;
+    default:
+      if constexpr (K == 8) {
+        if (pol == 2)
+          hipLaunchKernelGGL((k_round_sweep<K, MODE, 2>), dim3(grid), dim3(256), 0, s, p);
+        else
+          hipLaunchKernelGGL((k_round_sweep<K, MODE, 3>), dim3(grid), dim3(256), 0, s, p);
+      }
+  }
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_sweep_k(const RoundParams& p, bool replay, uint32_t blocks, hipStream_t s) {
+  const uint32_t need = (p.Lpad / 64u + 3u) / 4u;
+  const uint32_t grid = std::max(1u, blocks ? std::min(blocks, need) : need);
+  if (replay) return launch_mode<K, kModeReplay>(p, grid, s);
+  if (p.ablate_gather) return launch_mode<K, kModeAblate>(p, grid, s);
+  if (p.warm_skip && p.warm_all) return launch_mode<K, kModeWarm>(p, grid, s);
+  return launch_mode<K, kModeCheck>(p, grid, s);
+}
+
+template <int K>
+hipError_t occupancy_k(bool replay, int* bpc) {
+  return replay ? hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, k_round_sweep<K, kModeReplay, 1>, 256, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, k_round_sweep<K, kModeWarm, 1>, 256, 0);
+}
+
+}  // namespace
+
+#define AVK_SWEEP_SWITCH(k, CALL) \
+  switch (k) {                    \
+    case 1: return CALL(1);       \
+    case 2: return CALL(2);       \
+    case 3: return CALL(3);       \
+    case 4: return CALL(4);       \
+    case 5: return CALL(5);       \
+    case 6: return CALL(6);       \
+    case 7: return CALL(7);       \
+    case 8: return CALL(8);       \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s) {
+#define AVK_SW(K) launch_sweep_k<K>(p, replay, blocks, s)
+  AVK_SWEEP_SWITCH(k, AVK_SW)
+#undef AVK_SW
+}
+
+hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cus) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  e = hipDeviceGetAttribute(cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+#define AVK_OCC(K) occupancy_k<K>(replay, blocks_per_cu)
+  AVK_SWEEP_SWITCH(k, AVK_OCC)
+#undef AVK_OCC
+}
+
+}  // namespace avk

@@ -174,7 +174,11 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
 
 /* ---- tuning ----
  * "plane_nt"  (0/1): stream the state planes with non-temporal loads/stores.
- * "warm_skip" (0)  : disable skipping all-ones consider planes (A/B only). */
+ * "warm_skip" (0)  : disable skipping all-ones consider planes (A/B only).
+ * "kernel"    (1/2): round kernel for the uncapped path: 2 = persistent sweep
+ *                    (default, k <= 8), 1 = one wave per tile (A/B only).
+ * "sweep_blocks"   : workgroups of the sweep grid (0 = one wave per tile,
+ *                    -1 = every resident workgroup once, the default). */
 int av_set_option(av_engine* e, const char* name, int64_t value);
 
 /* ---- measurement ---- */

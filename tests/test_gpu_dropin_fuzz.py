@@ -20,12 +20,12 @@ def check(eng, sim, where):
     assert np.array_equal(got, exp), where
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
-def test_dropin_fuzz(oracle, seed):
+@pytest.mark.parametrize("seed,k", [(1, 4), (2, 4), (3, 4), (4, 8), (5, 8)])
+def test_dropin_fuzz(oracle, seed, k):
     rng = np.random.default_rng(seed)
     n, m = 5, 150
-    eng = avhip.Engine(n, m, k=4, seed=seed)  # no records (AV_INIT_NONE)
-    sim = oracle.Sim(n, m, 4, seed=seed, init_mode=0)
+    eng = avhip.Engine(n, m, k=k, seed=seed)  # no records (AV_INIT_NONE)
+    sim = oracle.Sim(n, m, k, seed=seed, init_mode=0)
     valid = np.ones(m, bool)
     for step in range(400):
         op = rng.integers(0, 10)

@@ -17,8 +17,12 @@ def rows(u):
     return [tuple(int(v) for v in r) for r in np.asarray(u).tolist()]
 
 
-def make_pair(oracle, n, m, k, seed=7, peer_mode=0, byz=0, init_mode=3, init_param=P80, log_capacity=0):
+def make_pair(oracle, n, m, k, seed=7, peer_mode=0, byz=0, init_mode=3, init_param=P80, log_capacity=0,
+              kernel=2, sweep_blocks=None):
     eng = avhip.Engine(n, m, k=k, seed=seed, peer_mode=peer_mode, byz_threshold=byz, log_capacity=log_capacity)
+    eng.set_option("kernel", kernel)
+    if sweep_blocks is not None:
+        eng.set_option("sweep_blocks", sweep_blocks)
     eng.init_records(init_mode, init_param)
     sim = oracle.Sim(n, m, k, seed=seed, peer_mode=peer_mode, byz_threshold=byz, init_mode=init_mode,
                      init_param=init_param)
@@ -64,10 +68,12 @@ SIM_CASES = [
 ]
 
 
+@pytest.mark.parametrize("kernel", [2, 1], ids=["sweep", "per_tile"])
 @pytest.mark.parametrize("case", SIM_CASES, ids=lambda c: f"n{c['n']}m{c['m']}k{c['k']}")
-def test_sim_rounds_parity(oracle, case):
+def test_sim_rounds_parity(oracle, case, kernel):
     eng, sim = make_pair(oracle, case["n"], case["m"], case["k"], seed=case["seed"],
-                         peer_mode=case.get("peer_mode", 0), byz=case.get("byz", 0), init_mode=case["init_mode"])
+                         peer_mode=case.get("peer_mode", 0), byz=case.get("byz", 0), init_mode=case["init_mode"],
+                         kernel=kernel)
     total_applied = 0
     for r in range(40):
         if r == 5:  # target invalidated mid-run (avalanche_test.go:534 pattern), later revalidated
@@ -86,6 +92,37 @@ def test_sim_rounds_parity(oracle, case):
     assert eng.round == 40
 
 
+@pytest.mark.parametrize("blocks", [0, 1, 3, 7])
+def test_sweep_grid_parity(oracle, blocks):
+    """The persistent sweep kernel with a grid smaller than the tile count
+    (every wave walks several tiles; counters flushed once per wave) and with
+    one wave per tile (0), across the warm-up, the warm steady state and
+    finalization (rounds 16-17: the exact per-vote path with deletion)."""
+    n, m, k = 700, 333, 8
+    eng, sim = make_pair(oracle, n, m, k, seed=17, byz=BYZ20, init_mode=2, sweep_blocks=blocks)
+    total = 0
+    for r in range(20):
+        eng.run_rounds(1)
+        exp_u, applied = sim.run_round()
+        total += applied
+        assert rows(eng.fetch_updates()) == rows(exp_u), f"round {r}"
+        assert eng.applied_votes() == total, f"round {r}"
+        if r % 4 == 3 or r >= 15:
+            assert_same_state(eng, sim, f"round {r}")
+    assert eng.finalized_count() > 0
+
+
+@pytest.mark.parametrize("kernel", [2, 1], ids=["sweep", "per_tile"])
+def test_tiny_network_peers_parity(oracle, kernel):
+    """N - 1 <= k: every other node is polled (the sampler's degenerate branch)."""
+    eng, sim = make_pair(oracle, 5, 90, 8, seed=2, init_mode=3, kernel=kernel)
+    for r in range(20):
+        eng.run_rounds(1)
+        exp_u, _ = sim.run_round()
+        assert rows(eng.fetch_updates()) == rows(exp_u), r
+    assert_same_state(eng, sim)
+
+
 def test_sim_capped_parity(oracle):
     """M > 4096: the workgroup-scan path enforces the 4096 poll cap."""
     eng, sim = make_pair(oracle, 20, 5000, 8, seed=3, byz=BYZ20, init_mode=3)
@@ -98,9 +135,10 @@ def test_sim_capped_parity(oracle):
 
 
 # ------------------------------------------------------------------ rounds, replay mode
-@pytest.mark.parametrize("n,m,k", [(9, 300, 8), (6, 4500, 8), (5, 4097, 2), (4, 8300, 8)])
-def test_replay_parity(oracle, n, m, k):
-    eng, sim = make_pair(oracle, n, m, k, seed=21, init_mode=3)
+@pytest.mark.parametrize("n,m,k,kernel", [(9, 300, 8, 2), (9, 300, 8, 1), (70, 1000, 5, 2), (6, 4500, 8, 2),
+                                          (5, 4097, 2, 2), (4, 8300, 8, 2)])
+def test_replay_parity(oracle, n, m, k, kernel):
+    eng, sim = make_pair(oracle, n, m, k, seed=21, init_mode=3, kernel=kernel)
     applied_total = 0
     for r in range(12):
         errs = oracle.gen_replay_errs(21, r, 0, n, m, k)
@@ -271,19 +309,20 @@ def test_node_shard_needs_comm():
 def test_c4_shape_properties():
     """C4 shape at 1/10 scale (100k nodes x 1000 targets, k=8, Bernoulli(0.8)):
     rounds 0-15 keep every record live (finalization needs >= 134 votes), so
-    applied votes == N*M*k per round; two runs are identical; the published
-    preference equals the records' accepted bit."""
+    applied votes == N*M*k per round; both round kernels give identical
+    results; the published preference equals the records' accepted bit."""
     n, m, k = 100_000, 1000, 8
     digests = []
-    for _ in range(2):
+    for kernel, warm_lane_bytes in ((1, 176), (2, 172)):
         e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4)
+        e.set_option("kernel", kernel)
         e.init_records(avhip.INIT_BERNOULLI, P80)
         lanes = e.layout_info()["lanes"]
         e.run_rounds(1)  # round 0: consider planes fill up (236 B per 32-record lane)
         assert e.alg_bytes() == lanes * 236 + 8 * e.updates_count()
         b1, u1 = e.alg_bytes(), e.updates_count()
-        e.run_rounds(15)  # warm: the all-ones consider planes are skipped (176 B per lane)
-        assert e.alg_bytes() - b1 == 15 * lanes * 176 + 8 * (e.updates_count() - u1)
+        e.run_rounds(15)  # warm: the all-ones consider planes are skipped (176 / 172 B per lane)
+        assert e.alg_bytes() - b1 == 15 * lanes * warm_lane_bytes + 8 * (e.updates_count() - u1)
         assert e.applied_votes() == n * m * k * 16
         u = e.fetch_updates()
         assert not np.isin(u[:, 4], [avhip.STATUS_FINALIZED, avhip.STATUS_INVALID]).any()
@@ -291,7 +330,7 @@ def test_c4_shape_properties():
         assert ((recs >> 17) < 128).all()
         pref = e.read_pref(0, n, 0, m)
         assert np.array_equal(pref, ((recs >> 16) & 1).astype(np.uint8))
-        digests.append((recs.tobytes().__hash__(), len(u)))
+        digests.append((hash(recs.tobytes()), hash(u.tobytes())))
         e.close()
     assert digests[0] == digests[1]
 

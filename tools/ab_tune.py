@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of round-kernel variants in ONE process (guide §5.4
-rule 24) on the C4 workload, plus the per-GPU kernel time of a target shard
-of the same network (what each rank runs at 2/4/8-way target sharding).
+rule 24) on the C4 workload, and the per-GPU kernel time of a target shard of
+the same network (what each rank runs at 2/4/8-way target sharding).
 
-    python tools/ab_tune.py [--rounds 6] [--json out.json]
+    python tools/ab_tune.py [--rounds 6] [--json out.json] [--variants sweep,per_tile,...]
+
+Variants: sweep (k_round_sweep, persistent grid), sweep_w1 (sweep kernel,
+one wave per tile), per_tile (k_round_fast), ablate (sweep, peer gather
+replaced by a coalesced read: timing only, results invalid).
 """
 import argparse
 import json
@@ -22,6 +26,18 @@ from avhip import sharding  # noqa: E402
 N, M, K = 1_000_000, 1000, 8
 P80 = int(0.8 * 2**32)
 
+VARIANTS = {
+    "sweep": dict(kernel=2),
+    "sweep_w1": dict(kernel=2, sweep_blocks=0),
+    "sweep_res": dict(kernel=2, sweep_blocks=-1),
+    "per_tile": dict(kernel=1),
+    "ablate": dict(kernel=2, ablate_gather=1),
+    "w1_sc1": dict(kernel=2, sweep_blocks=0, store_policy=2),
+    "w1_ntsc1": dict(kernel=2, sweep_blocks=0, store_policy=3),
+    "res_sc1": dict(kernel=2, sweep_blocks=-1, store_policy=2),
+    "w1_plain": dict(kernel=2, sweep_blocks=0, plane_nt=0),
+}
+
 
 def one_round_ms(e):
     e.set_timing(True)
@@ -35,63 +51,46 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--variants", default="sweep,sweep_w1,per_tile,ablate")
+    ap.add_argument("--shards", default="1,2,4,8")
     args = ap.parse_args()
+    names = args.variants.split(",")
     out = {}
-
-    # --- A/B: non-temporal planes on/off, consider-plane skip on/off (both engines warm)
-    warm = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, log_capacity=1 << 28)
-    cold = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, log_capacity=1 << 28)
-    for e in (warm, cold):
-        e.init_records(avhip.INIT_BERNOULLI, P80)
-    cold.set_option("warm_skip", 0)
-    for e in (warm, cold):
-        e.run_rounds(2)
-        e.synchronize()
-        try:
-            e.fetch_updates(decode=False)
-        except avhip.LogOverflow:
-            pass
-    lanes = warm.layout_info()["lanes"]
-    times = {"skip": [], "skip+nt": [], "noskip": [], "noskip+nt": []}
-    for _ in range(args.rounds):
-        for name, e, nt in (("skip", warm, 0), ("skip+nt", warm, 1), ("noskip", cold, 0), ("noskip+nt", cold, 1)):
-            e.set_option("plane_nt", nt)
-            times[name].append(one_round_ms(e))
-    for name, ts in times.items():
-        per_lane = 176 if name.startswith("skip") else 236
-        med = statistics.median(ts)
-        out[name] = {"median_ms": med, "min_ms": min(ts),
-                     "alg_GBs": lanes * per_lane / (med * 1e-3) / 1e9}
-    warm.close()
-    cold.close()
-
-    # --- per-rank kernel time at G-way target sharding (rank 0's shard, warm), nt on/off interleaved
-    for g in (1, 2, 4, 8):
+    for g in [int(x) for x in args.shards.split(",")]:
         t0, t1 = sharding.target_shard(M, g, 0)
-        e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, target_range=(t0, t1), log_capacity=1 << 27)
-        e.init_records(avhip.INIT_BERNOULLI, P80)
-        e.run_rounds(2)
-        e.synchronize()
-        try:
-            e.fetch_updates(decode=False)
-        except avhip.LogOverflow:
-            pass
-        variants = {"": (0, 0), "+nt": (1, 0), "+nt+ablate_gather": (1, 1)}
-        ts = {v: [] for v in variants}
-        b0 = e.alg_bytes()
-        for _ in range(args.rounds):
-            for v, (nt, abl) in variants.items():
-                e.set_option("plane_nt", nt)
-                e.set_option("ablate_gather", abl)
+        # one engine per variant, all at the same round with the same state
+        # (rounds 2.. stay below 15: no record can finalize, every tile is warm)
+        engs = {}
+        for v in names:
+            e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, target_range=(t0, t1), log_capacity=1 << 26)
+            opts = VARIANTS[v]
+            e.set_option("kernel", opts["kernel"])
+            e.set_option("ablate_gather", opts.get("ablate_gather", 0))
+            for opt in ("sweep_blocks", "store_policy", "plane_nt"):
+                if opt in opts:
+                    e.set_option(opt, opts[opt])
+            e.init_records(avhip.INIT_BERNOULLI, P80)
+            e.run_rounds(2)
+            e.synchronize()
+            e.discard_updates()
+            engs[v] = e
+        lanes = engs[names[0]].layout_info()["lanes"]
+        ts = {v: [] for v in names}
+        bpl = {}
+        for _ in range(min(args.rounds, 12)):
+            for v, e in engs.items():
+                b0 = e.alg_bytes()
                 ts[v].append(one_round_ms(e))
-        e.set_option("ablate_gather", 0)
-        bpl = (e.alg_bytes() - b0) / (len(variants) * args.rounds)
-        for v in variants:
+                bpl[v] = (e.alg_bytes() - b0) / lanes
+                e.discard_updates()
+        for v in names:
             med = statistics.median(ts[v])
-            out[f"shard{g}{v}"] = {
-                "targets": [t0, t1], "median_ms": med, "alg_GBs": bpl / (med * 1e-3) / 1e9,
+            out[f"shard{g}_{v}"] = {
+                "targets": [t0, t1], "median_ms": med, "min_ms": min(ts[v]),
+                "alg_GBs": bpl[v] * lanes / (med * 1e-3) / 1e9, "alg_bytes_per_lane": bpl[v],
                 "updates_per_s_per_gpu": N * (t1 - t0) * K / (med * 1e-3)}
-        e.close()
+        for e in engs.values():
+            e.close()
     print(json.dumps(out, indent=1))
     if args.json:
         with open(args.json, "w") as f:

@@ -28,7 +28,7 @@ step() {  # name, timeout-seconds, command...
 for s in "$@"; do
   case $s in
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step pytest_gpu 1500 python -m pytest tests -m gpu -x -q -p no:cacheprovider ;;
+    tests) step pytest_gpu 1500 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py ;;
     rccl2) step rccl2 240 python tools/rccl_two_rank_probe.py ;;
@@ -37,6 +37,9 @@ for s in "$@"; do
     rehearse4) step rehearse4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
             --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 4 --rehearse-one-gpu --no-secondary ;;
     ab) step ab 900 python tools/ab_tune.py --json $OUT/ab.json ;;
+    ab1) step ab1 600 python tools/ab_tune.py --shards 1 --json $OUT/ab1.json ;;
+    abpol) step abpol 600 python tools/ab_tune.py --shards 1,8 --variants sweep_w1,sweep_res,w1_sc1,w1_ntsc1,res_sc1,w1_plain --json $OUT/abpol.json ;;
+    gprobe) step gprobe 120 go-avalanche_amd/bin/gather_probe 20 ;;
     conv_c3) step conv_c3 900 python tools/run_to_finalization.py --workload c3 --json $OUT/conv_c3.json ;;
     conv_c5) step conv_c5 900 python tools/run_to_finalization.py --workload c5 --max-rounds 64 --json $OUT/conv_c5.json ;;
     conv_c4) step conv_c4 900 python tools/run_to_finalization.py --workload c4 --max-rounds 64 --json $OUT/conv_c4.json ;;
