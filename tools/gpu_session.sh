@@ -57,7 +57,7 @@ for s in "$@"; do
     calib_write) step calib_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/calib_write -o calib -- \
             go-avalanche_amd/bin/pmc_calib ;;
     pmc_sum) step pmc_sum 120 python tools/pmc_summary.py --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write \
-            --fetch $OUT/pmc_fetch --write $OUT/pmc_write --out $OUT/pmc_traffic_c4.json ;;
+            --fetch $OUT/pmc_fetch --write $OUT/pmc_write --kernel k_round_sweep --read-x1 36 --out $OUT/pmc_traffic_c4.json ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
