@@ -718,6 +718,16 @@ int av_updates_count(av_engine* e, int64_t* n) {
   return AV_OK;
 }
 
+int av_update_log_overflowed(av_engine* e, int32_t* out) {
+  AV_ENTER(e);
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  uint32_t ovf = 0;
+  AV_HIP(hipMemcpyAsync(&ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  *out = ovf ? 1 : 0;
+  return AV_OK;
+}
+
 int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
   AV_ENTER(e);
   AV_CHECK(n_out && (cap == 0 || out), AV_ERR_INVALID_ARG, "null argument");

@@ -284,6 +284,14 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
+// Raise the log-overflow flag: a relaxed check first and a plain store (the
+// flag only ever goes 0 -> 1 inside a round), so that a full log does not
+// put every wave of the grid behind one atomic on one word.
+__device__ __forceinline__ void note_overflow(const RoundParams& p, uint32_t lane) {
+  if (lane == 0 && __hip_atomic_load(p.log_overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    __hip_atomic_store(p.log_overflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // End-of-round StatusUpdate emission (processor.go:111) for one wave: one
 // atomic per emitting wave on a sharded log counter reserves the wave's
 // total; then, per slot, every iteration lets each lane with updates left
@@ -316,6 +324,10 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
   }
   uint64_t* dst = p.log + (size_t)shard * p.log_cap;
   uint32_t run = base;  // wave-uniform
+  if (base >= p.log_cap) {  // shard already full: nothing can be stored
+    note_overflow(p, lane);
+    return total;
+  }
   bool ovf = false;
   for (int j = 0; j < K; ++j) {  // not unrolled (data-dependent inner loop); E/Aj stay in VGPRs
     uint32_t e = E[j];
@@ -337,7 +349,7 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
       run += (uint32_t)__popcll(act);
     }
   }
-  if (__ballot(ovf) != 0ull && lane == 0) atomicOr(p.log_overflow, 1u);  // one atomic per wave
+  if (__ballot(ovf) != 0ull) note_overflow(p, lane);
   return total;
 }
 

@@ -70,7 +70,7 @@ EXPORTED = [
     "av_init_records", "av_add_targets", "av_set_valid", "av_register_votes", "av_is_accepted",
     "av_get_confidence", "av_get_invs", "av_run_rounds", "av_replay_round_errs", "av_replay_prepare",
     "av_replay_rounds", "av_synchronize", "av_round_index", "av_updates_count", "av_fetch_updates",
-    "av_applied_votes", "av_alg_bytes", "av_finalized_count", "av_live_records", "av_discard_updates", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
+    "av_update_log_overflowed", "av_applied_votes", "av_alg_bytes", "av_finalized_count", "av_live_records", "av_discard_updates", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
 ]
 
@@ -109,6 +109,7 @@ def lib():
         "av_round_index": (i32, [_vp, P(i64)]),
         "av_updates_count": (i32, [_vp, P(i64)]),
         "av_fetch_updates": (i32, [_vp, _vp, i64, P(i64)]),
+        "av_update_log_overflowed": (i32, [_vp, P(i32)]),
         "av_applied_votes": (i32, [_vp, P(i64)]),
         "av_alg_bytes": (i32, [_vp, P(i64)]),
         "av_finalized_count": (i32, [_vp, P(i64)]),
@@ -300,6 +301,11 @@ class Engine:
         out = C.c_int64(0)
         _check(lib().av_live_records(self._h, int(honest_only), C.byref(out)))
         return out.value
+
+    def log_overflowed(self) -> bool:
+        v = C.c_int32()
+        _check(lib().av_update_log_overflowed(self._h, C.byref(v)))
+        return bool(v.value)
 
     def discard_updates(self):
         _check(lib().av_discard_updates(self._h))

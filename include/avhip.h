@@ -148,6 +148,9 @@ int av_round_index(av_engine* e, int64_t* out);
 
 /* ---- outputs ---- */
 int av_updates_count(av_engine* e, int64_t* n);
+/* Whether the device StatusUpdate log overflowed since the last fetch/discard
+ * (the next av_fetch_updates will then fail with AV_ERR_OVERFLOW). */
+int av_update_log_overflowed(av_engine* e, int32_t* out);
 /* All StatusUpdates since the previous fetch, sorted canonical; clears the
  * log. AV_ERR_OVERFLOW if the device log or `cap` overflowed (*n_out holds the
  * required count when cap is too small). */

@@ -348,3 +348,19 @@ def test_run_to_finalization_properties(oracle):
     assert (u[:, 0] == 16).all() and (u[:, 2] == 5).all()  # 16*8 + 6 = 134th vote
     assert e.applied_votes() == n * m * 134
     assert (e.read_records() == (avhip.ABSENT_WORD | 1 << 16)).all()
+
+
+def test_update_log_overflow_reported(oracle):
+    """A device StatusUpdate log too small for a round: the round's state stays
+    exact, the overflow is reported (av_update_log_overflowed, then
+    AV_ERR_OVERFLOW from fetch), and the log works again after the fetch."""
+    n, m, k = 300, 517, 8
+    eng, sim = make_pair(oracle, n, m, k, seed=5, byz=BYZ20, init_mode=4, log_capacity=64)
+    eng.run_rounds(3)
+    for _ in range(3):
+        sim.run_round()
+    assert eng.log_overflowed()
+    with pytest.raises(avhip.LogOverflow):
+        eng.fetch_updates()
+    assert not eng.log_overflowed()
+    assert_same_state(eng, sim, "after overflow")

@@ -23,8 +23,8 @@ import torch  # noqa: E402,F401
 import avhip  # noqa: E402
 from avhip import sharding  # noqa: E402
 
-N, M, K = 1_000_000, 1000, 8
-P80 = int(0.8 * 2**32)
+sys.path.insert(0, ROOT)
+from bench import WORKLOADS  # noqa: E402
 
 VARIANTS = {
     "sweep": dict(kernel=2),
@@ -53,7 +53,10 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--variants", default="sweep,sweep_w1,per_tile,ablate")
     ap.add_argument("--shards", default="1,2,4,8")
+    ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     args = ap.parse_args()
+    N, M, K, init_mode, init_param, byz, replay, _ = WORKLOADS[args.workload]
+    assert not replay, "sim-mode workloads only"
     names = args.variants.split(",")
     out = {}
     for g in [int(x) for x in args.shards.split(",")]:
@@ -62,14 +65,15 @@ def main():
         # (rounds 2.. stay below 15: no record can finalize, every tile is warm)
         engs = {}
         for v in names:
-            e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, target_range=(t0, t1), log_capacity=1 << 26)
+            e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz, target_range=(t0, t1),
+                             log_capacity=1 << 27)
             opts = VARIANTS[v]
             e.set_option("kernel", opts["kernel"])
             e.set_option("ablate_gather", opts.get("ablate_gather", 0))
             for opt in ("sweep_blocks", "store_policy", "plane_nt"):
                 if opt in opts:
                     e.set_option(opt, opts[opt])
-            e.init_records(avhip.INIT_BERNOULLI, P80)
+            e.init_records(init_mode, init_param)
             e.run_rounds(2)
             e.synchronize()
             e.discard_updates()
@@ -85,7 +89,7 @@ def main():
                 e.discard_updates()
         for v in names:
             med = statistics.median(ts[v])
-            out[f"shard{g}_{v}"] = {
+            out[f"{args.workload}_shard{g}_{v}"] = {
                 "targets": [t0, t1], "median_ms": med, "min_ms": min(ts[v]),
                 "alg_GBs": bpl[v] * lanes / (med * 1e-3) / 1e9, "alg_bytes_per_lane": bpl[v],
                 "updates_per_s_per_gpu": N * (t1 - t0) * K / (med * 1e-3)}

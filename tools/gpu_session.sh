@@ -38,6 +38,7 @@ for s in "$@"; do
             --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 4 --rehearse-one-gpu --no-secondary ;;
     ab) step ab 900 python tools/ab_tune.py --json $OUT/ab.json ;;
     ab1) step ab1 600 python tools/ab_tune.py --shards 1 --json $OUT/ab1.json ;;
+    abc3) step abc3 600 python tools/ab_tune.py --workload c3 --shards 1 --variants sweep,per_tile,ablate --json $OUT/abc3.json ;;
     abpol) step abpol 600 python tools/ab_tune.py --shards 1,8 --variants sweep_w1,sweep_res,w1_sc1,w1_ntsc1,res_sc1,w1_plain --json $OUT/abpol.json ;;
     gprobe) step gprobe 120 go-avalanche_amd/bin/gather_probe 20 ;;
     conv_c3) step conv_c3 900 python tools/run_to_finalization.py --workload c3 --json $OUT/conv_c3.json ;;
