@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--plane-nt", type=int, default=None, help="override the plane_nt tuning option")
+    ap.add_argument("--kernel", type=int, default=None, choices=[1, 2],
+                    help="round kernel generation (A/B only; default: the engine's choice)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 rehearsal on a 1-GPU box: every rank on device 0, gloo for the host-side "
                          "barrier/reductions (target sharding only; not a measurement)")
@@ -117,6 +119,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     eng = avhip.Engine(n, m, log_capacity=min(est_updates, 1 << 29), **kw)
     if args.plane_nt is not None:
         eng.set_option("plane_nt", args.plane_nt)
+    if args.kernel is not None:
+        eng.set_option("kernel", args.kernel)
     eng.init_records(init_mode, init_param)
     if world > 1 and args.shard == "nodes":
         obj = [avhip.comm_unique_id() if rank == 0 else None]
@@ -172,8 +176,9 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     # launch (236 B per 32-record lane at k=8, 176 B once the consider planes
     # are warm, + 8 B per StatusUpdate) / its HIP-event average launch time.
     achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
-    kname = ("k_round_capped" if info["capped"] else "k_round_sweep" if k <= 8 else "k_round_fast") + \
-        f"<{k},{'true' if replay else 'false'}>"
+    gen2 = k <= 8 and args.kernel != 1
+    kname = (("k_round_node" if gen2 else "k_round_capped") if info["capped"]
+             else ("k_round_sweep" if gen2 else "k_round_fast")) + f"<{k},{'true' if replay else 'false'}>"
     return {
         "desc": desc, "n": n, "m": m, "k": k, "value": value, "elapsed": elapsed, "applied": applied,
         "emitted": emitted, "info": info, "kavg_ms": kavg_ms, "alg_bytes": alg_bytes, "achieved": achieved,

@@ -81,7 +81,8 @@ struct av_engine {
   bool c_monotone = true;
   bool plane_nt = true;  // tuning option "plane_nt" (A/B on MI355X: -8 % kernel time warm, -16 % cold)
   bool ablate_gather = false;  // diagnostics option "ablate_gather" (invalid results)
-  // round kernel: 2 = k_round_sweep (persistent, k <= 8, uncapped), 1 = k_round_fast (option "kernel")
+  // round kernels (option "kernel"): 2 = k_round_sweep (uncapped) / k_round_node (capped), k <= 8;
+  // 1 = k_round_fast / k_round_capped (the first versions; any k, A/B baseline)
   int kernel = 2;
   uint32_t sweep_blocks = 0;  // resident workgroups of the sweep grid (option "sweep_blocks"; 0 = one wave per tile)
   // every consider plane of every lane is all-ones: set after a sim round with k >= 8 in which every
@@ -195,6 +196,8 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   }
   if (sweep)
     AV_HIP(avk::launch_round_sweep(p, e->k, replay != nullptr, e->sweep_blocks, e->stream));
+  else if (e->kernel == 2 && e->k <= 8 && e->capped)
+    AV_HIP(avk::launch_round_node(p, e->k, replay != nullptr, e->stream));
   else
     AV_HIP(avk::launch_round(p, e->k, replay != nullptr, e->capped, e->stream));
   if (replay)

@@ -89,6 +89,8 @@ hipError_t launch_round(const RoundParams& p, int k, bool replay, bool capped, h
 // Persistent streaming round kernel (round_sweep.hip), uncapped path, k <= 8:
 // `blocks` workgroups of 256 threads sweep the tiles; 0 = one wave per tile.
 hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s);
+// Capped round (M > 4096, k <= 8; round_node.hip): one workgroup per node.
+hipError_t launch_round_node(const RoundParams& p, int k, bool replay, hipStream_t s);
 // Resident 256-thread workgroups per CU for the sweep kernel and the CU count.
 hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cus);
 

@@ -1,0 +1,243 @@
+// Round kernel under the 4096 poll cap (M > 4096, k <= 8): one workgroup per
+// node, one lane per 32-record block. GetInvsForNextPoll (processor.go:144-170)
+// hands the node's first 4096 live, valid targets in ascending target order
+// (rule R1); a workgroup prefix count of the live-valid bits selects them.
+//
+// The cap set changes inside a round only when a polled record finalizes
+// (it is deleted and the next record moves up). So:
+//  * no polled record of the node has count >= 120 (the usual case): the poll
+//    set is selected once, and the round runs like k_round_sweep — per-slot
+//    threshold networks, deferred confidence update, the shift registers of
+//    the polled records advanced by k votes at once (round_slots.h);
+//  * otherwise: the exact per-vote path, re-selecting the poll set before
+//    every slot (the first version's algorithm, kernels.hip k_round_capped).
+// Same layout, outputs and counters as k_round_capped; V/K move as dwordx4.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+#include "round_common.h"
+#include "round_slots.h"
+
+namespace avk {
+namespace {
+
+// The first (4096 - already) set bits of `bits`, in bit order.
+__device__ __forceinline__ uint32_t lowest_bits(uint32_t bits, uint32_t n) {
+  uint32_t out = 0u;
+  for (uint32_t q = 0; q < n; ++q) {
+    const uint32_t low = bits & (0u - bits);
+    out |= low;
+    bits ^= low;
+  }
+  return out;
+}
+
+// Poll-set selection (processor.go:165-167): the first kMaxPoll set bits of
+// `live` over the workgroup's lanes in lane order. Two barriers; wsum is
+// double-buffered by `phase`.
+__device__ __forceinline__ uint32_t cap_select(uint32_t live, uint32_t lane, uint32_t wave, uint32_t (&wsum)[2][16],
+                                               uint32_t phase) {
+  const uint32_t c = (uint32_t)__popc(live);
+  const uint32_t incl = wave_incl_scan(c, lane);
+  if (lane == 63u) wsum[phase][wave] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t q = 0; q < wave; ++q) before += wsum[phase][q];
+  const uint32_t excl = before + incl - c;
+  if (excl >= kMaxPoll) return 0u;
+  if (excl + c <= kMaxPoll) return live;
+  return lowest_bits(live, kMaxPoll - excl);
+}
+
+template <int K, bool REPLAY, bool NT, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
+  __shared__ uint32_t wsum[2][16];
+  const uint32_t nl = blockIdx.x;
+  const uint32_t b = threadIdx.x;
+  const uint32_t lane = b & 63u, wave = b >> 6;
+  const bool active = b < p.BL;
+  const uint32_t bc = active ? b : p.BL - 1u;  // inactive lanes read a valid lane, never store
+  const uint32_t g = nl * p.BL + bc;
+  const uint32_t node = p.n0 + nl;
+
+  // ---- state (tile layout of kernels.h: per-lane dwordx4 V/K groups, dword C/A planes)
+  uint32_t* const tp = p.planes + (size_t)(g >> 6) * (kPlanes * 64u);
+  const uint32_t tl = g & 63u;
+  u32x4* const grp = reinterpret_cast<u32x4*>(tp) + tl;
+  const u32x4 v0 = pld4<NT>(grp), v1 = pld4<NT>(grp + 64), k0 = pld4<NT>(grp + 128), k1 = pld4<NT>(grp + 192);
+  uint32_t A = pld<NT>(tp + 1536u + tl);
+  uint32_t C[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
+  const uint32_t vmask = active ? p.valid[bc] : 0u;
+
+  // ---- votes of this round: ys/ns hold y/n of [V_6..V_0, w_0..w_{K-1}]
+  uint32_t ys[7 + K], ns[7 + K], cwv[K];
+  if constexpr (REPLAY) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t cw = p.replay[(size_t)(2 * j + 1) * p.Lpad + g];
+      const uint32_t yw = p.replay[(size_t)(2 * j) * p.Lpad + g] & cw;  // err == 0 implies considered
+      ys[7 + j] = yw;
+      ns[7 + j] = ~yw & cw;
+      cwv[j] = cw;
+    }
+  } else {
+    uint32_t peers[K];
+    draw_peers<K>(p, node, nl, nl, 1u, lane, peers);  // every lane of the workgroup is the same node
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t w = p.pref_in[peers[j] * p.BL + bc];  // < N * BL < 2^31 (engine check)
+      ys[7 + j] = w;
+      ns[7 + j] = ~w;
+      cwv[j] = ~0u;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {  // old planes V_6..V_0
+    const uint32_t vi = (6 - i) < 4 ? v0[6 - i] : v1[2 - i];
+    ys[i] = vi & C[6 - i];
+    ns[i] = ~vi & C[6 - i];
+  }
+
+  const uint32_t live0 = ~k1[3];
+  const uint32_t P0 = live0 & vmask;  // live and IsValid (processor.go:95-103)
+  uint32_t polled = cap_select(P0, lane, wave, wsum, 0u);
+  uint32_t Kp[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    Kp[i] = k0[i];
+    Kp[4 + i] = k1[i];
+  }
+  const uint32_t nearfin = polled & Kp[6] & Kp[5] & Kp[4] & Kp[3];  // count >= 120
+  const bool exact = __syncthreads_or(nearfin != 0u) != 0;          // workgroup-uniform
+
+  uint32_t E[K], applied = 0u, died = 0u;
+  u32x4 o0, o1;
+  uint32_t Cn[8];
+  if (!exact) {
+    // the poll set is fixed for the round: shift every polled record by K votes
+    uint32_t alive = polled, c[4] = {0u, 0u, 0u, 0u}, F = 0u;
+    const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
+    round_slots<K, false>(ys, ns, low3, 0u, false, alive, A, E, c, F, applied);
+    applied = (uint32_t)K * (uint32_t)__popc(polled);
+    uint32_t cy = 0u;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const uint32_t ci = i < 4 ? c[i] : 0u;
+      const uint32_t t = Kp[i] ^ ci;
+      const uint32_t si = t ^ cy;
+      cy = (t & cy) | (Kp[i] & ci);
+      Kp[i] = (F & ci) | (~F & si);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t vi = i < 4 ? v0[i] : v1[i - 4];
+      const uint32_t vs = i < K ? ys[6 + K - i] : (i - K < 4 ? v0[i - K] : v1[i - K - 4]);
+      const uint32_t vn = (vs & polled) | (vi & ~polled);
+      if (i < 4)
+        o0[i] = vn;
+      else
+        o1[i - 4] = vn;
+      const uint32_t cs = i < K ? cwv[K - 1 - i] : C[i - K];
+      Cn[i] = (cs & polled) | (C[i] & ~polled);
+    }
+  } else {
+    // exact: per vote, re-select the poll set (a deleted record makes room)
+    St s;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s.V[i] = v0[i];
+      s.V[4 + i] = v1[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s.C[i] = C[i];
+      s.K[i] = Kp[i];
+    }
+    s.A = A;
+    uint32_t alive = P0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t pj = j == 0 ? polled : cap_select(alive, lane, wave, wsum, (uint32_t)j & 1u);
+      applied += (uint32_t)__popc(pj);
+      uint32_t fin;
+      vote_step<true>(s, ys[7 + j], cwv[j], pj, E[j], fin);
+      alive &= ~fin;
+    }
+    died = P0 & ~alive;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o0[i] = s.V[i] & ~died;
+      o1[i] = s.V[4 + i] & ~died;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      Cn[i] = s.C[i] | died;
+      Kp[i] = s.K[i];
+    }
+    A = s.A;
+  }
+
+  if (active) {
+    pst4<NT>(grp, o0);
+    pst4<NT>(grp + 64, o1);
+    u32x4 o2, o3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o2[i] = Kp[i];
+      o3[i] = Kp[4 + i];
+    }
+    pst4<NT>(grp + 128, o2);
+    pst4<NT>(grp + 192, o3);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pst<NT>(tp + 1024u + (uint32_t)i * 64u + tl, Cn[i]);
+    pst<NT>(tp + 1536u + tl, A);
+    p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
+  }
+  const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
+  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, died);
+  count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted, died);
+}
+
+template <int K, int MAXT>
+hipError_t launch_node_t(const RoundParams& p, bool replay, uint32_t bt, hipStream_t s) {
+  if (replay) {
+    if (p.plane_nt)
+      hipLaunchKernelGGL((k_round_node<K, true, true, MAXT>), dim3(p.NL), dim3(bt), 0, s, p);
+    else
+      hipLaunchKernelGGL((k_round_node<K, true, false, MAXT>), dim3(p.NL), dim3(bt), 0, s, p);
+  } else {
+    if (p.plane_nt)
+      hipLaunchKernelGGL((k_round_node<K, false, true, MAXT>), dim3(p.NL), dim3(bt), 0, s, p);
+    else
+      hipLaunchKernelGGL((k_round_node<K, false, false, MAXT>), dim3(p.NL), dim3(bt), 0, s, p);
+  }
+  return hipGetLastError();
+}
+
+// workgroup = the node's blocks rounded up to whole waves; a 512-thread bound
+// (M <= 16384) leaves the register allocator room (no scratch)
+template <int K>
+hipError_t launch_node_k(const RoundParams& p, bool replay, hipStream_t s) {
+  const uint32_t bt = ((p.BL + 63u) / 64u) * 64u;
+  return bt <= 512u ? launch_node_t<K, 512>(p, replay, bt, s) : launch_node_t<K, 1024>(p, replay, bt, s);
+}
+
+}  // namespace
+
+hipError_t launch_round_node(const RoundParams& p, int k, bool replay, hipStream_t s) {
+  switch (k) {
+    case 1: return launch_node_k<1>(p, replay, s);
+    case 2: return launch_node_k<2>(p, replay, s);
+    case 3: return launch_node_k<3>(p, replay, s);
+    case 4: return launch_node_k<4>(p, replay, s);
+    case 5: return launch_node_k<5>(p, replay, s);
+    case 6: return launch_node_k<6>(p, replay, s);
+    case 7: return launch_node_k<7>(p, replay, s);
+    case 8: return launch_node_k<8>(p, replay, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace avk

@@ -8,80 +8,34 @@
 // (:114-116).
 //
 // Same HBM layout, outputs and counters as k_round_fast (kernels.hip); what
-// differs is how the work maps onto CDNA4:
-//  * a fixed grid of resident waves sweeps the 64-lane tiles, so the per-wave
-//    counters are reduced and flushed once per wave, not once per tile;
+// differs is how the work maps onto CDNA4 (DESIGN.md §3):
 //  * the Philox peer draw runs once per (node, Philox block) across the
 //    wave's lanes and is handed to the node's lanes with ds_bpermute, instead
-//    of every lane of a node redrawing the same peers;
-//  * the ">6 of 8" thresholds of vote.go:58,61 are evaluated for all k slots
-//    at once as sliding windows over [old planes | new votes] (prefix
-//    aggregates on both sides of the boundary, 2 VALU ops per window);
-//  * when no record of the wave can reach count 128 this round (count < 120,
-//    k <= 8), the confidence update is a bit-sliced popcount of the agreeing
-//    votes after the last flip added once, not a 7-plane ripple per vote;
-//    otherwise the exact per-vote ripple with deletion runs;
+//    of every lane of a node redrawing the same peers (round_slots.h);
+//  * per slot, the ">6 of 8" thresholds of vote.go:58,61 are one 14-op
+//    at-most-one-zero network over the 8-vote window of [old planes | new
+//    votes]; on warm planes with sim votes the no side runs on the complement
+//    of the same registers;
+//  * the confidence update is deferred: a 4-plane counter of agreements since
+//    the last flip, added once at the end (count = flipped ? c : count + c);
+//    a wave holding a record with count >= 120 also detects, per slot, the
+//    vote that takes a record from 127 to 128 (finalization and deletion);
 //  * once every consider plane is known to be all-ones (sim votes only, the
 //    engine tracks it), the consider planes are neither read nor written and
-//    the per-tile check load disappears.
+//    the per-tile warmth probe disappears;
+//  * 72 VGPRs at k = 8 (7 waves per SIMD); one wave per tile, or a resident
+//    grid walking the tiles when tiles are few (the per-wave counters are
+//    then flushed once per wave).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 
 #include "kernels.h"
 #include "round_common.h"
+#include "round_slots.h"
 
 namespace avk {
 namespace {
-
-__device__ __forceinline__ uint32_t div_bl(const RoundParams& p, uint32_t n) {
-  const uint32_t t = __umulhi(n, p.bl_magic);
-  return (t + ((n - t) >> p.bl_sh1)) >> p.bl_sh2;
-}
-
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-
-// Thresholds of vote.go:58,61 at slot j. The 8-vote window after slot j is
-// seq[j .. j+7] of the sequence seq = [V_6 .. V_0, w_0 .. w_{K-1}] (old
-// shift-register planes, oldest first, then this round's votes). y = votes &
-// consider, n = ^votes & consider (vote.go:58, :61); "popcount > 6" of 8
-// planes = at most one zero = a 14-op bit-sliced network (u | t folds into
-// one v_bitop3 per plane).
-template <int J, int K, bool NEG = false>
-__device__ __forceinline__ uint32_t atleast7_window(const uint32_t (&seq)[7 + K]) {
-  uint32_t t = NEG ? ~seq[J] : seq[J], u = ~0u;
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    const uint32_t x = NEG ? ~seq[J + i] : seq[J + i];
-    u = (u & x) | t;
-    t &= x;
-  }
-  return u;
-}
-
-// yes / no thresholds of slot J; SYM: n == ~y on the whole window (sim votes
-// on warm planes), so the no side runs on the complement of ys in place
-template <int J, int K, bool SYM>
-__device__ __forceinline__ void thresholds(const uint32_t (&ys)[7 + K], const uint32_t (&ns)[7 + K], uint32_t& yes,
-                                           uint32_t& no) {
-  yes = atleast7_window<J, K>(ys);
-  no = SYM ? atleast7_window<J, K, true>(ys) : atleast7_window<J, K>(ns);
-}
-
-// The rarely taken peer draws (round-robin mode, N - 1 <= k, one block per
-// node, or a repeated candidate) out of line, so their registers do not
-// weigh on the hot path.
-template <int K>
-struct PeerList {
-  uint32_t v[K];
-};
-template <int K>
-__device__ __forceinline__ PeerList<K> sample_peers_general(uint64_t seed, uint32_t node, uint32_t round,
-                                                         uint32_t n_nodes, int mode) {
-  PeerList<K> r;
-  sample_peers<K>(seed, node, round, n_nodes, mode, r.v);
-  return r;
-}
 
 struct SweepAcc {
   uint32_t applied = 0, died = 0, lane_bytes = 0;
@@ -89,84 +43,6 @@ struct SweepAcc {
 };
 
 enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3 };
-
-// Per-slot step of the round. The count update is deferred: c (4 planes)
-// counts the agreeing conclusive votes since the last flip (vote.go:66-69),
-// F marks records that flipped (vote.go:72-74; count reset to 0), and at the
-// end count_new = F ? c : count + c. det (some polled record of the wave has
-// count >= 120, wave-uniform): also detect the vote that takes a record from 127 to 128 —
-// an agreement with no flip before it in the round and low3 + c == 8, where
-// low3 = count & 7 (count >= 120 means bits 3..6 are set) — which finalizes
-// and deletes it (vote.go:68, processor.go:114-116); later slots skip it.
-template <int K, bool SYM, int J = 0>
-__device__ __forceinline__ void round_slots(const uint32_t (&ys)[7 + K], const uint32_t (&ns)[7 + K],
-                                            const uint32_t (&low3)[3], uint32_t nearfin, bool det, uint32_t& alive,
-                                            uint32_t& A, uint32_t (&E)[K], uint32_t (&c)[4], uint32_t& F,
-                                            uint32_t& applied) {
-  if constexpr (J < K) {
-    uint32_t yes, no;
-    thresholds<J, K, SYM>(ys, ns, yes, no);
-    applied += (uint32_t)__popc(alive);
-    const uint32_t concl = (yes | no) & alive;  // conclusive (vote.go:61-63)
-    const uint32_t flip = concl & (A ^ yes);    // disagrees: reset to yes?1:0 (vote.go:72-74)
-    const uint32_t agree = concl ^ flip;        // agrees: confidence += 2 (vote.go:66-69)
-    uint32_t carry = agree;
-    A ^= flip;
-    constexpr int planes = J < 1 ? 1 : J < 3 ? 2 : J < 7 ? 3 : 4;  // c <= J + 1
-#pragma unroll
-    for (int i = 0; i < planes; ++i) {
-      const uint32_t ci = J == 0 ? 0u : c[i] & ~flip;
-      c[i] = ci ^ carry;
-      carry &= ci;
-    }
-    uint32_t e = flip;
-    if (det) {  // wave-uniform
-      // low3 + c == 8 (c <= 8, low3 <= 7): sum bits 0..2 clear, bit 3 set
-      const uint32_t c3 = planes > 3 ? c[3] : 0u;
-      const uint32_t c2 = planes > 2 ? c[2] : 0u;
-      const uint32_t s0 = low3[0] ^ c[0], k0 = low3[0] & c[0];
-      const uint32_t t1 = low3[1] ^ c[1], s1 = t1 ^ k0, k1 = bfi(t1, k0, low3[1]);
-      const uint32_t t2 = low3[2] ^ c2, s2 = t2 ^ k1, k2 = bfi(t2, k1, low3[2]);
-      const uint32_t s3 = c3 ^ k2;
-      const uint32_t fin = agree & ~F & nearfin & ~(s0 | s1 | s2) & s3;
-      e |= fin;
-      alive &= ~fin;
-    }
-    F |= flip;
-    E[J] = e;
-    round_slots<K, SYM, J + 1>(ys, ns, low3, nearfin, det, alive, A, E, c, F, applied);
-  }
-}
-
-// Plane-stream cache policy POL: 0 = default loads/stores, 1 = non-temporal
-// loads and stores, 2 = non-temporal loads + sc1 stores (write-through, the
-// line leaves the XCD's L2), 3 = non-temporal loads + nt sc1 stores. 2/3 keep
-// the streamed state out of L2 so that more of the gathered preference table
-// stays there (MI355X_MICROARCH.md: plain/nt stores keep the line in L2, sc1
-// stores drop it).
-constexpr int32_t kRsrcWord3 = 0x00020000;  // raw 32-bit buffer (gfx9 family)
-template <int POL>
-__device__ __forceinline__ u32x4 ld4(const u32x4* q) {
-  return pld4<(POL > 0)>(q);
-}
-template <int POL>
-__device__ __forceinline__ uint32_t ld1(const uint32_t* q) {
-  return pld<(POL > 0)>(q);
-}
-template <int POL>
-__device__ __forceinline__ void st4(__amdgpu_buffer_rsrc_t r, u32x4* q, uint32_t off, u32x4 v) {
-  if constexpr (POL < 2)
-    pst4<(POL > 0)>(q, v);
-  else
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, POL == 2 ? 16 : 18);
-}
-template <int POL>
-__device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, uint32_t* q, uint32_t off, uint32_t v) {
-  if constexpr (POL < 2)
-    pst<(POL > 0)>(q, v);
-  else
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, POL == 2 ? 16 : 18);
-}
 
 // One 64-lane tile of the round. WARM: consider planes all-ones (neither
 // loaded nor stored; sim votes only). POL: plane-stream cache policy.
@@ -205,39 +81,7 @@ __device__ __forceinline__ void sweep_tile(const RoundParams& p, uint32_t tile, 
     }
   } else {
     uint32_t peers[K];
-    const uint32_t others = p.n_nodes - 1u;
-    constexpr uint32_t NB = (K + 3) / 4;
-    const uint32_t nlA = uni(nl);                                                      // lane 0 is always active
-    const uint32_t nn = (uint32_t)__builtin_amdgcn_readlane((int)nl, 63) - nlA + 1u;  // nodes in this tile
-    bool general = p.peer_mode == 1 || (uint32_t)K >= others || nn * NB > 64u;
-    if (!general) {
-      // producer lane q draws Philox block q % NB of the tile's node q / NB ...
-      const uint32_t q = lane;
-      const uint32_t pnode = p.n0 + nlA + min(q / NB, nn - 1u);
-      uint32_t x[4];
-      philox(x, p.seed, pnode, p.round, q % NB, kDomPeers);
-      uint32_t prod[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t u = __umulhi(x[i], others);
-        prod[i] = u + (u >= pnode ? 1u : 0u);
-      }
-      // ... and every lane of that node takes its candidates with ds_bpermute
-      const uint32_t base = (nl - nlA) * NB;
-      bool distinct = true;
-#pragma unroll
-      for (int c = 0; c < K; ++c) {
-        peers[c] = (uint32_t)__shfl((int)prod[c & 3], (int)(base + (uint32_t)c / 4u), 64);
-#pragma unroll
-        for (int d = 0; d < c; ++d) distinct &= peers[c] != peers[d];
-      }
-      general = !distinct;
-    }
-    if (general) {
-      const PeerList<K> r = sample_peers_general<K>(p.seed, node, p.round, p.n_nodes, p.peer_mode);
-#pragma unroll
-      for (int j = 0; j < K; ++j) peers[j] = r.v[j];
-    }
+    draw_peers<K>(p, node, nl, uni(nl), (uint32_t)__builtin_amdgcn_readlane((int)nl, 63) - uni(nl) + 1u, lane, peers);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       // ABLATE (timing diagnostics only, results invalid): the node's own row, coalesced

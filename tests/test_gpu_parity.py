@@ -123,9 +123,10 @@ def test_tiny_network_peers_parity(oracle, kernel):
     assert_same_state(eng, sim)
 
 
-def test_sim_capped_parity(oracle):
+@pytest.mark.parametrize("kernel", [2, 1], ids=["node", "capped_v1"])
+def test_sim_capped_parity(oracle, kernel):
     """M > 4096: the workgroup-scan path enforces the 4096 poll cap."""
-    eng, sim = make_pair(oracle, 20, 5000, 8, seed=3, byz=BYZ20, init_mode=3)
+    eng, sim = make_pair(oracle, 20, 5000, 8, seed=3, byz=BYZ20, init_mode=3, kernel=kernel)
     for r in range(6):
         eng.run_rounds(1)
         exp_u, applied = sim.run_round()
@@ -136,7 +137,7 @@ def test_sim_capped_parity(oracle):
 
 # ------------------------------------------------------------------ rounds, replay mode
 @pytest.mark.parametrize("n,m,k,kernel", [(9, 300, 8, 2), (9, 300, 8, 1), (70, 1000, 5, 2), (6, 4500, 8, 2),
-                                          (5, 4097, 2, 2), (4, 8300, 8, 2)])
+                                          (6, 4500, 8, 1), (5, 4097, 2, 2), (4, 8300, 8, 2), (3, 20000, 8, 2)])
 def test_replay_parity(oracle, n, m, k, kernel):
     eng, sim = make_pair(oracle, n, m, k, seed=21, init_mode=3, kernel=kernel)
     applied_total = 0
@@ -364,3 +365,19 @@ def test_update_log_overflow_reported(oracle):
         eng.fetch_updates()
     assert not eng.log_overflowed()
     assert_same_state(eng, sim, "after overflow")
+
+
+@pytest.mark.parametrize("kernel", [2, 1], ids=["node", "capped_v1"])
+def test_capped_finalization_parity(oracle, kernel):
+    """M > 4096 with more live records than the cap, run through finalization:
+    records deleted at count 128 make room for the next ones inside a round
+    (the per-vote poll-set re-selection path)."""
+    n, m, k = 12, 4500, 8
+    eng, sim = make_pair(oracle, n, m, k, seed=13, init_mode=2, kernel=kernel)
+    for r in range(22):
+        eng.run_rounds(1)
+        exp_u, applied = sim.run_round()
+        assert rows(eng.fetch_updates()) == rows(exp_u), r
+        if r >= 15:
+            assert_same_state(eng, sim, f"round {r}")
+    assert eng.finalized_count() > 0

@@ -45,6 +45,7 @@ for s in "$@"; do
     conv_c5) step conv_c5 900 python tools/run_to_finalization.py --workload c5 --max-rounds 64 --json $OUT/conv_c5.json ;;
     conv_c4) step conv_c4 900 python tools/run_to_finalization.py --workload c4 --max-rounds 64 --json $OUT/conv_c4.json ;;
     bench_c2) step bench_c2 900 python bench.py --workload c2 --no-cpu-baseline ;;
+    bench_c2v1) step bench_c2v1 900 python bench.py --workload c2 --no-cpu-baseline --kernel 1 ;;
     bench_c3) step bench_c3 900 python bench.py --workload c3 --no-cpu-baseline ;;
     bench_c5) step bench_c5 900 python bench.py --workload c5 --no-cpu-baseline ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- \
