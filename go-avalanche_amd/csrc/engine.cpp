@@ -619,6 +619,38 @@ int av_get_invs(av_engine* e, int64_t node, int64_t* out_targets, int64_t cap, i
   return AV_OK;
 }
 
+int av_get_invs_batch(av_engine* e, int64_t n0, int64_t n1, int64_t* offsets, int32_t* targets, int64_t cap,
+                      int64_t* total) {
+  AV_ENTER(e);
+  AV_CHECK(offsets && total && (cap == 0 || targets), AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(n0 >= e->n0 && n0 <= n1 && n1 <= e->n1, AV_ERR_INVALID_ARG, "node range outside this engine's shard");
+  const uint32_t n = (uint32_t)(n1 - n0);
+  *total = 0;
+  offsets[0] = 0;
+  if (!n) return AV_OK;
+  Scratch sc;
+  AV_HIP(sc.ensure((size_t)n * 4));
+  auto* dcounts = static_cast<uint32_t*>(sc.p);
+  AV_HIP(avk::launch_poll_sets(e->planes, e->valid, e->BL, (uint32_t)(n0 - e->n0), n, (uint32_t)e->t0, dcounts,
+                               nullptr, nullptr, e->stream));
+  std::vector<uint32_t> counts(n);
+  AV_HIP(hipMemcpyAsync(counts.data(), dcounts, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  for (uint32_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + counts[i];
+  *total = offsets[n];
+  AV_CHECK(*total <= cap, AV_ERR_OVERFLOW, "cap too small (%lld needed)", (long long)*total);
+  if (!*total) return AV_OK;
+  Scratch so, st;
+  AV_HIP(so.ensure((size_t)(n + 1) * 8));
+  AV_HIP(st.ensure((size_t)*total * 4));
+  AV_HIP(hipMemcpyAsync(so.p, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(avk::launch_poll_sets(e->planes, e->valid, e->BL, (uint32_t)(n0 - e->n0), n, (uint32_t)e->t0, nullptr,
+                               static_cast<const int64_t*>(so.p), static_cast<int32_t*>(st.p), e->stream));
+  AV_HIP(hipMemcpyAsync(targets, st.p, (size_t)*total * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+
 int av_run_rounds(av_engine* e, int32_t rounds) {
   AV_ENTER(e);
   AV_CHECK(rounds >= 0, AV_ERR_INVALID_ARG, "rounds < 0");

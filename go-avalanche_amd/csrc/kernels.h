@@ -144,6 +144,9 @@ hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t B
                              hipStream_t s);
 hipError_t launch_count_live(const uint32_t* planes, const uint32_t* valid, const uint32_t* byz, uint32_t n0,
                              uint32_t BL, uint32_t L, int honest_only, unsigned long long* out, hipStream_t s);
+// Batched poll sets: counts (out == nullptr path) or CSR targets at offsets.
+hipError_t launch_poll_sets(const uint32_t* planes, const uint32_t* valid, uint32_t BL, uint32_t nl0, uint32_t n,
+                            uint32_t t0, uint32_t* counts, const int64_t* offsets, int32_t* out, hipStream_t s);
 hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets,
                               uint32_t log_cap, uint32_t shards, uint64_t* out, hipStream_t s);
 

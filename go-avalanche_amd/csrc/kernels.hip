@@ -507,6 +507,35 @@ __global__ void k_compact_log(const uint64_t* log, const uint32_t* counts, const
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
+// Batched GetInvsForNextPoll (processor.go:144-170) for local nodes
+// [nl0, nl0 + gridDim.x): one 64-lane workgroup per node walks the node's
+// blocks in order with a running wave prefix count of live, valid records
+// (rule R1: ascending target order, at most kMaxPoll). counts == nullptr:
+// write the poll set at out + offsets[node]; else only count it.
+__global__ __launch_bounds__(64) void k_poll_sets(const uint32_t* planes, const uint32_t* valid, uint32_t BL,
+                                                  uint32_t nl0, uint32_t t0, uint32_t* counts,
+                                                  const int64_t* offsets, int32_t* out) {
+  const uint32_t i = blockIdx.x, nl = nl0 + i, lane = threadIdx.x;
+  uint32_t run = 0;  // records selected so far (wave-uniform)
+  for (uint32_t b0 = 0; b0 < BL && run < kMaxPoll; b0 += 64u) {
+    const uint32_t b = b0 + lane;
+    const uint32_t bits = b < BL ? ~*pw(planes, nl * BL + b, kPK + 7) & valid[b] : 0u;
+    const uint32_t c = (uint32_t)__popc(bits);
+    const uint32_t incl = wave_incl_scan(c, lane);
+    if (!counts && c) {
+      uint32_t pos = run + incl - c, x = bits;
+      int32_t* dst = out + offsets[i];
+      while (x && pos < kMaxPoll) {
+        const uint32_t bit = (uint32_t)__ffs(x) - 1u;
+        x &= x - 1u;
+        dst[pos++] = (int32_t)(t0 + 32u * b + bit);
+      }
+    }
+    run += (uint32_t)__shfl((int)incl, 63, 64);
+  }
+  if (counts && lane == 0) counts[i] = min(run, kMaxPoll);
+}
+
 template <int K>
 hipError_t launch_round_k(const RoundParams& p, bool replay, bool capped, hipStream_t s) {
   if (capped) {
@@ -636,6 +665,13 @@ hipError_t launch_count_live(const uint32_t* planes, const uint32_t* valid, cons
   if (!L) return hipSuccess;
   const uint32_t blocks = std::min<uint32_t>(2048u, (L + 255u) / 256u);
   hipLaunchKernelGGL(k_count_live, dim3(blocks), dim3(256), 0, s, planes, valid, byz, n0, BL, L, honest_only, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_poll_sets(const uint32_t* planes, const uint32_t* valid, uint32_t BL, uint32_t nl0, uint32_t n,
+                            uint32_t t0, uint32_t* counts, const int64_t* offsets, int32_t* out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_poll_sets, dim3(n), dim3(64), 0, s, planes, valid, BL, nl0, t0, counts, offsets, out);
   return hipGetLastError();
 }
 

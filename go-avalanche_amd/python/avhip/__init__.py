@@ -68,7 +68,7 @@ class Config(C.Structure):
 EXPORTED = [
     "av_abi_version", "av_config_init", "av_create", "av_destroy", "av_strerror", "av_last_error",
     "av_init_records", "av_add_targets", "av_set_valid", "av_register_votes", "av_is_accepted",
-    "av_get_confidence", "av_get_invs", "av_run_rounds", "av_replay_round_errs", "av_replay_prepare",
+    "av_get_confidence", "av_get_invs", "av_get_invs_batch", "av_run_rounds", "av_replay_round_errs", "av_replay_prepare",
     "av_replay_rounds", "av_synchronize", "av_round_index", "av_updates_count", "av_fetch_updates",
     "av_update_log_overflowed", "av_applied_votes", "av_alg_bytes", "av_finalized_count", "av_live_records", "av_discard_updates", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
@@ -101,6 +101,7 @@ def lib():
         "av_is_accepted": (i32, [_vp, i64, i64, P(i32)]),
         "av_get_confidence": (i32, [_vp, i64, i64, P(C.c_uint16)]),
         "av_get_invs": (i32, [_vp, i64, _vp, i64, P(i64)]),
+        "av_get_invs_batch": (i32, [_vp, i64, i64, _vp, _vp, i64, P(i64)]),
         "av_run_rounds": (i32, [_vp, i32]),
         "av_replay_round_errs": (i32, [_vp, _vp]),
         "av_replay_prepare": (i32, [_vp, i32]),
@@ -243,6 +244,19 @@ class Engine:
         n = C.c_int64(0)
         _check(lib().av_get_invs(self._h, node, _ptr(buf), buf.size, C.byref(n)))
         return buf[: n.value].copy()
+
+    def get_invs_batch(self, n0=None, n1=None):
+        """Poll sets of nodes [n0, n1) as CSR (offsets int64[n+1], targets int32[total])."""
+        n0 = self.node_range[0] if n0 is None else n0
+        n1 = self.node_range[1] if n1 is None else n1
+        offs = np.zeros(n1 - n0 + 1, np.int64)
+        total = C.c_int64(0)
+        rc = lib().av_get_invs_batch(self._h, n0, n1, _ptr(offs), None, 0, C.byref(total))
+        if rc not in (AV_OK, AV_ERR_OVERFLOW):
+            _check(rc)
+        tg = np.zeros(max(total.value, 1), np.int32)
+        _check(lib().av_get_invs_batch(self._h, n0, n1, _ptr(offs), _ptr(tg), tg.size, C.byref(total)))
+        return offs, tg[: total.value]
 
     # ---- rounds ----
     def run_rounds(self, rounds=1):

@@ -15,6 +15,7 @@
  *   av_is_accepted      <- (*Processor).IsAccepted              processor.go:125-130
  *   av_get_confidence   <- (*Processor).GetConfidence           processor.go:133-140
  *   av_get_invs         <- (*Processor).GetInvsForNextPoll      processor.go:144-170
+ *   av_get_invs_batch   <- GetInvsForNextPoll of many Processors processor.go:144-170
  *   av_round_index      <- (*Processor).GetRound                processor.go:40-42
  *   av_set_valid        <- Target.IsValid / isWorthyPolling     avalanche.go:89-90, processor.go:185-187
  *   av_run_rounds       <- the example's poll loop for every node at once
@@ -130,6 +131,12 @@ int av_is_accepted(av_engine* e, int64_t node, int64_t target, int32_t* out);
 int av_get_confidence(av_engine* e, int64_t node, int64_t target, uint16_t* out);
 /* Live valid targets in ascending index, truncated to 4096. */
 int av_get_invs(av_engine* e, int64_t node, int64_t* out_targets, int64_t cap, int64_t* n_out);
+/* GetInvsForNextPoll for every local node in [n0, n1) at once (device
+ * compaction): node n's poll set is targets[offsets[n-n0] .. offsets[n-n0+1])
+ * (offsets: n1-n0+1 entries). AV_ERR_OVERFLOW with *total = the required size
+ * if cap is too small. */
+int av_get_invs_batch(av_engine* e, int64_t n0, int64_t n1, int64_t* offsets, int32_t* targets, int64_t cap,
+                      int64_t* total);
 
 /* ---- batched rounds: the hot path ---- */
 /* Enqueue `rounds` synchronous rounds: each node polls

@@ -381,3 +381,38 @@ def test_capped_finalization_parity(oracle, kernel):
         if r >= 15:
             assert_same_state(eng, sim, f"round {r}")
     assert eng.finalized_count() > 0
+
+
+def _oracle_poll_sets(sim, valid, t0=0):
+    dump = sim.dump()
+    live = (dump >> 17) < 128
+    sets = []
+    for row in live & valid[None, :]:
+        sets.append((np.flatnonzero(row)[:avhip.MAX_ELEMENT_POLL] + t0).tolist())
+    return sets
+
+
+@pytest.mark.parametrize("n,m", [(40, 700), (9, 5000)])
+def test_poll_sets_batch_parity(oracle, n, m):
+    """av_get_invs_batch (GetInvsForNextPoll of every node, processor.go:144-170,
+    device compaction) == the oracle's live valid records in target order, capped
+    at 4096, == per-node av_get_invs; through finalization and invalid targets."""
+    eng, sim = make_pair(oracle, n, m, 8, seed=23, byz=BYZ20, init_mode=2)
+    valid = np.ones(m, bool)
+    for r in range(19):
+        if r == 3:
+            for t in (0, 5, m - 1):
+                eng.set_valid(t, False)
+                sim.set_valid(t, False)
+                valid[t] = False
+        eng.run_rounds(1)
+        sim.run_round()
+        if r in (0, 15, 16, 18):
+            offs, tg = eng.get_invs_batch()
+            got = [tg[offs[i]:offs[i + 1]].tolist() for i in range(n)]
+            assert got == _oracle_poll_sets(sim, valid), r
+            for node in (0, n // 2, n - 1):
+                assert eng.get_invs(node).tolist() == got[node]
+            offs2, tg2 = eng.get_invs_batch(2, 5)
+            assert [tg2[offs2[i]:offs2[i + 1]].tolist() for i in range(3)] == got[2:5]
+    eng.fetch_updates()
