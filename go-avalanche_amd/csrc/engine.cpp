@@ -223,13 +223,15 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
 // one wave per tile is fastest for large tile counts (C4 on 1-4 GPUs: the
 // dispatcher keeps the active tiles in a narrow, DRAM-friendly window); a
 // resident grid that walks the tiles wins slightly once there are only a few
-// tiles per resident wave (C4 8-way target shard: 62.5k tiles, ~9 per wave).
-uint32_t default_sweep_blocks(const av_engine* e) {
+// tiles per resident wave (C4 8-way target shard: 62.5k tiles, ~12 per wave),
+// where the warm sweep also pipelines each wave's next tile. force: always the
+// resident grid (A/B).
+uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
   if (e->k > 8 || e->capped) return 0;
   int bpc = 0, cus = 0;
   if (avk::round_sweep_occupancy(e->k, false, &bpc, &cus) != hipSuccess || bpc <= 0 || cus <= 0) return 0;
   const uint64_t resident_waves = (uint64_t)bpc * cus * 4;
-  return (uint64_t)(e->Lpad / 64) <= 12 * resident_waves ? (uint32_t)(bpc * cus) : 0u;
+  return force || (uint64_t)(e->Lpad / 64) <= 16 * resident_waves ? (uint32_t)(bpc * cus) : 0u;
 }
 
 int refresh_pref(av_engine* e) {
@@ -916,11 +918,11 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   } else if (n == "store_policy") {
     AV_CHECK(value >= 0 && value <= 3, AV_ERR_INVALID_ARG, "store_policy must be in [0, 3]");
     e->store_policy = (uint32_t)value;
-  } else if (n == "sweep_blocks") {  // 0 = one wave per tile, -1 = every resident workgroup once (default)
-    AV_CHECK(value >= -1 && value < (1ll << 31), AV_ERR_INVALID_ARG, "bad sweep_blocks");
+  } else if (n == "sweep_blocks") {  // 0 = one wave per tile, -1 = the default choice, -2 = resident grid
+    AV_CHECK(value >= -2 && value < (1ll << 31), AV_ERR_INVALID_ARG, "bad sweep_blocks");
     if (value < 0) {
       AV_ENTER(e);
-      e->sweep_blocks = default_sweep_blocks(e);
+      e->sweep_blocks = default_sweep_blocks(e, value == -2);
     } else {
       e->sweep_blocks = (uint32_t)value;
     }

@@ -23,27 +23,49 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin
 // seq[j .. j+7] of the sequence seq = [V_6 .. V_0, w_0 .. w_{K-1}] (old
 // shift-register planes, oldest first, then this round's votes). y = votes &
 // consider, n = ^votes & consider (vote.go:58, :61); "popcount > 6" of 8
-// planes = at most one zero = a 14-op bit-sliced network (u | t folds into
-// one v_bitop3 per plane).
-template <int J, int K, bool NEG = false>
-__device__ __forceinline__ uint32_t atleast7_window(const uint32_t (&seq)[7 + K]) {
-  uint32_t t = NEG ? ~seq[J] : seq[J], u = ~0u;
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    const uint32_t x = NEG ? ~seq[J + i] : seq[J + i];
-    u = (u & x) | t;
-    t &= x;
-  }
-  return u;
+// planes = "at most one zero". Over a set of planes, Agg2 keeps z0 = "no
+// zero" and z1 = "at most one zero" (2 VALU ops per plane pushed, one
+// v_and_or + one and). Window j = new votes w_0..w_j (a prefix carried from
+// slot to slot, one push per slot) + old planes V_0..V_{6-j} (recomputed per
+// slot: 6-j pushes), combined in 2 ops: 144 VALU ops for all 8 slots of both
+// sides instead of 8 x 2 x 14 for the plain per-window network, and only 4
+// registers of carried state.
+struct Agg2 {
+  uint32_t z0, z1;
+};
+__device__ __forceinline__ void agg_push(Agg2& a, uint32_t x) {
+  a.z1 = a.z0 | (a.z1 & x);
+  a.z0 &= x;
 }
+__device__ __forceinline__ uint32_t agg_le1(const Agg2& p, const Agg2& q) { return (p.z0 & q.z1) | (p.z1 & q.z0); }
 
-// yes / no thresholds of slot J; SYM: n == ~y on the whole window (sim votes
-// on warm planes), so the no side runs on the complement of ys in place
+// yes / no thresholds of slot J; Py / Pn carry the new-vote prefix of the two
+// sides. SYM: n == ~y on the whole window (sim votes on warm planes), so the
+// no side runs on the complement of ys in place (the NOT folds into bitop3).
 template <int J, int K, bool SYM>
-__device__ __forceinline__ void thresholds(const uint32_t (&ys)[7 + K], const uint32_t (&ns)[7 + K], uint32_t& yes,
-                                           uint32_t& no) {
-  yes = atleast7_window<J, K>(ys);
-  no = SYM ? atleast7_window<J, K, true>(ys) : atleast7_window<J, K>(ns);
+__device__ __forceinline__ void thresholds(const uint32_t (&ys)[7 + K], const uint32_t (&ns)[7 + K], Agg2& Py,
+                                           Agg2& Pn, uint32_t& yes, uint32_t& no) {
+  const uint32_t y = ys[7 + J], n = SYM ? ~ys[7 + J] : ns[7 + J];
+  if constexpr (J == 0) {
+    Py = Agg2{y, ~0u};
+    Pn = Agg2{n, ~0u};
+  } else {
+    agg_push(Py, y);
+    agg_push(Pn, n);
+  }
+  if constexpr (J <= 6) {
+    Agg2 Sy{ys[6], ~0u}, Sn{SYM ? ~ys[6] : ns[6], ~0u};  // V_0
+#pragma unroll
+    for (int i = 5; i >= J; --i) {  // V_1 .. V_{6-J}
+      agg_push(Sy, ys[i]);
+      agg_push(Sn, SYM ? ~ys[i] : ns[i]);
+    }
+    yes = agg_le1(Py, Sy);
+    no = agg_le1(Pn, Sn);
+  } else {
+    yes = Py.z1;
+    no = Pn.z1;
+  }
 }
 
 // The rarely taken peer draws (round-robin mode, N - 1 <= k, one block per
@@ -73,10 +95,10 @@ template <int K, bool SYM, int J = 0>
 __device__ __forceinline__ void round_slots(const uint32_t (&ys)[7 + K], const uint32_t (&ns)[7 + K],
                                             const uint32_t (&low3)[3], uint32_t nearfin, bool det, uint32_t& alive,
                                             uint32_t& A, uint32_t (&E)[K], uint32_t (&c)[4], uint32_t& F,
-                                            uint32_t& applied) {
+                                            uint32_t& applied, Agg2 Py = Agg2{}, Agg2 Pn = Agg2{}) {
   if constexpr (J < K) {
     uint32_t yes, no;
-    thresholds<J, K, SYM>(ys, ns, yes, no);
+    thresholds<J, K, SYM>(ys, ns, Py, Pn, yes, no);
     applied += (uint32_t)__popc(alive);
     const uint32_t concl = (yes | no) & alive;  // conclusive (vote.go:61-63)
     const uint32_t flip = concl & (A ^ yes);    // disagrees: reset to yes?1:0 (vote.go:72-74)
@@ -105,7 +127,7 @@ __device__ __forceinline__ void round_slots(const uint32_t (&ys)[7 + K], const u
     }
     F |= flip;
     E[J] = e;
-    round_slots<K, SYM, J + 1>(ys, ns, low3, nearfin, det, alive, A, E, c, F, applied);
+    round_slots<K, SYM, J + 1>(ys, ns, low3, nearfin, det, alive, A, E, c, F, applied, Py, Pn);
   }
 }
 

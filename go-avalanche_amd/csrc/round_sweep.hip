@@ -12,10 +12,11 @@
 //  * the Philox peer draw runs once per (node, Philox block) across the
 //    wave's lanes and is handed to the node's lanes with ds_bpermute, instead
 //    of every lane of a node redrawing the same peers (round_slots.h);
-//  * per slot, the ">6 of 8" thresholds of vote.go:58,61 are one 14-op
-//    at-most-one-zero network over the 8-vote window of [old planes | new
-//    votes]; on warm planes with sim votes the no side runs on the complement
-//    of the same registers;
+//  * per slot, the ">6 of 8" thresholds of vote.go:58,61 are "at most one
+//    zero" over the 8-vote window of [old planes | new votes]: a prefix of the
+//    new votes carried from slot to slot plus the shrinking old part,
+//    combined in 2 ops (round_slots.h); on warm planes with sim votes the no
+//    side runs on the complement of the same registers;
 //  * the confidence update is deferred: a 4-plane counter of agreements since
 //    the last flip, added once at the end (count = flipped ? c : count + c);
 //    a wave holding a record with count >= 120 also detects, per slot, the
@@ -25,7 +26,8 @@
 //    the per-tile warmth probe disappears;
 //  * 72 VGPRs at k = 8 (7 waves per SIMD); one wave per tile, or a resident
 //    grid walking the tiles when tiles are few (the per-wave counters are
-//    then flushed once per wave).
+//    then flushed once per wave, and each wave issues its next tile's loads
+//    before computing the current one).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,55 +44,102 @@ struct SweepAcc {
   uint32_t emitted = 0;  // wave-uniform
 };
 
-enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3 };
+enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3, kModeWarmPipe = 4 };
 
-// One 64-lane tile of the round. WARM: consider planes all-ones (neither
-// loaded nor stored; sim votes only). POL: plane-stream cache policy.
+// Everything one 64-lane tile loads before its round step: the state planes
+// (vote.go:25-29; V0-7 and K0-7 as dwordx4 groups, A, C0-7 unless warm), the
+// validity word, the node's Byzantine word, and the k vote words (replayed
+// planes, or the peers' published preference words). Split from the step so
+// that a wave can issue tile t + stride's loads before it computes tile t.
+template <int K, bool REPLAY, bool WARM>
+struct TileIn {
+  u32x4 v0, v1, k0, k1;
+  uint32_t A, vmask, byzw;
+  uint32_t C[WARM ? 1 : 8];
+  uint32_t w[K];                 // yes bits: err == 0 (vote.go:55)
+  uint32_t cw[REPLAY ? K : 1];   // consider bits: int32(err) >= 0 (vote.go:56); sim votes: all-ones
+};
+
+struct LaneIdx {
+  uint32_t g, gc, nl, b, node;
+  bool active;
+};
+
+__device__ __forceinline__ LaneIdx lane_idx(const RoundParams& p, uint32_t tile, uint32_t lane) {
+  LaneIdx x;
+  x.g = tile * 64u + lane;
+  x.active = x.g < p.L;
+  x.gc = x.active ? x.g : p.L - 1u;  // inactive lanes read a valid lane, never store
+  x.nl = div_bl(p, x.gc);
+  x.b = x.gc - x.nl * p.BL;
+  x.node = p.n0 + x.nl;
+  return x;
+}
+
 template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE>
-__device__ __forceinline__ void sweep_tile(const RoundParams& p, uint32_t tile, uint32_t lane, uint32_t extra_bytes,
-                                           SweepAcc& acc) {
-  const uint32_t g = tile * 64u + lane;
-  const bool active = g < p.L;
-  const uint32_t gc = active ? g : p.L - 1u;  // inactive lanes read a valid lane, never store
-  const uint32_t nl = div_bl(p, gc);
-  const uint32_t b = gc - nl * p.BL;
-  const uint32_t node = p.n0 + nl;
-
-  // ---- state planes (vote.go:25-29): V0-7 and K0-7 as dwordx4 groups, A, C0-7 unless warm
-  uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
-  u32x4* const grp = reinterpret_cast<u32x4*>(tp) + lane;
-  const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(tp, 0, kPlanes * 64 * 4, kRsrcWord3);
-  const u32x4 v0 = ld4<POL>(grp), v1 = ld4<POL>(grp + 64), k0 = ld4<POL>(grp + 128), k1 = ld4<POL>(grp + 192);
-  uint32_t A = ld1<POL>(tp + 1536u + lane);
-  uint32_t C[8];
+__device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
+                                          TileIn<K, REPLAY, WARM>& in) {
+  const LaneIdx x = lane_idx(p, tile, lane);
+  const uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
+  const u32x4* const grp = reinterpret_cast<const u32x4*>(tp) + lane;
+  in.v0 = ld4<POL>(grp);
+  in.v1 = ld4<POL>(grp + 64);
+  in.k0 = ld4<POL>(grp + 128);
+  in.k1 = ld4<POL>(grp + 192);
+  in.A = ld1<POL>(tp + 1536u + lane);
+  if constexpr (!WARM) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) C[i] = WARM ? ~0u : ld1<POL>(tp + 1024u + (uint32_t)i * 64u + lane);
-  const uint32_t vmask = active ? p.valid[b] : 0u;
-
-  // ---- this round's votes: ys/ns hold y/n of [V_6..V_0, w_0..w_{K-1}]
-  constexpr bool SYM = WARM && !REPLAY;  // n == ~y everywhere: ns is never read
-  uint32_t ys[7 + K], ns[7 + K], cwv[K];
+    for (int i = 0; i < 8; ++i) in.C[i] = ld1<POL>(tp + 1024u + (uint32_t)i * 64u + lane);
+  }
+  in.vmask = x.active ? p.valid[x.b] : 0u;
+  in.byzw = p.byz[x.node >> 5];
   if constexpr (REPLAY) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const uint32_t cw = p.replay[(size_t)(2 * j + 1) * p.Lpad + gc];
-      const uint32_t yw = p.replay[(size_t)(2 * j) * p.Lpad + gc] & cw;  // err == 0 implies considered
-      ys[7 + j] = yw;
-      ns[7 + j] = ~yw & cw;
-      cwv[j] = cw;
+      in.cw[j] = p.replay[(size_t)(2 * j + 1) * p.Lpad + x.gc];
+      in.w[j] = p.replay[(size_t)(2 * j) * p.Lpad + x.gc];
     }
   } else {
     uint32_t peers[K];
-    draw_peers<K>(p, node, nl, uni(nl), (uint32_t)__builtin_amdgcn_readlane((int)nl, 63) - uni(nl) + 1u, lane, peers);
+    draw_peers<K>(p, x.node, x.nl, uni(x.nl), (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - uni(x.nl) + 1u,
+                  lane, peers);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       // ABLATE (timing diagnostics only, results invalid): the node's own row, coalesced
-      const uint32_t src = ABLATE ? node : peers[j];
-      const uint32_t w = p.pref_in[src * p.BL + b];  // < N * BL < 2^31 (engine check)
-      ys[7 + j] = w;  // honest or Byzantine answers: never neutral
-      ns[7 + j] = SYM ? 0u : ~w;
-      cwv[j] = ~0u;
+      const uint32_t src = ABLATE ? x.node : peers[j];
+      in.w[j] = p.pref_in[src * p.BL + x.b];  // < N * BL < 2^31 (engine check); never neutral
     }
+  }
+}
+
+// The round step of one loaded tile. WARM: consider planes all-ones (neither
+// loaded nor stored; sim votes only). POL: plane-stream cache policy.
+template <int K, bool REPLAY, bool WARM, int POL>
+__device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
+                                             const TileIn<K, REPLAY, WARM>& in, uint32_t extra_bytes, SweepAcc& acc) {
+  const LaneIdx x = lane_idx(p, tile, lane);
+  const bool active = x.active;
+  const uint32_t b = x.b, node = x.node;
+  uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
+  u32x4* const grp = reinterpret_cast<u32x4*>(tp) + lane;
+  const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(tp, 0, kPlanes * 64 * 4, kRsrcWord3);
+  const u32x4 v0 = in.v0, v1 = in.v1, k0 = in.k0, k1 = in.k1;
+  uint32_t A = in.A;
+  uint32_t C[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) C[i] = WARM ? ~0u : in.C[WARM ? 0 : i];
+  const uint32_t vmask = in.vmask;
+
+  // ---- ys/ns hold y/n of [V_6..V_0, w_0..w_{K-1}]
+  constexpr bool SYM = WARM && !REPLAY;  // n == ~y everywhere: ns is never read
+  uint32_t ys[7 + K], ns[7 + K], cwv[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t cw = REPLAY ? in.cw[REPLAY ? j : 0] : ~0u;
+    const uint32_t yw = in.w[j] & cw;  // err == 0 implies considered
+    ys[7 + j] = yw;
+    ns[7 + j] = SYM ? 0u : ~yw & cw;
+    cwv[j] = cw;
   }
 #pragma unroll
   for (int i = 0; i < 7; ++i) {  // old planes V_6..V_0
@@ -195,48 +244,68 @@ __device__ __forceinline__ void sweep_tile(const RoundParams& p, uint32_t tile, 
   acc.emitted += emitted;
 }
 
-__device__ __forceinline__ unsigned long long wave_sum64(uint32_t v) {
-  unsigned long long x = v;
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) x += (unsigned long long)__shfl_xor((long long)x, d, 64);
-  return x;
-}
-
 // MODE: kModeWarm (sim, every consider plane all-ones), kModeCheck (sim, per
 // tile: the oldest consider plane decides), kModeReplay (replayed votes),
 // kModeAblate (kModeCheck with the peer gather replaced by a coalesced read of
-// the node's own row: timing diagnostics only, results invalid).
+// the node's own row: timing diagnostics only, results invalid), kModeWarmPipe
+// (kModeWarm for a resident grid: the next tile's loads are issued before the
+// current tile is computed; 93 VGPRs, 5 waves per SIMD).
 template <int K, int MODE, int POL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeReplay ? 6 : 7))) void k_round_sweep(const RoundParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeReplay ? 6 : 7))) void k_round_sweep(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave0 = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * 4u;
   const uint32_t tiles = p.Lpad >> 6;
   SweepAcc acc;
-  for (uint32_t tile = wave0; tile < tiles; tile += nwaves) {
-    constexpr bool AB = MODE == kModeAblate;
-    if constexpr (MODE == kModeReplay) {
-      sweep_tile<K, true, false, POL, false>(p, tile, lane, 0u, acc);
-    } else if constexpr (MODE == kModeWarm) {
-      sweep_tile<K, false, true, POL, false>(p, tile, lane, 0u, acc);
-    } else {
-      bool warm = false;
-      if (p.warm_skip) {
-        // all-ones oldest consider plane <=> all consider planes all-ones (monotone sim votes)
-        const uint32_t g = tile * 64u + lane;
-        const uint32_t c7 = g < p.L ? p.planes[(size_t)tile * (kPlanes * 64u) + 1024u + 7u * 64u + lane] : ~0u;
-        warm = __all(c7 == ~0u);
+  if constexpr (MODE == kModeWarmPipe) {
+    // software-pipelined: tile t + nwaves's loads (state, peer draw, gathers)
+    // are in flight while tile t is computed
+    TileIn<K, false, true> cur, nxt;
+    uint32_t tile = wave0;
+    if (tile < tiles) load_tile<K, false, true, POL, false>(p, tile, lane, cur);
+    for (; tile < tiles; tile += nwaves) {
+      const uint32_t next = tile + nwaves;
+      if (next < tiles) load_tile<K, false, true, POL, false>(p, next, lane, nxt);
+      process_tile<K, false, true, POL>(p, tile, lane, cur, 0u, acc);
+      cur = nxt;
+    }
+  } else {
+    for (uint32_t tile = wave0; tile < tiles; tile += nwaves) {
+      constexpr bool AB = MODE == kModeAblate;
+      if constexpr (MODE == kModeWarm) {
+        TileIn<K, false, true> in;
+        load_tile<K, false, true, POL, false>(p, tile, lane, in);
+        process_tile<K, false, true, POL>(p, tile, lane, in, 0u, acc);
+      } else if constexpr (MODE == kModeReplay) {
+        TileIn<K, true, false> in;
+        load_tile<K, true, false, POL, false>(p, tile, lane, in);
+        process_tile<K, true, false, POL>(p, tile, lane, in, 0u, acc);
+      } else {
+        bool warm = false;
+        if (p.warm_skip) {
+          // all-ones oldest consider plane <=> all consider planes all-ones (monotone sim votes)
+          const uint32_t g = tile * 64u + lane;
+          const uint32_t c7 = g < p.L ? p.planes[(size_t)tile * (kPlanes * 64u) + 1024u + 7u * 64u + lane] : ~0u;
+          warm = __all(c7 == ~0u);
+        }
+        if (warm) {
+          TileIn<K, false, true> in;
+          load_tile<K, false, true, POL, AB>(p, tile, lane, in);
+          process_tile<K, false, true, POL>(p, tile, lane, in, 4u, acc);
+        } else {
+          TileIn<K, false, false> in;
+          load_tile<K, false, false, POL, AB>(p, tile, lane, in);
+          process_tile<K, false, false, POL>(p, tile, lane, in, 0u, acc);
+        }
       }
-      if (warm)
-        sweep_tile<K, false, true, POL, AB>(p, tile, lane, 4u, acc);
-      else
-        sweep_tile<K, false, false, POL, AB>(p, tile, lane, 0u, acc);
     }
   }
-  // one flush per wave (shard = wave index)
-  const unsigned long long s = wave_sum64(acc.applied);
-  const unsigned long long f = wave_sum64(acc.died);
-  const unsigned long long by = wave_sum64(acc.lane_bytes) + 8ull * acc.emitted;
+  // one flush per wave (shard = wave index); 32-bit sums: a wave's lanes
+  // accumulate < 2^32 over the tiles a grid gives it (the engine's grids
+  // walk <= 16 tiles per wave by default, 2^32 / (64 * 32 * 8) = 262k at most)
+  const unsigned long long s = wave_sum(acc.applied);
+  const unsigned long long f = __ballot(acc.died != 0u) ? wave_sum(acc.died) : 0ull;
+  const unsigned long long by = (unsigned long long)wave_sum(acc.lane_bytes) + 8ull * acc.emitted;
   if (lane == 0) {
     const uint32_t shard = wave0 % p.log_shards;
     if (s) atomicAdd(&p.applied[shard], s);
@@ -269,14 +338,15 @@ hipError_t launch_sweep_k(const RoundParams& p, bool replay, uint32_t blocks, hi
   const uint32_t grid = std::max(1u, blocks ? std::min(blocks, need) : need);
   if (replay) return launch_mode<K, kModeReplay>(p, grid, s);
   if (p.ablate_gather) return launch_mode<K, kModeAblate>(p, grid, s);
-  if (p.warm_skip && p.warm_all) return launch_mode<K, kModeWarm>(p, grid, s);
+  if (p.warm_skip && p.warm_all)  // a resident grid walks several tiles per wave: pipeline them
+    return blocks && grid < need ? launch_mode<K, kModeWarmPipe>(p, grid, s) : launch_mode<K, kModeWarm>(p, grid, s);
   return launch_mode<K, kModeCheck>(p, grid, s);
 }
 
 template <int K>
 hipError_t occupancy_k(bool replay, int* bpc) {
   return replay ? hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, k_round_sweep<K, kModeReplay, 1>, 256, 0)
-                : hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, k_round_sweep<K, kModeWarm, 1>, 256, 0);
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, k_round_sweep<K, kModeWarmPipe, 1>, 256, 0);
 }
 
 }  // namespace

@@ -188,7 +188,9 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  * "kernel"    (1/2): round kernel for the uncapped path: 2 = persistent sweep
  *                    (default, k <= 8), 1 = one wave per tile (A/B only).
  * "sweep_blocks"   : workgroups of the sweep grid (0 = one wave per tile,
- *                    -1 = every resident workgroup once, the default). */
+ *                    -1 = the engine's choice (default), -2 = every resident
+ *                    workgroup once, walking the tiles).
+ * "store_policy"   : 2 = write-through (sc1) plane stores, 3 = nt sc1 (A/B). */
 int av_set_option(av_engine* e, const char* name, int64_t value);
 
 /* ---- measurement ---- */

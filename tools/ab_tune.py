@@ -29,12 +29,12 @@ from bench import WORKLOADS  # noqa: E402
 VARIANTS = {
     "sweep": dict(kernel=2),
     "sweep_w1": dict(kernel=2, sweep_blocks=0),
-    "sweep_res": dict(kernel=2, sweep_blocks=-1),
+    "sweep_res": dict(kernel=2, sweep_blocks=-2),
     "per_tile": dict(kernel=1),
     "ablate": dict(kernel=2, ablate_gather=1),
     "w1_sc1": dict(kernel=2, sweep_blocks=0, store_policy=2),
     "w1_ntsc1": dict(kernel=2, sweep_blocks=0, store_policy=3),
-    "res_sc1": dict(kernel=2, sweep_blocks=-1, store_policy=2),
+    "res_sc1": dict(kernel=2, sweep_blocks=-2, store_policy=2),
     "w1_plain": dict(kernel=2, sweep_blocks=0, plane_nt=0),
 }
 

@@ -40,7 +40,9 @@ for s in "$@"; do
     ab1) step ab1 600 python tools/ab_tune.py --shards 1 --json $OUT/ab1.json ;;
     abc3) step abc3 600 python tools/ab_tune.py --workload c3 --shards 1 --variants sweep,per_tile,ablate --json $OUT/abc3.json ;;
     abpol) step abpol 600 python tools/ab_tune.py --shards 1,8 --variants sweep_w1,sweep_res,w1_sc1,w1_ntsc1,res_sc1,w1_plain --json $OUT/abpol.json ;;
+    abres) step abres 600 python tools/ab_tune.py --shards 1,2,4,8 --variants sweep,sweep_w1,sweep_res,ablate --json $OUT/abres.json ;;
     gprobe) step gprobe 120 go-avalanche_amd/bin/gather_probe 20 ;;
+    mprobe) step mprobe 120 go-avalanche_amd/bin/mix_probe ;;
     conv_c3) step conv_c3 900 python tools/run_to_finalization.py --workload c3 --json $OUT/conv_c3.json ;;
     conv_c5) step conv_c5 900 python tools/run_to_finalization.py --workload c5 --max-rounds 64 --json $OUT/conv_c5.json ;;
     conv_c4) step conv_c4 900 python tools/run_to_finalization.py --workload c4 --max-rounds 64 --json $OUT/conv_c4.json ;;
@@ -60,6 +62,12 @@ for s in "$@"; do
             go-avalanche_amd/bin/pmc_calib ;;
     pmc_sum) step pmc_sum 120 python tools/pmc_summary.py --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write \
             --fetch $OUT/pmc_fetch --write $OUT/pmc_write --kernel k_round_sweep --read-x1 36 --out $OUT/pmc_traffic_c4.json ;;
+    pmc_sq8) step pmc_sq8 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq8 -o ab -- \
+            python3 tools/ab_tune.py --shards 8 --variants sweep_w1,ablate --rounds 3 ;;
+    pmc_tcc8) step pmc_tcc8 300 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_tcc8 -o ab -- \
+            python3 tools/ab_tune.py --shards 8 --variants sweep_w1,ablate --rounds 3 ;;
+    pmc_sq1) step pmc_sq1 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq1 -o ab -- \
+            python3 tools/ab_tune.py --shards 1 --variants sweep_w1 --rounds 3 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
