@@ -126,8 +126,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         obj = [avhip.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(world, rank, obj[0])
-    if replay:
-        eng.replay_prepare(warmup + steps)
+    if replay:  # both passes' rounds (the roofline pass re-runs warmup + steps)
+        eng.replay_prepare(2 * (warmup + steps))
     run = eng.replay_rounds if replay else eng.run_rounds
     info = eng.layout_info()
 
@@ -138,10 +138,9 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         eng.fetch_updates(decode=False)
     except avhip.LogOverflow:
         pass  # the log is cleared on overflow; warmup updates are not measured
-    applied0, bytes0 = eng.applied_votes(), eng.alg_bytes()
+    applied0 = eng.applied_votes()
 
-    # ---- timed region
-    eng.set_timing(True)
+    # ---- timed region (no per-launch events: their queue packets add ~10 us between kernels)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -152,14 +151,26 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    eng.set_timing(False)
     log_overflow = eng.log_overflowed()  # updates past the device log's capacity were counted, not stored
-    kern_ms, launches = eng.kernel_stats()
     applied = eng.applied_votes() - applied0
     emitted = eng.updates_count()
+
+    # ---- roofline pass: the same work again (records re-initialized, warmup,
+    # `steps` rounds), every launch bracketed by HIP events on the engine's stream
+    eng.discard_updates()
+    eng.init_records(init_mode, init_param)
+    run(warmup)
+    eng.synchronize()
+    eng.discard_updates()
+    bytes1 = eng.alg_bytes()
+    eng.set_timing(True)
+    run(steps)
+    eng.synchronize()
+    eng.set_timing(False)
+    kern_ms, launches = eng.kernel_stats()
     # algorithmic bytes per launch, counted by the round kernel itself (planes
     # actually streamed, gathered vote words, published words, StatusUpdates)
-    alg_bytes = (eng.alg_bytes() - bytes0) / max(launches, 1)
+    alg_bytes = (eng.alg_bytes() - bytes1) / max(launches, 1)
     kavg_ms = kern_ms / max(launches, 1)
     eng.close()
 
