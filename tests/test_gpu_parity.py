@@ -1,6 +1,8 @@
 """GPU parity tests: the HIP engine (through the C ABI of libavhip.so) against
 the CPU oracle on identical seeded inputs, and against the golden vectors
 transcribed from the reference's tests. Bit-exact everywhere (integer path)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -416,3 +418,82 @@ def test_poll_sets_batch_parity(oracle, n, m):
             offs2, tg2 = eng.get_invs_batch(2, 5)
             assert [tg2[offs2[i]:offs2[i + 1]].tolist() for i in range(3)] == got[2:5]
     eng.fetch_updates()
+
+
+def test_target_shard_identity_8way():
+    """Eight target shards (BL = 4 per shard: the 8-GPU C4 decomposition) ==
+    one engine, bit for bit, through finalization and deletion (rounds 16-19)."""
+    n, m, k, R = 3000, 1000, 8, 20
+    full = avhip.Engine(n, m, k=k, seed=31, byz_threshold=BYZ20)
+    full.init_records(avhip.INIT_ACCEPTED, 0)
+    from avhip import sharding
+    parts = [avhip.Engine(n, m, k=k, seed=31, byz_threshold=BYZ20, target_range=sharding.target_shard(m, 8, r))
+             for r in range(8)]
+    for p in parts:
+        p.init_records(avhip.INIT_ACCEPTED, 0)
+    for r in range(R):
+        full.run_rounds(1)
+        for p in parts:
+            p.run_rounds(1)
+        u = np.concatenate([p.fetch_updates() for p in parts])
+        u = u[np.lexsort((u[:, 3], u[:, 2], u[:, 1], u[:, 0]))]
+        assert np.array_equal(full.fetch_updates(), u), r
+    merged = np.concatenate([p.read_records() for p in parts], axis=1)
+    assert np.array_equal(full.read_records(), merged)
+    assert full.applied_votes() == sum(p.applied_votes() for p in parts)
+    assert full.finalized_count() == sum(p.finalized_count() for p in parts) > 0
+
+
+def test_cross_kernel_full_c4():
+    """configs C4 at full size (1M nodes x 1000 targets, k=8, Bernoulli(0.8)):
+    the sweep kernel and the first-generation per-tile kernel agree on every
+    round's StatusUpdate count and on the records and published preferences of
+    sampled nodes, rounds 0-15; round 15's update streams agree exactly."""
+    n, m, k, R = 1_000_000, 1000, 8, 16
+    engs = []
+    for kernel in (2, 1):
+        e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4, log_capacity=1 << 26)
+        e.set_option("kernel", kernel)
+        e.init_records(avhip.INIT_BERNOULLI, P80)
+        engs.append(e)
+    rng = np.random.default_rng(0)
+    sample = np.unique(np.concatenate([[0, 1, n - 1], rng.integers(0, n, 64)]))
+    for r in range(R):
+        for e in engs:
+            e.run_rounds(1)
+        counts = [e.updates_count() for e in engs]
+        assert counts[0] == counts[1], (r, counts)
+        if r == R - 1:
+            a, b = (e.fetch_updates() for e in engs)
+            assert np.array_equal(a, b)
+        else:
+            for e in engs:
+                e.discard_updates()
+        if r % 5 == 0 or r == R - 1:
+            for node in sample[:8]:
+                ra, rb = (e.read_records(int(node), int(node) + 1, 0, m) for e in engs)
+                assert np.array_equal(ra, rb), (r, int(node))
+    for node in sample:
+        ra, rb = (e.read_records(int(node), int(node) + 1, 0, m) for e in engs)
+        assert np.array_equal(ra, rb), int(node)
+        pa, pb = (e.read_pref(int(node), int(node) + 1, 0, m) for e in engs)
+        assert np.array_equal(pa, pb), int(node)
+    assert engs[0].applied_votes() == engs[1].applied_votes() == n * m * k * R
+    for e in engs:
+        e.close()
+
+
+def test_sweep_parity_c3_shape(oracle):
+    """The C3 shape (double-spend pairs, 20 % Byzantine flip-flop voters) at
+    2000 nodes x 2000 targets, 30 rounds: sweep kernel vs oracle, bit-exact."""
+    n, m, k = 2000, 2000, 8
+    eng, sim = make_pair(oracle, n, m, k, seed=0xA7A1A9C4, byz=BYZ20, init_mode=4, log_capacity=1 << 24)
+    threads = min(8, os.cpu_count() or 1)
+    total = 0
+    for r in range(30):
+        eng.run_rounds(1)
+        exp_u, applied = sim.run_round(threads=threads)
+        total += applied
+        assert np.array_equal(eng.fetch_updates(), exp_u), r
+    assert_same_state(eng, sim)
+    assert eng.applied_votes() == total
