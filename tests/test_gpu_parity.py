@@ -424,11 +424,11 @@ def test_target_shard_identity_8way():
     """Eight target shards (BL = 4 per shard: the 8-GPU C4 decomposition) ==
     one engine, bit for bit, through finalization and deletion (rounds 16-19)."""
     n, m, k, R = 3000, 1000, 8, 20
-    full = avhip.Engine(n, m, k=k, seed=31, byz_threshold=BYZ20)
+    full = avhip.Engine(n, m, k=k, seed=31, byz_threshold=BYZ20, log_capacity=1 << 23)
     full.init_records(avhip.INIT_ACCEPTED, 0)
     from avhip import sharding
-    parts = [avhip.Engine(n, m, k=k, seed=31, byz_threshold=BYZ20, target_range=sharding.target_shard(m, 8, r))
-             for r in range(8)]
+    parts = [avhip.Engine(n, m, k=k, seed=31, byz_threshold=BYZ20, target_range=sharding.target_shard(m, 8, r),
+                          log_capacity=1 << 22) for r in range(8)]
     for p in parts:
         p.init_records(avhip.INIT_ACCEPTED, 0)
     for r in range(R):
