@@ -113,10 +113,27 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
   const bool exact = __syncthreads_or(nearfin != 0u) != 0;          // workgroup-uniform
 
   uint32_t E[K], applied = 0u, died = 0u;
-  u32x4 o0, o1;
-  uint32_t Cn[8];
   if (!exact) {
-    // the poll set is fixed for the round: shift every polled record by K votes
+    // the poll set is fixed for the round: every polled record shifts by K
+    // votes; its V/C planes are final now (stored before the slot loop so
+    // their registers are free during it)
+    if (active) {
+      u32x4 o0, o1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t vi = i < 4 ? v0[i] : v1[i - 4];
+        const uint32_t vs = i < K ? ys[6 + K - i] : (i - K < 4 ? v0[i - K] : v1[i - K - 4]);
+        const uint32_t vn = (vs & polled) | (vi & ~polled);
+        if (i < 4)
+          o0[i] = vn;
+        else
+          o1[i - 4] = vn;
+        const uint32_t cs = i < K ? cwv[K - 1 - i] : C[i - K];
+        pst<NT>(tp + 1024u + (uint32_t)i * 64u + tl, (cs & polled) | (C[i] & ~polled));
+      }
+      pst4<NT>(grp, o0);
+      pst4<NT>(grp + 64, o1);
+    }
     uint32_t alive = polled, c[4] = {0u, 0u, 0u, 0u}, F = 0u;
     const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
     round_slots<K, false>(ys, ns, low3, 0u, false, alive, A, E, c, F, applied);
@@ -129,18 +146,6 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
       const uint32_t si = t ^ cy;
       cy = (t & cy) | (Kp[i] & ci);
       Kp[i] = (F & ci) | (~F & si);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t vi = i < 4 ? v0[i] : v1[i - 4];
-      const uint32_t vs = i < K ? ys[6 + K - i] : (i - K < 4 ? v0[i - K] : v1[i - K - 4]);
-      const uint32_t vn = (vs & polled) | (vi & ~polled);
-      if (i < 4)
-        o0[i] = vn;
-      else
-        o1[i - 4] = vn;
-      const uint32_t cs = i < K ? cwv[K - 1 - i] : C[i - K];
-      Cn[i] = (cs & polled) | (C[i] & ~polled);
     }
   } else {
     // exact: per vote, re-select the poll set (a deleted record makes room)
@@ -156,32 +161,45 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
       s.K[i] = Kp[i];
     }
     s.A = A;
-    uint32_t alive = P0;
+    // a rolled loop over the slots, its vote words and outputs in private
+    // arrays: the rare path must not raise the kernel's register count
+    uint32_t wv[K], cv[K], Ex[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const uint32_t pj = j == 0 ? polled : cap_select(alive, lane, wave, wsum, (uint32_t)j & 1u);
+      wv[j] = ys[7 + j];
+      cv[j] = cwv[j];
+    }
+    uint32_t alive = P0, pj = polled;
+#pragma nounroll
+    for (int j = 0; j < K; ++j) {
+      if (j > 0) pj = cap_select(alive, lane, wave, wsum, (uint32_t)j & 1u);
       applied += (uint32_t)__popc(pj);
-      uint32_t fin;
-      vote_step<true>(s, ys[7 + j], cwv[j], pj, E[j], fin);
+      uint32_t fin, e;
+      vote_step<true>(s, wv[j], cv[j], pj, e, fin);
+      Ex[j] = e;
       alive &= ~fin;
     }
+#pragma unroll
+    for (int j = 0; j < K; ++j) E[j] = Ex[j];
     died = P0 & ~alive;
+    if (active) {
+      u32x4 o0, o1;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      o0[i] = s.V[i] & ~died;
-      o1[i] = s.V[4 + i] & ~died;
+      for (int i = 0; i < 4; ++i) {
+        o0[i] = s.V[i] & ~died;
+        o1[i] = s.V[4 + i] & ~died;
+      }
+      pst4<NT>(grp, o0);
+      pst4<NT>(grp + 64, o1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pst<NT>(tp + 1024u + (uint32_t)i * 64u + tl, s.C[i] | died);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      Cn[i] = s.C[i] | died;
-      Kp[i] = s.K[i];
-    }
+    for (int i = 0; i < 8; ++i) Kp[i] = s.K[i];
     A = s.A;
   }
 
   if (active) {
-    pst4<NT>(grp, o0);
-    pst4<NT>(grp + 64, o1);
     u32x4 o2, o3;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -190,8 +208,6 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
     }
     pst4<NT>(grp + 128, o2);
     pst4<NT>(grp + 192, o3);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) pst<NT>(tp + 1024u + (uint32_t)i * 64u + tl, Cn[i]);
     pst<NT>(tp + 1536u + tl, A);
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
   }
