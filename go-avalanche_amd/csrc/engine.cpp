@@ -68,6 +68,7 @@ struct av_engine {
   uint64_t* log = nullptr;
   uint32_t* log_count = nullptr;
   uint32_t* log_overflow = nullptr;
+  uint32_t* node_flags = nullptr;  // capped engines: nodes k_round_node leaves to the exact pass
   uint32_t log_cap = 0;
   uint32_t log_shards = 1;
   unsigned long long* applied = nullptr;
@@ -178,6 +179,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   p.peer_mode = e->cfg.peer_mode;
   p.warm_all = e->warm_all ? 1u : 0u;
   p.store_policy = e->store_policy;
+  p.node_flags = nullptr;
   p.bl_magic = e->bl_magic;
   p.bl_sh1 = e->bl_sh1;
   p.bl_sh2 = e->bl_sh2;
@@ -196,8 +198,10 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   }
   if (sweep)
     AV_HIP(avk::launch_round_sweep(p, e->k, replay != nullptr, e->sweep_blocks, e->stream));
-  else if (e->kernel == 2 && e->k <= 8 && e->capped)
+  else if (e->kernel == 2 && e->k <= 8 && e->capped) {
+    p.node_flags = e->node_flags;
     AV_HIP(avk::launch_round_node(p, e->k, replay != nullptr, e->stream));
+  }
   else
     AV_HIP(avk::launch_round(p, e->k, replay != nullptr, e->capped, e->stream));
   if (replay)
@@ -278,7 +282,7 @@ int av_destroy(av_engine* e) {
     (void)hipEventDestroy(ev.second);
   }
   if (e->comm) (void)ncclCommDestroy(e->comm);
-  void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->valid, e->byz, e->log, e->log_count, e->log_overflow,
+  void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->applied, e->bytes, e->finalized, e->scratch_count, e->replay};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -353,6 +357,10 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->log, (size_t)e->log_cap * e->log_shards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->log_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->log_overflow, 1)) != hipSuccess) return hip_fail(he, "alloc log");
+  if (e->capped) {
+    if ((he = dev_alloc(&e->node_flags, e->NL)) != hipSuccess) return hip_fail(he, "alloc node flags");
+    (void)hipMemsetAsync(e->node_flags, 0, (size_t)e->NL * 4, e->stream);
+  }
   if ((he = dev_alloc(&e->applied, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
   if ((he = dev_alloc(&e->bytes, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
   (void)hipMemsetAsync(e->bytes, 0, avk::kLogShards * 8, e->stream);

@@ -41,6 +41,7 @@ struct RoundParams {
   uint64_t* log;             // [kLogShards][log_cap]
   uint32_t* log_count;       // [kLogShards]
   uint32_t* log_overflow;    // [1]
+  uint32_t* node_flags;      // [NL] capped path: nodes left to the exact pass (nullptr: none)
   unsigned long long* applied;  // [kLogShards] regsiterVote applications
   unsigned long long* bytes;    // [kLogShards] algorithmic bytes moved by the round kernel
   unsigned long long* finalized;  // [kLogShards] records finalized (deleted, processor.go:114-116)
@@ -89,7 +90,9 @@ hipError_t launch_round(const RoundParams& p, int k, bool replay, bool capped, h
 // Persistent streaming round kernel (round_sweep.hip), uncapped path, k <= 8:
 // `blocks` workgroups of 256 threads sweep the tiles; 0 = one wave per tile.
 hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s);
-// Capped round (M > 4096, k <= 8; round_node.hip): one workgroup per node.
+// Capped round (M > 4096, k <= 8; round_node.hip): one workgroup per node;
+// nodes that may finalize a record this round are flagged in p.node_flags and
+// left to the exact pass (k_round_capped over the flagged nodes only).
 hipError_t launch_round_node(const RoundParams& p, int k, bool replay, hipStream_t s);
 // Resident 256-thread workgroups per CU for the sweep kernel and the CU count.
 hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cus);

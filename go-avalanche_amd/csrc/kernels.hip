@@ -161,6 +161,11 @@ template <int K, bool REPLAY>
 __global__ __launch_bounds__(1024) void k_round_capped(const RoundParams p) {
   __shared__ uint32_t wsum[2][16];
   const uint32_t nl = blockIdx.x;
+  if (p.node_flags) {  // exact pass behind k_round_node: only the nodes it flagged
+    if (p.node_flags[nl] == 0u) return;  // workgroup-uniform
+    __syncthreads();
+    if (threadIdx.x == 0) p.node_flags[nl] = 0u;
+  }
   const uint32_t b = threadIdx.x;
   const uint32_t lane = b & 63u, wave = b >> 6;
   const bool active = b < p.BL;

@@ -9,8 +9,10 @@
 //    set is selected once, and the round runs like k_round_sweep — per-slot
 //    threshold networks, deferred confidence update, the shift registers of
 //    the polled records advanced by k votes at once (round_slots.h);
-//  * otherwise: the exact per-vote path, re-selecting the poll set before
-//    every slot (the first version's algorithm, kernels.hip k_round_capped).
+//  * otherwise the node is flagged and left untouched; a second launch of the
+//    first version's exact kernel (kernels.hip k_round_capped: per-vote
+//    poll-set re-selection, deletion at 128) processes the flagged nodes only.
+//    Keeping the exact path out of this kernel keeps it at ~66 VGPRs.
 // Same layout, outputs and counters as k_round_capped; V/K move as dwordx4.
 #include <hip/hip_runtime.h>
 
@@ -112,28 +114,33 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
   const uint32_t nearfin = polled & Kp[6] & Kp[5] & Kp[4] & Kp[3];  // count >= 120
   const bool exact = __syncthreads_or(nearfin != 0u) != 0;          // workgroup-uniform
 
-  uint32_t E[K], applied = 0u, died = 0u;
-  if (!exact) {
-    // the poll set is fixed for the round: every polled record shifts by K
-    // votes; its V/C planes are final now (stored before the slot loop so
-    // their registers are free during it)
-    if (active) {
-      u32x4 o0, o1;
+  if (exact) {  // some polled record may reach 128: the exact pass (k_round_capped) takes this node
+    if (b == 0) p.node_flags[nl] = 1u;
+    return;
+  }
+  uint32_t E[K], applied = 0u;
+  const uint32_t died = 0u;
+  // the poll set is fixed for the round: every polled record shifts by K
+  // votes; its V/C planes are final now (stored before the slot loop so
+  // their registers are free during it)
+  if (active) {
+    u32x4 o0, o1;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t vi = i < 4 ? v0[i] : v1[i - 4];
-        const uint32_t vs = i < K ? ys[6 + K - i] : (i - K < 4 ? v0[i - K] : v1[i - K - 4]);
-        const uint32_t vn = (vs & polled) | (vi & ~polled);
-        if (i < 4)
-          o0[i] = vn;
-        else
-          o1[i - 4] = vn;
-        const uint32_t cs = i < K ? cwv[K - 1 - i] : C[i - K];
-        pst<NT>(tp + 1024u + (uint32_t)i * 64u + tl, (cs & polled) | (C[i] & ~polled));
-      }
-      pst4<NT>(grp, o0);
-      pst4<NT>(grp + 64, o1);
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t vi = i < 4 ? v0[i] : v1[i - 4];
+      const uint32_t vs = i < K ? ys[6 + K - i] : (i - K < 4 ? v0[i - K] : v1[i - K - 4]);
+      const uint32_t vn = (vs & polled) | (vi & ~polled);
+      if (i < 4)
+        o0[i] = vn;
+      else
+        o1[i - 4] = vn;
+      const uint32_t cs = i < K ? cwv[K - 1 - i] : C[i - K];
+      pst<NT>(tp + 1024u + (uint32_t)i * 64u + tl, (cs & polled) | (C[i] & ~polled));
     }
+    pst4<NT>(grp, o0);
+    pst4<NT>(grp + 64, o1);
+  }
+  {
     uint32_t alive = polled, c[4] = {0u, 0u, 0u, 0u}, F = 0u;
     const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
     round_slots<K, false>(ys, ns, low3, 0u, false, alive, A, E, c, F, applied);
@@ -147,56 +154,6 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
       cy = (t & cy) | (Kp[i] & ci);
       Kp[i] = (F & ci) | (~F & si);
     }
-  } else {
-    // exact: per vote, re-select the poll set (a deleted record makes room)
-    St s;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      s.V[i] = v0[i];
-      s.V[4 + i] = v1[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      s.C[i] = C[i];
-      s.K[i] = Kp[i];
-    }
-    s.A = A;
-    // a rolled loop over the slots, its vote words and outputs in private
-    // arrays: the rare path must not raise the kernel's register count
-    uint32_t wv[K], cv[K], Ex[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      wv[j] = ys[7 + j];
-      cv[j] = cwv[j];
-    }
-    uint32_t alive = P0, pj = polled;
-#pragma nounroll
-    for (int j = 0; j < K; ++j) {
-      if (j > 0) pj = cap_select(alive, lane, wave, wsum, (uint32_t)j & 1u);
-      applied += (uint32_t)__popc(pj);
-      uint32_t fin, e;
-      vote_step<true>(s, wv[j], cv[j], pj, e, fin);
-      Ex[j] = e;
-      alive &= ~fin;
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j) E[j] = Ex[j];
-    died = P0 & ~alive;
-    if (active) {
-      u32x4 o0, o1;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        o0[i] = s.V[i] & ~died;
-        o1[i] = s.V[4 + i] & ~died;
-      }
-      pst4<NT>(grp, o0);
-      pst4<NT>(grp + 64, o1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) pst<NT>(tp + 1024u + (uint32_t)i * 64u + tl, s.C[i] | died);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) Kp[i] = s.K[i];
-    A = s.A;
   }
 
   if (active) {
@@ -243,17 +200,21 @@ hipError_t launch_node_k(const RoundParams& p, bool replay, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_round_node(const RoundParams& p, int k, bool replay, hipStream_t s) {
+  if (!p.node_flags) return hipErrorInvalidValue;
+  hipError_t e;
   switch (k) {
-    case 1: return launch_node_k<1>(p, replay, s);
-    case 2: return launch_node_k<2>(p, replay, s);
-    case 3: return launch_node_k<3>(p, replay, s);
-    case 4: return launch_node_k<4>(p, replay, s);
-    case 5: return launch_node_k<5>(p, replay, s);
-    case 6: return launch_node_k<6>(p, replay, s);
-    case 7: return launch_node_k<7>(p, replay, s);
-    case 8: return launch_node_k<8>(p, replay, s);
+    case 1: e = launch_node_k<1>(p, replay, s); break;
+    case 2: e = launch_node_k<2>(p, replay, s); break;
+    case 3: e = launch_node_k<3>(p, replay, s); break;
+    case 4: e = launch_node_k<4>(p, replay, s); break;
+    case 5: e = launch_node_k<5>(p, replay, s); break;
+    case 6: e = launch_node_k<6>(p, replay, s); break;
+    case 7: e = launch_node_k<7>(p, replay, s); break;
+    case 8: e = launch_node_k<8>(p, replay, s); break;
     default: return hipErrorInvalidValue;
   }
+  if (e != hipSuccess) return e;
+  return launch_round(p, k, replay, /*capped=*/true, s);  // the exact pass over the flagged nodes
 }
 
 }  // namespace avk
