@@ -197,6 +197,26 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     }
 
 
+def allgather_probe(world, local_rank, total_bytes=1_000_000 * 128, reps=5):
+    per = total_bytes // world // 4 * 4
+    src = torch.ones(per // 4, dtype=torch.int32, device=f"cuda:{local_rank}")
+    dst = torch.empty(world * (per // 4), dtype=torch.int32, device=f"cuda:{local_rank}")
+    dist.all_gather_into_tensor(dst, src)  # warm
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_gather_into_tensor(dst, src)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local_rank}")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t)
+    inbound = per * (world - 1)
+    return {"bytes_total": per * world, "ms": dt * 1e3, "inbound_GBs_per_gpu": inbound / dt / 1e9,
+            "note": "C4 node-sharded round exchange (1M x 1000 bits), torch.distributed all_gather_into_tensor"}
+
+
 def roofline(r, traffic=None):
     return {"bound": "hbm", "achieved": r["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": r["achieved"] / HBM_PEAK_GBS, "traffic": traffic, "kernel": r["kernel"],
@@ -222,6 +242,15 @@ def main():
 
     r = measure(args.workload, args, world, rank, local_rank, args.steps, args.warmup)
     secondary = None
+    if world > 1 and not args.rehearse_one_gpu and not args.no_secondary:
+        # the exchange a node-sharded C4 round would need: every rank's published-
+        # preference rows (N/G x 128 B) all-gathered over xGMI (RCCL through
+        # torch.distributed); recorded for the node- vs target-sharding choice
+        # (DESIGN.md §5), not part of the timed value
+        try:
+            secondary = {"xgmi_allgather": allgather_probe(world, local_rank)}
+        except Exception as exc:  # a diagnostic: never costs the measured line
+            secondary = {"xgmi_allgather": {"error": repr(exc)[:200]}}
     if world == 1 and not args.no_secondary and args.workload != "c2":
         c2 = measure("c2", args, world, rank, local_rank, 14, 2)
         secondary = {"c2": {"workload": c2["desc"], "value": c2["value"], "unit": "vote-record updates/s",
