@@ -158,14 +158,29 @@ __global__ __launch_bounds__(256) void k_round_fast(const RoundParams p) {
 // target order (GetInvsForNextPoll truncation, processor.go:165-167).
 // ---------------------------------------------------------------------------
 template <int K, bool REPLAY>
+__device__ __forceinline__ void capped_node(const RoundParams& p, uint32_t nl, uint32_t (&wsum)[2][16]);
+
+template <int K, bool REPLAY>
 __global__ __launch_bounds__(1024) void k_round_capped(const RoundParams p) {
   __shared__ uint32_t wsum[2][16];
-  const uint32_t nl = blockIdx.x;
-  if (p.node_flags) {  // exact pass behind k_round_node: only the nodes it flagged
-    if (p.node_flags[nl] == 0u) return;  // workgroup-uniform
+  if (!p.node_flags) {
+    capped_node<K, REPLAY>(p, blockIdx.x, wsum);
+    return;
+  }
+  // exact pass behind k_round_node: a small grid walks the nodes and takes
+  // only the ones it flagged (an almost empty pass costs ~1-2 us, not the
+  // dispatch of one workgroup per node)
+  for (uint32_t nl = blockIdx.x; nl < p.NL; nl += gridDim.x) {
+    if (p.node_flags[nl] == 0u) continue;  // workgroup-uniform
     __syncthreads();
     if (threadIdx.x == 0) p.node_flags[nl] = 0u;
+    capped_node<K, REPLAY>(p, nl, wsum);
+    __syncthreads();  // wsum reuse by the next node
   }
+}
+
+template <int K, bool REPLAY>
+__device__ __forceinline__ void capped_node(const RoundParams& p, uint32_t nl, uint32_t (&wsum)[2][16]) {
   const uint32_t b = threadIdx.x;
   const uint32_t lane = b & 63u, wave = b >> 6;
   const bool active = b < p.BL;
@@ -235,7 +250,7 @@ __global__ __launch_bounds__(1024) void k_round_capped(const RoundParams p) {
     store_state(p.planes, g, s);
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
   }
-  const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
+  const uint32_t wave_id = nl * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
   const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
   count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted, died);
 }
@@ -545,10 +560,11 @@ template <int K>
 hipError_t launch_round_k(const RoundParams& p, bool replay, bool capped, hipStream_t s) {
   if (capped) {
     const uint32_t bt = ((p.BL + 63u) / 64u) * 64u;
+    const uint32_t grid = p.node_flags ? std::min(p.NL, 128u) : p.NL;
     if (replay)
-      hipLaunchKernelGGL((k_round_capped<K, true>), dim3(p.NL), dim3(bt), 0, s, p);
+      hipLaunchKernelGGL((k_round_capped<K, true>), dim3(grid), dim3(bt), 0, s, p);
     else
-      hipLaunchKernelGGL((k_round_capped<K, false>), dim3(p.NL), dim3(bt), 0, s, p);
+      hipLaunchKernelGGL((k_round_capped<K, false>), dim3(grid), dim3(bt), 0, s, p);
   } else {
     const uint32_t blocks = (p.Lpad + 255u) / 256u;
     if (replay)

@@ -70,6 +70,8 @@ for s in "$@"; do
             python3 tools/ab_tune.py --shards 1 --variants sweep_w1 --rounds 3 ;;
     gaps) step gaps 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps -o gap -- python3 tools/gap_probe.py --workload c4 ;;
     gaps2) step gaps2 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps2 -o gap -- python3 tools/gap_probe.py --workload c2 ;;
+    profc2) step profc2 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc2 -o c2 -- \
+            python3 bench.py --workload c2 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
