@@ -497,3 +497,38 @@ def test_sweep_parity_c3_shape(oracle):
         assert np.array_equal(eng.fetch_updates(), exp_u), r
     assert_same_state(eng, sim)
     assert eng.applied_votes() == total
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_config_fuzz(oracle, seed):
+    """Randomized network shapes through the round kernels vs the oracle:
+    N, M (BL from 1 to > 64 per node, tiles straddling nodes, M > 4096 with
+    the cap), k in 1..10, init modes, Byzantine share, peer mode, target
+    validity flips, both kernel generations and both sweep grids."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(3, 400))
+    m = int(rng.choice([int(rng.integers(1, 40)), int(rng.integers(40, 2100)), int(rng.integers(4097, 6000))]))
+    if m > 4096:
+        n = min(n, 40)
+    k = int(rng.integers(1, 11))
+    init_mode = int(rng.integers(1, 5))
+    byz = int(rng.choice([0, int(0.2 * 2**32), int(0.45 * 2**32)]))
+    peer_mode = int(rng.random() < 0.15)
+    kernel = int(rng.choice([1, 2]))
+    blocks = int(rng.choice([-1, 0, -2]))
+    eng, sim = make_pair(oracle, n, m, k, seed=int(rng.integers(1, 2**31)), peer_mode=peer_mode, byz=byz,
+                         init_mode=init_mode, init_param=int(rng.integers(0, 2**32)), log_capacity=1 << 22,
+                         kernel=kernel)
+    if kernel == 2 and blocks != -1:
+        eng.set_option("sweep_blocks", blocks)
+    rounds = int(rng.integers(5, 40))
+    for r in range(rounds):
+        if rng.random() < 0.1:
+            t = int(rng.integers(0, m))
+            v = bool(rng.integers(0, 2))
+            eng.set_valid(t, v)
+            sim.set_valid(t, v)
+        eng.run_rounds(1)
+        exp_u, _ = sim.run_round()
+        assert rows(eng.fetch_updates()) == rows(exp_u), (r, n, m, k)
+    assert_same_state(eng, sim, f"n={n} m={m} k={k} kernel={kernel} blocks={blocks}")
