@@ -92,6 +92,10 @@ struct av_engine {
   bool warm_all = false;
   uint32_t bl_magic = 1, bl_sh1 = 0, bl_sh2 = 0;
   uint32_t store_policy = 0;  // option "store_policy": 2 = sc1 (write-through) plane stores, 3 = nt sc1
+  // upper bound on any live record's count (confidence >> 1) at the start of the next round: a
+  // round adds at most k, init/add start at 0, anything else sets it to 127. While it is < 120 no
+  // record can finalize in the next round (k <= 8), so the capped path skips its exact pass.
+  int count_bound = 127;
   std::vector<uint32_t> valid_host;
   // replay stream
   uint32_t* replay = nullptr;
@@ -200,10 +204,11 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     AV_HIP(avk::launch_round_sweep(p, e->k, replay != nullptr, e->sweep_blocks, e->stream));
   else if (e->kernel == 2 && e->k <= 8 && e->capped) {
     p.node_flags = e->node_flags;
-    AV_HIP(avk::launch_round_node(p, e->k, replay != nullptr, e->stream));
+    AV_HIP(avk::launch_round_node(p, e->k, replay != nullptr, /*exact_pass=*/e->count_bound >= 120, e->stream));
   }
   else
     AV_HIP(avk::launch_round(p, e->k, replay != nullptr, e->capped, e->stream));
+  e->count_bound = std::min(127, e->count_bound + e->k);
   if (replay)
     e->warm_all = false;
   else if (e->c_monotone && e->k >= 8 && !e->capped && all_valid)
@@ -397,6 +402,7 @@ int av_create(const av_config* cfg, av_engine** out) {
 int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
   AV_ENTER(e);
   e->warm_all = false;
+  e->count_bound = 0;  // every record starts at count 0 (NewVoteRecord, vote.go:33-35)
   AV_CHECK(init_mode >= AV_INIT_NONE && init_mode <= AV_INIT_PAIRS, AV_ERR_INVALID_ARG, "bad init_mode");
   avk::InitParams p{};
   p.planes = e->planes;
@@ -487,6 +493,7 @@ int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const 
   AV_CHECK(n >= 0 && (n == 0 || (targets && errs && status_out)), AV_ERR_INVALID_ARG, "null argument");
   AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
   for (int64_t i = 0; i < n; ++i) status_out[i] = -1;
+  e->count_bound = std::min<int64_t>(127, e->count_bound + n);  // at most one step per vote
   // group votes by block, keeping Response order inside each block
   std::vector<uint32_t> cnt(e->BL + 1, 0);
   int64_t nv = 0;
@@ -575,6 +582,7 @@ int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t
   const size_t n = (size_t)(n1 - n0) * (size_t)(t1 - t0);
   if (!n) return AV_OK;
   e->c_monotone = false;
+  e->count_bound = 127;  // arbitrary counts written
   Scratch s;
   AV_HIP(s.ensure(n * 4));
   AV_HIP(hipMemcpyAsync(s.p, in, n * 4, hipMemcpyHostToDevice, e->stream));

@@ -92,8 +92,9 @@ hipError_t launch_round(const RoundParams& p, int k, bool replay, bool capped, h
 hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s);
 // Capped round (M > 4096, k <= 8; round_node.hip): one workgroup per node;
 // nodes that may finalize a record this round are flagged in p.node_flags and
-// left to the exact pass (k_round_capped over the flagged nodes only).
-hipError_t launch_round_node(const RoundParams& p, int k, bool replay, hipStream_t s);
+// left to the exact pass (k_round_capped over the flagged nodes only), which
+// the caller may skip when no count can have reached 120 (exact_pass false).
+hipError_t launch_round_node(const RoundParams& p, int k, bool replay, bool exact_pass, hipStream_t s);
 // Resident 256-thread workgroups per CU for the sweep kernel and the CU count.
 hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cus);
 

@@ -199,7 +199,7 @@ hipError_t launch_node_k(const RoundParams& p, bool replay, hipStream_t s) {
 
 }  // namespace
 
-hipError_t launch_round_node(const RoundParams& p, int k, bool replay, hipStream_t s) {
+hipError_t launch_round_node(const RoundParams& p, int k, bool replay, bool exact_pass, hipStream_t s) {
   if (!p.node_flags) return hipErrorInvalidValue;
   hipError_t e;
   switch (k) {
@@ -213,7 +213,7 @@ hipError_t launch_round_node(const RoundParams& p, int k, bool replay, hipStream
     case 8: e = launch_node_k<8>(p, replay, s); break;
     default: return hipErrorInvalidValue;
   }
-  if (e != hipSuccess) return e;
+  if (e != hipSuccess || !exact_pass) return e;
   return launch_round(p, k, replay, /*capped=*/true, s);  // the exact pass over the flagged nodes
 }
 
