@@ -67,6 +67,10 @@ struct av_engine {
   uint32_t* byz = nullptr;
   uint64_t* log = nullptr;
   uint32_t* log_count = nullptr;
+  uint64_t* dlog = nullptr;          // dense lane records (kernels.h dense_words(k) u64 each)
+  uint32_t* dlog_count = nullptr;
+  uint32_t* upd_count = nullptr;     // StatusUpdates emitted per shard (singles + dense bits)
+  uint32_t dlog_cap = 0;
   uint32_t* log_overflow = nullptr;
   uint32_t* node_flags = nullptr;  // capped engines: nodes k_round_node leaves to the exact pass
   uint32_t log_cap = 0;
@@ -161,6 +165,10 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   p.replay = replay;
   p.log = e->log;
   p.log_count = e->log_count;
+  p.dlog = e->dlog;
+  p.dlog_count = e->dlog_count;
+  p.upd_count = e->upd_count;
+  p.dlog_cap = e->dlog_cap;
   p.log_overflow = e->log_overflow;
   p.applied = e->applied;
   p.bytes = e->bytes;
@@ -288,6 +296,7 @@ int av_destroy(av_engine* e) {
   }
   if (e->comm) (void)ncclCommDestroy(e->comm);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
+                  e->dlog, e->dlog_count, e->upd_count,
                   e->applied, e->bytes, e->finalized, e->scratch_count, e->replay};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -333,6 +342,8 @@ int av_create(const av_config* cfg, av_engine** out) {
   if (e->capped && e->BL > 1024) return bad("capped path supports M <= 32768");
   const uint64_t L = (uint64_t)e->NL * e->BL;
   if (L >= (1ull << 31)) return bad("too many lanes for one engine: shard further");
+  // the round kernels index the published-preference table (all N nodes x BL words) in 32 bits
+  if ((uint64_t)e->N * e->BL >= (1ull << 31)) return bad("preference table over 2^31 words: shard targets further");
   e->L = (uint32_t)L;
   e->Lpad = (uint32_t)((L + 63) / 64 * 64);
   avk::bl_divider(e->BL, e->bl_magic, e->bl_sh1, e->bl_sh2);
@@ -361,6 +372,15 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->byz, (e->N + 31) / 32)) != hipSuccess) return hip_fail(he, "alloc byz");
   if ((he = dev_alloc(&e->log, (size_t)e->log_cap * e->log_shards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->log_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  // a dense record holds >= dense_min(k) updates: log_cap / dense_min records
+  // take any log_cap updates that go dense (8 B of capacity per update)
+  const uint32_t dw = avk::dense_words((uint32_t)e->k);
+  e->dlog_cap = std::max<uint32_t>(e->log_cap / avk::dense_min((uint32_t)e->k), 16);
+  if ((he = dev_alloc(&e->dlog, (size_t)e->dlog_cap * e->log_shards * dw)) != hipSuccess) return hip_fail(he, "alloc log");
+  if ((he = dev_alloc(&e->dlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  if ((he = dev_alloc(&e->upd_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  (void)hipMemsetAsync(e->dlog_count, 0, avk::kLogShards * 4, e->stream);
+  (void)hipMemsetAsync(e->upd_count, 0, avk::kLogShards * 4, e->stream);
   if ((he = dev_alloc(&e->log_overflow, 1)) != hipSuccess) return hip_fail(he, "alloc log");
   if (e->capped) {
     if ((he = dev_alloc(&e->node_flags, e->NL)) != hipSuccess) return hip_fail(he, "alloc node flags");
@@ -759,11 +779,22 @@ int av_round_index(av_engine* e, int64_t* out) {
   return AV_OK;
 }
 
+// Reset the three log counters (and the overflow flag) on the engine stream.
+int clear_log(av_engine* e) {
+  AV_HIP(hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream));
+  AV_HIP(hipMemsetAsync(e->dlog_count, 0, avk::kLogShards * 4, e->stream));
+  AV_HIP(hipMemsetAsync(e->upd_count, 0, avk::kLogShards * 4, e->stream));
+  AV_HIP(hipMemsetAsync(e->log_overflow, 0, 4, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  e->log_base = e->round;
+  return AV_OK;
+}
+
 int av_updates_count(av_engine* e, int64_t* n) {
   AV_ENTER(e);
   AV_CHECK(n, AV_ERR_INVALID_ARG, "null argument");
   std::vector<uint32_t> counts(avk::kLogShards);
-  AV_HIP(hipMemcpyAsync(counts.data(), e->log_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpyAsync(counts.data(), e->upd_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
   int64_t total = 0;
   for (uint32_t c : counts) total += c;
@@ -784,45 +815,72 @@ int av_update_log_overflowed(av_engine* e, int32_t* out) {
 int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
   AV_ENTER(e);
   AV_CHECK(n_out && (cap == 0 || out), AV_ERR_INVALID_ARG, "null argument");
-  std::vector<uint32_t> counts(avk::kLogShards);
+  std::vector<uint32_t> counts(avk::kLogShards), dcounts(avk::kLogShards), upd(avk::kLogShards);
   uint32_t ovf = 0;
   AV_HIP(hipMemcpyAsync(counts.data(), e->log_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpyAsync(dcounts.data(), e->dlog_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpyAsync(upd.data(), e->upd_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipMemcpyAsync(&ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
-  int64_t total = 0;
-  std::vector<uint64_t> offs(avk::kLogShards);
+  int64_t total = 0, singles = 0, records = 0;
+  std::vector<uint64_t> offs(avk::kLogShards), doffs(avk::kLogShards);
   for (uint32_t i = 0; i < avk::kLogShards; ++i) {
-    offs[i] = (uint64_t)total;
-    total += std::min<uint32_t>(counts[i], e->log_cap);
+    total += upd[i];
+    offs[i] = (uint64_t)singles;
+    singles += std::min<uint32_t>(counts[i], e->log_cap);
+    doffs[i] = (uint64_t)records;
+    records += std::min<uint32_t>(dcounts[i], e->dlog_cap);
   }
   *n_out = total;
   if (ovf) {
-    int64_t all = 0;
-    for (uint32_t c : counts) all += c;
-    *n_out = all;
-    AV_HIP(hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream));
-    AV_HIP(hipMemsetAsync(e->log_overflow, 0, 4, e->stream));
-    AV_HIP(hipStreamSynchronize(e->stream));
-    e->log_base = e->round;
+    int rc = clear_log(e);
+    if (rc != AV_OK) return rc;
     return fail(AV_ERR_OVERFLOW, "device StatusUpdate log overflowed (%lld updates, capacity %lld per shard)",
-                (long long)all, (long long)e->log_cap);
+                (long long)total, (long long)e->log_cap);
   }
   AV_CHECK(total <= cap, AV_ERR_OVERFLOW, "cap too small: %lld updates pending", (long long)total);
   if (total > 0) {
-    Scratch s;
-    AV_HIP(s.ensure((size_t)total * 8 + avk::kLogShards * 8));
-    auto* dense = static_cast<uint64_t*>(s.p);
-    auto* doffs = dense + total;
-    AV_HIP(hipMemcpyAsync(doffs, offs.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
-    AV_HIP(avk::launch_compact_log(e->log, e->log_count, doffs, e->log_cap, e->log_shards, dense, e->stream));
-    AV_HIP(hipMemcpyAsync(out, dense, (size_t)total * 8, hipMemcpyDeviceToHost, e->stream));
+    Scratch sc;
+    const uint32_t K = (uint32_t)e->k, dw = avk::dense_words(K);
+    AV_HIP(sc.ensure((size_t)(singles + dw * records) * 8 + 2 * avk::kLogShards * 8));
+    auto* dsingles = static_cast<uint64_t*>(sc.p);
+    auto* drecords = dsingles + singles;
+    auto* doff1 = drecords + dw * records;
+    auto* doff3 = doff1 + avk::kLogShards;
+    AV_HIP(hipMemcpyAsync(doff1, offs.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
+    AV_HIP(hipMemcpyAsync(doff3, doffs.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
+    AV_HIP(avk::launch_compact_log(e->log, e->log_count, doff1, e->log_cap, e->log_shards, 1, dsingles, e->stream));
+    AV_HIP(avk::launch_compact_log(e->dlog, e->dlog_count, doff3, e->dlog_cap, e->log_shards, dw, drecords,
+                                   e->stream));
+    AV_HIP(hipMemcpyAsync(out, dsingles, (size_t)singles * 8, hipMemcpyDeviceToHost, e->stream));
+    std::vector<uint64_t> rec((size_t)records * dw);
+    AV_HIP(hipMemcpyAsync(rec.data(), drecords, rec.size() * 8, hipMemcpyDeviceToHost, e->stream));
     AV_HIP(hipStreamSynchronize(e->stream));
+    // expand dense lane records (kernels.h): key (the block's first target,
+    // slot 0), E_0..E_{k-1}, final A, deletion mask; A after slot j = final A
+    // ^ parity of the later slots' updates
+    int64_t n = singles;
+    for (int64_t r = 0; r < records; ++r) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(rec.data() + (size_t)r * dw);
+      const uint64_t key = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+      const uint32_t died = w[3 + K];
+      uint32_t par = 0;
+      for (int j = (int)K - 1; j >= 0; --j) {
+        const uint32_t aj = w[2 + K] ^ par;
+        par ^= w[2 + j];
+        for (uint32_t em = w[2 + j]; em && n < total; em &= em - 1u) {
+          const uint32_t bit = (uint32_t)__builtin_ctz(em);
+          const uint64_t a = (aj >> bit) & 1u;
+          const uint64_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
+          out[n++] = key + ((uint64_t)j << 24) + ((uint64_t)bit << 2) + st;
+        }
+      }
+    }
+    AV_CHECK(n == total, AV_ERR_HIP, "StatusUpdate log inconsistent (%lld of %lld)", (long long)n,
+             (long long)total);
     std::sort(out, out + total);
   }
-  AV_HIP(hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream));
-  AV_HIP(hipStreamSynchronize(e->stream));
-  e->log_base = e->round;
-  return AV_OK;
+  return clear_log(e);
 }
 
 int av_applied_votes(av_engine* e, int64_t* out) {
@@ -868,11 +926,7 @@ int av_live_records(av_engine* e, int32_t honest_only, int64_t* out) {
 
 int av_discard_updates(av_engine* e) {
   AV_ENTER(e);
-  AV_HIP(hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream));
-  AV_HIP(hipMemsetAsync(e->log_overflow, 0, 4, e->stream));
-  AV_HIP(hipStreamSynchronize(e->stream));
-  e->log_base = e->round;
-  return AV_OK;
+  return clear_log(e);
 }
 
 int av_alg_bytes(av_engine* e, int64_t* out) {

@@ -38,8 +38,11 @@ struct RoundParams {
   const uint32_t* valid;     // [BL] Target.IsValid() bits
   const uint32_t* byz;       // [ceil(N/32)] Byzantine node bits
   const uint32_t* replay;    // [k][2][Lpad] yes/consider planes (replay mode)
-  uint64_t* log;             // [kLogShards][log_cap]
-  uint32_t* log_count;       // [kLogShards]
+  uint64_t* log;             // [kLogShards][log_cap] single StatusUpdates
+  uint32_t* log_count;       // [kLogShards] singles reserved per shard
+  uint64_t* dlog;            // [kLogShards][dlog_cap][dense_words(k)] dense lane records
+  uint32_t* dlog_count;      // [kLogShards] dense records reserved per shard
+  uint32_t* upd_count;       // [kLogShards] StatusUpdates emitted (singles + dense bits)
   uint32_t* log_overflow;    // [1]
   uint32_t* node_flags;      // [NL] capped path: nodes left to the exact pass (nullptr: none)
   unsigned long long* applied;  // [kLogShards] regsiterVote applications
@@ -47,6 +50,7 @@ struct RoundParams {
   unsigned long long* finalized;  // [kLogShards] records finalized (deleted, processor.go:114-116)
   uint64_t seed;
   uint32_t log_cap;          // entries per shard
+  uint32_t dlog_cap;         // dense records per shard
   uint32_t log_shards;       // shards in use (<= kLogShards; min(waves, kLogShards))
   uint32_t n_nodes;          // N (global)
   uint32_t n0;               // first local node (global id)
@@ -76,6 +80,15 @@ inline void bl_divider(uint32_t d, uint32_t& magic, uint32_t& sh1, uint32_t& sh2
   sh1 = l < 1 ? l : 1;
   sh2 = l > 1 ? l - 1 : 0;
 }
+
+// A lane (32-record block) with many StatusUpdates in one round logs one dense
+// record instead of single entries: u32 words [key lo, key hi (pack_update
+// with the block's first target, slot 0, status 0), E_0 .. E_{k-1} (updated
+// records per slot), A (final accepted plane), died (records deleted this
+// round)], padded to whole u64 words; fetch expands it. Dense when its size
+// is at most that of the singles: 8 * count >= 8 * dense_words(k).
+__host__ __device__ constexpr uint32_t dense_words(uint32_t k) { return (k + 5u) / 2u; }  // u64 words
+__host__ __device__ constexpr uint32_t dense_min(uint32_t k) { return dense_words(k); }   // updates
 
 // Update-log entry (one StatusUpdate, avalanche.go:59-62):
 //   [63:52] round - log_base | [51:28] node | [27:24] slot | [23:2] target | [1:0] status
@@ -151,7 +164,8 @@ hipError_t launch_count_live(const uint32_t* planes, const uint32_t* valid, cons
 // Batched poll sets: counts (out == nullptr path) or CSR targets at offsets.
 hipError_t launch_poll_sets(const uint32_t* planes, const uint32_t* valid, uint32_t BL, uint32_t nl0, uint32_t n,
                             uint32_t t0, uint32_t* counts, const int64_t* offsets, int32_t* out, hipStream_t s);
+// Concatenate the shards' first min(count, cap) entries of `words` u64 each.
 hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets,
-                              uint32_t log_cap, uint32_t shards, uint64_t* out, hipStream_t s);
+                              uint32_t log_cap, uint32_t shards, uint32_t words, uint64_t* out, hipStream_t s);
 
 }  // namespace avk

@@ -116,10 +116,11 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
   }
   const uint32_t wave_id = g >> 6;
-  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
+  uint32_t upd = 0;
+  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died, upd);
   constexpr uint32_t plane_bytes = WARM ? (18u + 17u) * 4u : 2u * kPlanes * 4u;
   constexpr uint32_t bytes = plane_bytes + (REPLAY ? 8u : 4u) * K + 4u;
-  count_stats(p, wave_id, lane, applied, active, bytes, emitted, died);
+  count_stats(p, wave_id, lane, applied, active, bytes, emitted, upd, died);
 }
 
 // ---------------------------------------------------------------------------
@@ -251,8 +252,10 @@ __device__ __forceinline__ void capped_node(const RoundParams& p, uint32_t nl, u
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
   }
   const uint32_t wave_id = nl * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
-  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died);
-  count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted, died);
+  uint32_t upd = 0;
+  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, s.A, died, upd);
+  count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted, upd,
+              died);
 }
 
 // ---------------------------------------------------------------------------
@@ -519,11 +522,11 @@ __global__ void k_count_live(const uint32_t* planes, const uint32_t* valid, cons
 }
 
 __global__ void k_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets, uint32_t log_cap,
-                              uint64_t* out) {
+                              uint32_t words, uint64_t* out) {
   const uint32_t shard = blockIdx.x;
-  const uint32_t n = min(counts[shard], log_cap);
-  const uint64_t* src = log + (size_t)shard * log_cap;
-  uint64_t* dst = out + offsets[shard];
+  const uint32_t n = min(counts[shard], log_cap) * words;
+  const uint64_t* src = log + (size_t)shard * log_cap * words;
+  uint64_t* dst = out + offsets[shard] * words;
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
 }
 
@@ -697,8 +700,8 @@ hipError_t launch_poll_sets(const uint32_t* planes, const uint32_t* valid, uint3
 }
 
 hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets, uint32_t log_cap,
-                              uint32_t shards, uint64_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_compact_log, dim3(shards), dim3(256), 0, s, log, counts, offsets, log_cap, out);
+                              uint32_t shards, uint32_t words, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_compact_log, dim3(shards), dim3(256), 0, s, log, counts, offsets, log_cap, words, out);
   return hipGetLastError();
 }
 

@@ -291,75 +291,106 @@ __device__ __forceinline__ void note_overflow(const RoundParams& p, uint32_t lan
     __hip_atomic_store(p.log_overflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// End-of-round StatusUpdate emission (processor.go:111) for one wave: one
-// atomic per emitting wave on a sharded log counter reserves the wave's
-// total; then, per slot, every iteration lets each lane with updates left
-// emit one entry into consecutive log slots (mbcnt over the active lanes),
-// so every store instruction writes one contiguous run. The log order is
-// irrelevant: the packed key sorts to the canonical (round, node, slot,
-// target) order on fetch. Status is derived from the final A plane: after
-// slot j, A_j = A_final ^ parity(E at later slots) (only flips change A); a
-// record finalized this round has a single E bit (count 127 -> 128 cannot
-// follow a flip within 16 votes).
+// End-of-round StatusUpdate emission (processor.go:111) for one wave. Status
+// comes from the final A plane: after slot j, A_j = A_final ^ parity(E at
+// later slots) (only flips change A); a record finalized this round has a
+// single E bit (count 127 -> 128 cannot follow a flip within 16 votes).
+//  * a lane with >= dense_min(K) updates (6 at k=8) writes one dense record
+//    (kernels.h: key, E_0..E_{K-1}, A, died; 48 B at k=8) — a finalization
+//    storm costs ~3 B per update instead of 8;
+//  * the other lanes' updates are single packed words: one atomic per wave on
+//    a sharded counter reserves the wave's total, then each iteration lets
+//    every lane with updates left write one entry into consecutive slots
+//    (mbcnt over the active lanes), one contiguous run per store instruction.
+// The log order is irrelevant: the packed key sorts to the canonical (round,
+// node, slot, target) order on fetch. Returns the bytes written (wave-uniform)
+// and adds the wave's update count to *updates.
 template <int K>
 __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t wave_id, uint32_t lane,
                                                  uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
-                                                 uint32_t A_final, uint32_t died) {
+                                                 uint32_t A_final, uint32_t died, uint32_t& updates) {
   uint32_t any = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) any |= E[j];
   if (__ballot(any != 0u) == 0ull) return 0u;
   uint32_t cnt = 0;
 #pragma unroll
-  for (int j = 0; j < K; ++j) cnt += __popc(E[j]);
-  const uint32_t total = wave_sum(cnt);
+  for (int j = 0; j < K; ++j) cnt += (uint32_t)__popc(E[j]);
+  constexpr uint32_t DW = dense_words(K);
+  const bool dense = cnt >= dense_min(K);
+  const uint64_t dl = __ballot(dense);
+  const uint32_t tot_u = wave_sum(cnt), tot_s = wave_sum(dense ? 0u : cnt);
+  const uint32_t tot_d = (uint32_t)__popcll(dl);
+  updates += tot_u;
   const uint32_t shard = wave_id % p.log_shards;
-  uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(&p.log_count[shard], total);
+  uint32_t base = 0, dbase = 0;
+  if (lane == 0) {
+    if (tot_s) base = atomicAdd(&p.log_count[shard], tot_s);
+    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard], tot_d);
+  }
   base = (uint32_t)__shfl((int)base, 0, 64);
-  uint32_t Aj[K];
-  uint32_t par = 0;
-#pragma unroll
-  for (int j = K - 1; j >= 0; --j) {
-    Aj[j] = A_final ^ par;
-    par ^= E[j];
-  }
-  uint64_t* dst = p.log + (size_t)shard * p.log_cap;
-  uint32_t run = base;  // wave-uniform
-  if (base >= p.log_cap) {  // shard already full: nothing can be stored
-    note_overflow(p, lane);
-    return total;
-  }
+  dbase = (uint32_t)__shfl((int)dbase, 0, 64);
   bool ovf = false;
-  for (int j = 0; j < K; ++j) {  // not unrolled (data-dependent inner loop); E/Aj stay in VGPRs
-    uint32_t e = E[j];
-    for (;;) {
-      const uint64_t act = __ballot(e != 0u);
-      if (act == 0ull) break;
-      if (e) {
-        const uint32_t bit = (uint32_t)__ffs(e) - 1u;
-        e &= e - 1u;
-        const uint32_t a = (Aj[j] >> bit) & 1u;
-        const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
-        const uint32_t pos =
-            run + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-        if (pos < p.log_cap)
-          dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
-        else
-          ovf = true;
+  if (dense) {
+    const uint32_t pos = dbase + __builtin_amdgcn_mbcnt_hi((uint32_t)(dl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dl, 0u));
+    if (pos < p.dlog_cap) {
+      uint32_t* rec = reinterpret_cast<uint32_t*>(p.dlog + ((size_t)shard * p.dlog_cap + pos) * DW);
+      const uint64_t key = pack_update(p.round_rel, node, 0u, tbase, 0u);
+      rec[0] = (uint32_t)key;
+      rec[1] = (uint32_t)(key >> 32);
+#pragma unroll
+      for (int j = 0; j < K; ++j) rec[2 + j] = E[j];
+      rec[2 + K] = A_final;
+      rec[3 + K] = died;
+    } else {
+      ovf = true;
+    }
+  }
+  if (tot_s) {
+    uint32_t Aj[K];
+    uint32_t par = 0;
+#pragma unroll
+    for (int j = K - 1; j >= 0; --j) {
+      Aj[j] = A_final ^ par;
+      par ^= E[j];
+    }
+    uint64_t* dst = p.log + (size_t)shard * p.log_cap;
+    uint32_t run = base;  // wave-uniform
+    if (base >= p.log_cap) {  // shard already full: nothing can be stored
+      ovf = true;
+    } else {
+      for (int j = 0; j < K; ++j) {  // not unrolled (data-dependent inner loop); E/Aj stay in VGPRs
+        uint32_t e = dense ? 0u : E[j];
+        for (;;) {
+          const uint64_t act = __ballot(e != 0u);
+          if (act == 0ull) break;
+          if (e) {
+            const uint32_t bit = (uint32_t)__ffs(e) - 1u;
+            e &= e - 1u;
+            const uint32_t a = (Aj[j] >> bit) & 1u;
+            const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
+            const uint32_t pos = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+            if (pos < p.log_cap)
+              dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
+            else
+              ovf = true;
+          }
+          run += (uint32_t)__popcll(act);
+        }
       }
-      run += (uint32_t)__popcll(act);
     }
   }
   if (__ballot(ovf) != 0ull) note_overflow(p, lane);
-  return total;
+  return 8u * tot_s + 8u * DW * tot_d;
 }
 
 // Per-wave counters: regsiterVote applications (the metric numerator) and the
 // algorithmic bytes this wave moved (state planes actually read/written,
-// gathered vote words, the published word, 8 B per emitted StatusUpdate).
+// gathered vote words, the published word, the StatusUpdate log bytes written).
 __device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied,
-                                            bool active, uint32_t bytes_per_lane, uint32_t emitted, uint32_t died) {
+                                            bool active, uint32_t bytes_per_lane, uint32_t emitted_bytes,
+                                            uint32_t updates, uint32_t died) {
   const uint32_t s = wave_sum(applied);
   const uint32_t f = wave_sum(__popc(died));
   const uint32_t nact = (uint32_t)__popcll(__ballot(active));
@@ -367,7 +398,8 @@ __device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_
     const uint32_t shard = wave_id % p.log_shards;
     if (s) atomicAdd(&p.applied[shard], (unsigned long long)s);
     if (f) atomicAdd(&p.finalized[shard], (unsigned long long)f);
-    atomicAdd(&p.bytes[shard], (unsigned long long)nact * bytes_per_lane + 8ull * emitted);
+    atomicAdd(&p.bytes[shard], (unsigned long long)nact * bytes_per_lane + emitted_bytes);
+    if (updates) atomicAdd(&p.upd_count[shard], updates);
   }
 }
 

@@ -169,8 +169,10 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
     p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
   }
   const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
-  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, died);
-  count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted, died);
+  uint32_t upd = 0;
+  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, died, upd);
+  count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted, upd,
+              died);
 }
 
 template <int K, int MAXT>

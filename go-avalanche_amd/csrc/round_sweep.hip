@@ -41,7 +41,7 @@ namespace {
 
 struct SweepAcc {
   uint32_t applied = 0, died = 0, lane_bytes = 0;
-  uint32_t emitted = 0;  // wave-uniform
+  uint32_t emitted_bytes = 0, updates = 0;  // wave-uniform: StatusUpdate log bytes written, updates emitted
 };
 
 enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3, kModeWarmPipe = 4 };
@@ -219,29 +219,18 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     const uint32_t prow = node * p.BL + b;  // < N * BL < 2^31
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, 0x7FFFFFFF, kRsrcWord3);
     st1<POL>(pr, p.pref_out + prow, prow * 4u, is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A);
-    if (died) {  // deleted records: canonical votes 0 / consider all-ones (rare; same lane, same addresses)
-      u32x4 d0 = pld4<false>(grp), d1 = pld4<false>(grp + 64);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        d0[i] &= ~died;
-        d1[i] &= ~died;
-      }
-      pst4<false>(grp, d0);
-      pst4<false>(grp + 64, d1);
-      if (!WARM) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) tp[1024u + (uint32_t)i * 64u + lane] |= died;
-      }
-    }
+    // a record deleted this round keeps the vote/consider planes stored
+    // above: K7 marks it dead, every reader masks by K7 (k_read_records,
+    // k_add_targets resets all planes) and the next round's store zeroes them
   }
-  const uint32_t emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died);
+  const uint32_t emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates);
 
   constexpr uint32_t plane_bytes = WARM ? 2u * 17u * 4u : 2u * kPlanes * 4u;
   constexpr uint32_t lane_bytes = plane_bytes + (REPLAY ? 8u : 4u) * K + 4u;
   acc.applied += applied;
   acc.died += (uint32_t)__popc(died);
   acc.lane_bytes += active ? lane_bytes + extra_bytes : 0u;
-  acc.emitted += emitted;
+  acc.emitted_bytes += emitted;
 }
 
 // MODE: kModeWarm (sim, every consider plane all-ones), kModeCheck (sim, per
@@ -305,12 +294,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   // walk <= 16 tiles per wave by default, 2^32 / (64 * 32 * 8) = 262k at most)
   const unsigned long long s = wave_sum(acc.applied);
   const unsigned long long f = __ballot(acc.died != 0u) ? wave_sum(acc.died) : 0ull;
-  const unsigned long long by = (unsigned long long)wave_sum(acc.lane_bytes) + 8ull * acc.emitted;
+  const unsigned long long by = (unsigned long long)wave_sum(acc.lane_bytes) + acc.emitted_bytes;
   if (lane == 0) {
     const uint32_t shard = wave0 % p.log_shards;
     if (s) atomicAdd(&p.applied[shard], s);
     if (f) atomicAdd(&p.finalized[shard], f);
     if (by) atomicAdd(&p.bytes[shard], by);
+    if (acc.updates) atomicAdd(&p.upd_count[shard], acc.updates);
   }
 }
 

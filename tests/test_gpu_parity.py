@@ -309,6 +309,22 @@ def test_node_shard_needs_comm():
 
 
 # ------------------------------------------------------------------ full-size properties
+def dense_words(k):  # kernels.h dense_words: u64 words of a dense lane record
+    return (k + 5) // 2
+
+
+def emitted_bytes(u, k=8):
+    """Log bytes the round kernels write for decoded updates `u`: a (round,
+    node, 32-target block) with >= dense_words(k) updates is one dense record
+    of dense_words(k) u64 words; other updates are 8-B single words."""
+    if len(u) == 0:
+        return 0
+    key = np.stack([u[:, 0], u[:, 1], u[:, 3] // 32], axis=1)
+    _, counts = np.unique(key, axis=0, return_counts=True)
+    dw = dense_words(k)
+    return int(np.where(counts >= dw, 8 * dw, 8 * counts).sum())
+
+
 def test_c4_shape_properties():
     """C4 shape at 1/10 scale (100k nodes x 1000 targets, k=8, Bernoulli(0.8)):
     rounds 0-15 keep every record live (finalization needs >= 134 votes), so
@@ -322,12 +338,14 @@ def test_c4_shape_properties():
         e.init_records(avhip.INIT_BERNOULLI, P80)
         lanes = e.layout_info()["lanes"]
         e.run_rounds(1)  # round 0: consider planes fill up (236 B per 32-record lane)
-        assert e.alg_bytes() == lanes * 236 + 8 * e.updates_count()
-        b1, u1 = e.alg_bytes(), e.updates_count()
+        b1 = e.alg_bytes()
         e.run_rounds(15)  # warm: the all-ones consider planes are skipped (176 / 172 B per lane)
-        assert e.alg_bytes() - b1 == 15 * lanes * warm_lane_bytes + 8 * (e.updates_count() - u1)
+        b16 = e.alg_bytes()
         assert e.applied_votes() == n * m * k * 16
         u = e.fetch_updates()
+        r0 = u[:, 0] == 0
+        assert b1 == lanes * 236 + emitted_bytes(u[r0])
+        assert b16 - b1 == 15 * lanes * warm_lane_bytes + emitted_bytes(u[~r0])
         assert not np.isin(u[:, 4], [avhip.STATUS_FINALIZED, avhip.STATUS_INVALID]).any()
         recs = e.read_records(0, n, 0, m)
         assert ((recs >> 17) < 128).all()

@@ -68,6 +68,12 @@ for s in "$@"; do
             python3 tools/ab_tune.py --shards 8 --variants sweep_w1,ablate --rounds 3 ;;
     pmc_sq1) step pmc_sq1 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq1 -o ab -- \
             python3 tools/ab_tune.py --shards 1 --variants sweep_w1 --rounds 3 ;;
+    pmc_conv_sq) step pmc_conv_sq 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_conv_sq -o conv -- \
+            python3 tools/run_to_finalization.py --workload c4 --max-rounds 20 ;;
+    pmc_conv_wr) step pmc_conv_wr 300 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_conv_wr -o conv -- \
+            python3 tools/run_to_finalization.py --workload c4 --max-rounds 20 ;;
+    pmc_conv_rd) step pmc_conv_rd 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_conv_rd -o conv -- \
+            python3 tools/run_to_finalization.py --workload c4 --max-rounds 20 ;;
     gaps) step gaps 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps -o gap -- python3 tools/gap_probe.py --workload c4 ;;
     gaps2) step gaps2 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps2 -o gap -- python3 tools/gap_probe.py --workload c2 ;;
     profc2) step profc2 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc2 -o c2 -- \
