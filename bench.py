@@ -127,17 +127,26 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(world, rank, obj[0])
     if replay:  # both passes' rounds (the roofline pass re-runs warmup + steps)
-        eng.replay_prepare(2 * (warmup + steps))
+        eng.replay_prepare(3 * (warmup + steps))
     run = eng.replay_rounds if replay else eng.run_rounds
     info = eng.layout_info()
 
-    # ---- warmup (untimed), then drain the StatusUpdate log
+    # ---- device warm-up (untimed): after process start the GPU runs these
+    # kernels up to ~15 % slower for the first ~20-30 ms of sustained load,
+    # whatever the launch pattern (tools/gap_probe.py --events-first, DESIGN.md
+    # §4); one untimed pass of the same rounds, then the records start over
+    run(warmup + steps)
+    eng.synchronize()
+    eng.discard_updates()
+    eng.init_records(init_mode, init_param)
+
+    # ---- warmup (untimed), then empty the StatusUpdate log. Discarded on the
+    # device, not fetched: sorting round 0-1's ~10^8 updates on the host took
+    # ~4.7 s, long enough for the idle GPU to lose the warm-up above (the timed
+    # rounds then ran at 0.70-0.82 ms instead of 0.65; profiles/r01 trace)
     run(warmup)
     eng.synchronize()
-    try:  # drain what the warmup emitted (the timed region starts with an empty log)
-        eng.fetch_updates(decode=False)
-    except avhip.LogOverflow:
-        pass  # the log is cleared on overflow; warmup updates are not measured
+    eng.discard_updates()
     applied0 = eng.applied_votes()
 
     # ---- timed region (no per-launch events: their queue packets add ~10 us between kernels)
@@ -184,8 +193,9 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         elapsed, applied, emitted = float(tmax), float(tot[0]), float(tot[1])
     value = applied / elapsed
     # roofline of this rank's round kernel: algorithmic bytes per
-    # launch (236 B per 32-record lane at k=8, 176 B once the consider planes
-    # are warm, + 8 B per StatusUpdate) / its HIP-event average launch time.
+    # launch as counted by the kernel (per 32-record lane at k=8: 236 B cold,
+    # 172 B warm, 136 B with recomputed vote registers; + the StatusUpdate log)
+    # / its HIP-event average launch time.
     achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
     gen2 = k <= 8 and args.kernel != 1
     kname = (("k_round_node" if gen2 else "k_round_capped") if info["capped"]
@@ -270,6 +280,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "device_warmup_rounds": args.warmup + args.steps,
             "ms_per_step": r["elapsed"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong",

@@ -61,8 +61,20 @@ struct av_engine {
   bool capped = false;
   hipStream_t stream = nullptr;
   uint32_t* planes = nullptr;
-  uint32_t* pref[2] = {nullptr, nullptr};
+  // published-preference snapshots, rotated by 3: round r reads pref[cur]
+  // (S_r) and writes pref[nxt(cur)] (S_r+1); pref[prv(cur)] (S_r-1) is kept
+  // for tiles whose vote planes are recomputed (vstale)
+  uint32_t* pref[3] = {nullptr, nullptr, nullptr};
   int cur = 0;
+  static int nxt(int c) { return c == 2 ? 0 : c + 1; }
+  static int prv(int c) { return c == 0 ? 2 : c - 1; }
+  // recomputed vote registers (kernels.h vv): option "virtual_votes" and the
+  // smallest BL it is used at (option "vv_min_bl": below it the 7 extra
+  // gathered rows cost more requests than the 64 B per lane of V planes save)
+  uint32_t* vstale = nullptr;  // [tiles]
+  bool v_stale = false;        // some tile may be stale
+  bool virtual_votes = true;
+  uint32_t vv_min_bl = 16;
   uint32_t* valid = nullptr;
   uint32_t* byz = nullptr;
   uint64_t* log = nullptr;
@@ -106,6 +118,8 @@ struct av_engine {
   int64_t replay_cap_rounds = 0, replay_first = 0, replay_ready = 0;
   // timing
   bool timing = false;
+  bool round_marker = false;  // option "round_marker" (diagnostics)
+  hipEvent_t marker = nullptr;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
@@ -151,15 +165,13 @@ struct Scratch {
   }
 };
 
-int launch_one_round(av_engine* e, const uint32_t* replay) {
-  AV_CHECK(e->round - e->log_base < 4096, AV_ERR_OVERFLOW,
-           "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
-  AV_CHECK(e->NL == (uint32_t)e->N || e->comm != nullptr || e->N == e->n1 - e->n0, AV_ERR_UNSUPPORTED,
-           "node-sharded engine needs av_comm_init before running rounds");
+avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   avk::RoundParams p{};
   p.planes = e->planes;
   p.pref_in = e->pref[e->cur];
-  p.pref_out = e->pref[e->cur ^ 1];
+  p.pref_out = e->pref[av_engine::nxt(e->cur)];
+  p.pref_prev = e->pref[av_engine::prv(e->cur)];
+  p.vstale = e->vstale;
   p.valid = e->valid;
   p.byz = e->byz;
   p.replay = replay;
@@ -195,7 +207,35 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   p.bl_magic = e->bl_magic;
   p.bl_sh1 = e->bl_sh1;
   p.bl_sh2 = e->bl_sh2;
+  return p;
+}
+
+// Write back the vote planes of tiles the last warm k = 8 sim round left
+// stale (kernels.h vv); every path that reads or writes records other than
+// such a round calls this first.
+int materialize_votes(av_engine* e) {
+  if (!e->v_stale) return AV_OK;
+  AV_HIP(avk::launch_vv_materialize(round_params(e, nullptr), e->stream));
+  e->v_stale = false;
+  return AV_OK;
+}
+
+int launch_one_round(av_engine* e, const uint32_t* replay) {
+  AV_CHECK(e->round - e->log_base < 4096, AV_ERR_OVERFLOW,
+           "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
+  AV_CHECK(e->NL == (uint32_t)e->N || e->comm != nullptr || e->N == e->n1 - e->n0, AV_ERR_UNSUPPORTED,
+           "node-sharded engine needs av_comm_init before running rounds");
+  avk::RoundParams p = round_params(e, replay);
   const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped;
+  // vote planes may be left unstored: the sweep's warm sim modes at k = 8 (launch_sweep_k)
+  const bool vv = e->virtual_votes && sweep && e->k == 8 && !replay && e->c_monotone && e->warm_all &&
+                  !e->ablate_gather && e->BL >= e->vv_min_bl;
+  if (!vv) {
+    int rc = materialize_votes(e);
+    if (rc != AV_OK) return rc;
+  }
+  p.vv = vv ? 1u : 0u;
+  if (vv) e->v_stale = true;
   bool all_valid = true;
   for (uint32_t b = 0; b < e->BL; ++b) {
     const int64_t tb = e->t0 + 32ll * b;
@@ -224,14 +264,17 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   if (e->timing) {
     AV_HIP(hipEventRecord(ev1, e->stream));
     e->events.emplace_back(ev0, ev1);
+  } else if (e->round_marker) {  // diagnostics: a timing-free event after every round
+    if (!e->marker) AV_HIP(hipEventCreateWithFlags(&e->marker, hipEventDisableTiming));
+    AV_HIP(hipEventRecord(e->marker, e->stream));
   }
   if (e->comm) {
     const size_t count = (size_t)e->NL * e->BL;
-    uint32_t* out = e->pref[e->cur ^ 1];
+    uint32_t* out = e->pref[av_engine::nxt(e->cur)];
     ncclResult_t r = ncclAllGather(out + (size_t)e->n0 * e->BL, out, count, ncclUint32, e->comm, e->stream);
     AV_CHECK(r == ncclSuccess, AV_ERR_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
   }
-  e->cur ^= 1;
+  e->cur = av_engine::nxt(e->cur);
   e->round++;
   return AV_OK;
 }
@@ -295,7 +338,8 @@ int av_destroy(av_engine* e) {
     (void)hipEventDestroy(ev.second);
   }
   if (e->comm) (void)ncclCommDestroy(e->comm);
-  void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
+  if (e->marker) (void)hipEventDestroy(e->marker);
+  void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->dlog, e->dlog_count, e->upd_count,
                   e->applied, e->bytes, e->finalized, e->scratch_count, e->replay};
   for (void* b : bufs)
@@ -368,6 +412,9 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->planes, plane_words)) != hipSuccess) return hip_fail(he, "alloc planes");
   if ((he = dev_alloc(&e->pref[0], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->pref[1], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
+  if ((he = dev_alloc(&e->pref[2], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
+  if ((he = dev_alloc(&e->vstale, e->Lpad / 64)) != hipSuccess) return hip_fail(he, "alloc planes");
+  (void)hipMemsetAsync(e->vstale, 0, (size_t)(e->Lpad / 64) * 4, e->stream);
   if ((he = dev_alloc(&e->valid, e->BL)) != hipSuccess) return hip_fail(he, "alloc valid");
   if ((he = dev_alloc(&e->byz, (e->N + 31) / 32)) != hipSuccess) return hip_fail(he, "alloc byz");
   if ((he = dev_alloc(&e->log, (size_t)e->log_cap * e->log_shards)) != hipSuccess) return hip_fail(he, "alloc log");
@@ -396,6 +443,7 @@ int av_create(const av_config* cfg, av_engine** out) {
   (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
   (void)hipMemsetAsync(e->applied, 0, avk::kLogShards * 8, e->stream);
   (void)hipMemsetAsync(e->pref[1], 0, pref_words * 4, e->stream);
+  (void)hipMemsetAsync(e->pref[2], 0, pref_words * 4, e->stream);
   // every real target starts valid
   e->valid_host.assign(e->BL, 0u);
   for (uint32_t b = 0; b < e->BL; ++b) {
@@ -423,6 +471,10 @@ int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
   AV_ENTER(e);
   e->warm_all = false;
   e->count_bound = 0;  // every record starts at count 0 (NewVoteRecord, vote.go:33-35)
+  if (e->v_stale) {  // every plane is rewritten
+    AV_HIP(hipMemsetAsync(e->vstale, 0, (size_t)(e->Lpad / 64) * 4, e->stream));
+    e->v_stale = false;
+  }
   AV_CHECK(init_mode >= AV_INIT_NONE && init_mode <= AV_INIT_PAIRS, AV_ERR_INVALID_ARG, "bad init_mode");
   avk::InitParams p{};
   p.planes = e->planes;
@@ -453,6 +505,8 @@ int av_set_valid(av_engine* e, int64_t target, int32_t valid) {
   AV_ENTER(e);
   AV_CHECK(target >= 0 && target < e->M, AV_ERR_INVALID_ARG, "target out of range");
   if (!local_target(e, target)) return AV_OK;
+  int rc = materialize_votes(e);  // stale tiles must not gain live-but-invalid records
+  if (rc != AV_OK) return rc;
   const int64_t tl = target - e->t0;
   const uint32_t b = (uint32_t)(tl >> 5), m = 1u << (tl & 31);
   e->valid_host[b] = valid ? (e->valid_host[b] | m) : (e->valid_host[b] & ~m);
@@ -466,6 +520,10 @@ int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uin
   AV_ENTER(e);
   AV_CHECK(n >= 0 && (n == 0 || (targets && accepted && added)), AV_ERR_INVALID_ARG, "null argument");
   AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
+  {
+    int rc = materialize_votes(e);
+    if (rc != AV_OK) return rc;
+  }
   e->warm_all = false;
   std::vector<uint32_t> tl;
   std::vector<uint8_t> acc;
@@ -512,6 +570,10 @@ int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const 
   AV_ENTER(e);
   AV_CHECK(n >= 0 && (n == 0 || (targets && errs && status_out)), AV_ERR_INVALID_ARG, "null argument");
   AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
+  {
+    int rc = materialize_votes(e);
+    if (rc != AV_OK) return rc;
+  }
   for (int64_t i = 0; i < n; ++i) status_out[i] = -1;
   e->count_bound = std::min<int64_t>(127, e->count_bound + n);  // at most one step per vote
   // group votes by block, keeping Response order inside each block
@@ -583,6 +645,10 @@ int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1
   AV_ENTER(e);
   AV_CHECK(out && n0 >= e->n0 && n0 <= n1 && n1 <= e->n1 && t0 >= e->t0 && t0 <= t1 && t1 <= e->t1,
            AV_ERR_INVALID_ARG, "range outside this engine's shard");
+  {
+    int rc = materialize_votes(e);
+    if (rc != AV_OK) return rc;
+  }
   const size_t n = (size_t)(n1 - n0) * (size_t)(t1 - t0);
   if (!n) return AV_OK;
   Scratch s;
@@ -599,6 +665,10 @@ int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t
   AV_ENTER(e);
   AV_CHECK(in && n0 >= e->n0 && n0 <= n1 && n1 <= e->n1 && t0 >= e->t0 && t0 <= t1 && t1 <= e->t1,
            AV_ERR_INVALID_ARG, "range outside this engine's shard");
+  {
+    int rc = materialize_votes(e);
+    if (rc != AV_OK) return rc;
+  }
   const size_t n = (size_t)(n1 - n0) * (size_t)(t1 - t0);
   if (!n) return AV_OK;
   e->c_monotone = false;
@@ -996,6 +1066,13 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     } else {
       e->sweep_blocks = (uint32_t)value;
     }
+  } else if (n == "round_marker") {
+    e->round_marker = value != 0;
+  } else if (n == "virtual_votes") {  // 0: always store the vote planes (A/B)
+    e->virtual_votes = value != 0;
+  } else if (n == "vv_min_bl") {
+    AV_CHECK(value >= 1 && value < (1ll << 31), AV_ERR_INVALID_ARG, "bad vv_min_bl");
+    e->vv_min_bl = (uint32_t)value;
   } else if (n == "warm_skip") {  // may only be switched off (it is a proven invariant, not a hint)
     if (!value) e->c_monotone = false;
   } else {

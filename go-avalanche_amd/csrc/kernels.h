@@ -69,6 +69,13 @@ struct RoundParams {
   uint32_t warm_all;         // every consider plane of every lane is all-ones (no per-tile check)
   uint32_t store_policy;     // 0/1: per plane_nt; 2: sc1 plane/pref stores; 3: nt sc1 (k = 8)
   uint32_t bl_magic, bl_sh1, bl_sh2;  // n / BL = (t + ((n - t) >> sh1)) >> sh2, t = mulhi(n, magic)
+  // Recomputed vote registers (k = 8, warm sim rounds): after a
+  // round of 8 sim votes a record's vote register is exactly that round's 8
+  // gathered words, so a tile may skip storing its V planes and the next
+  // round regathers them from the previous snapshot instead of reading them.
+  uint32_t vv;               // this round may leave V planes unstored (vstale)
+  uint32_t* vstale;          // [tiles] 1: the tile's V planes are stale; V = votes of round - 1
+  const uint32_t* pref_prev; // [N_pad][BL] snapshot of round - 1 (read by stale tiles)
 };
 
 // Division by the (runtime) block count BL without a hardware divide:
@@ -110,6 +117,9 @@ hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t
 hipError_t launch_round_node(const RoundParams& p, int k, bool replay, bool exact_pass, hipStream_t s);
 // Resident 256-thread workgroups per CU for the sweep kernel and the CU count.
 hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cus);
+// Write back the V planes of stale tiles (p.vstale, p.pref_prev, p.round = the
+// round after the one that left them stale); k = 8 only.
+hipError_t launch_vv_materialize(const RoundParams& p, hipStream_t s);
 
 struct InitParams {
   uint32_t* planes;

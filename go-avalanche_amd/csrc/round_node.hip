@@ -86,7 +86,7 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
     }
   } else {
     uint32_t peers[K];
-    draw_peers<K>(p, node, nl, nl, 1u, lane, peers);  // every lane of the workgroup is the same node
+    draw_peers<K>(p, p.round, node, nl, nl, 1u, lane, peers);  // every lane of the workgroup is the same node
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const uint32_t w = p.pref_in[peers[j] * p.BL + bc];  // < N * BL < 2^31 (engine check)

@@ -169,8 +169,8 @@ __device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, uint32_t* q, uint3
 // N - 1 <= k, more than 64 / NB nodes in the wave, a repeated candidate) take
 // the general draw.
 template <int K>
-__device__ __forceinline__ void draw_peers(const RoundParams& p, uint32_t node, uint32_t nl, uint32_t nlA, uint32_t nn,
-                                           uint32_t lane, uint32_t (&peers)[K]) {
+__device__ __forceinline__ void draw_peers(const RoundParams& p, uint32_t round, uint32_t node, uint32_t nl,
+                                           uint32_t nlA, uint32_t nn, uint32_t lane, uint32_t (&peers)[K]) {
   const uint32_t others = p.n_nodes - 1u;
   constexpr uint32_t NB = (K + 3) / 4;
   bool general = p.peer_mode == 1 || (uint32_t)K >= others || nn * NB > 64u;
@@ -179,7 +179,7 @@ __device__ __forceinline__ void draw_peers(const RoundParams& p, uint32_t node, 
     const uint32_t q = lane;
     const uint32_t pnode = p.n0 + nlA + min(q / NB, nn - 1u);
     uint32_t x[4];
-    philox(x, p.seed, pnode, p.round, q % NB, kDomPeers);
+    philox(x, p.seed, pnode, round, q % NB, kDomPeers);
     uint32_t prod[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -198,7 +198,7 @@ __device__ __forceinline__ void draw_peers(const RoundParams& p, uint32_t node, 
     general = !distinct;
   }
   if (general) {
-    const PeerList<K> r = sample_peers_general<K>(p.seed, node, p.round, p.n_nodes, p.peer_mode);
+    const PeerList<K> r = sample_peers_general<K>(p.seed, node, round, p.n_nodes, p.peer_mode);
 #pragma unroll
     for (int j = 0; j < K; ++j) peers[j] = r.v[j];
   }

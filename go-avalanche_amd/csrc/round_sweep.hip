@@ -55,6 +55,7 @@ template <int K, bool REPLAY, bool WARM>
 struct TileIn {
   u32x4 v0, v1, k0, k1;
   uint32_t A, vmask, byzw;
+  uint32_t stale;                // wave-uniform: V planes stale, v0/v1 regathered (kernels.h vstale)
   uint32_t C[WARM ? 1 : 8];
   uint32_t w[K];                 // yes bits: err == 0 (vote.go:55)
   uint32_t cw[REPLAY ? K : 1];   // consider bits: int32(err) >= 0 (vote.go:56); sim votes: all-ones
@@ -76,14 +77,18 @@ __device__ __forceinline__ LaneIdx lane_idx(const RoundParams& p, uint32_t tile,
   return x;
 }
 
-template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE>
+template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE, bool VVM = false>
 __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
                                           TileIn<K, REPLAY, WARM>& in) {
   const LaneIdx x = lane_idx(p, tile, lane);
   const uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
   const u32x4* const grp = reinterpret_cast<const u32x4*>(tp) + lane;
-  in.v0 = ld4<POL>(grp);
-  in.v1 = ld4<POL>(grp + 64);
+  constexpr bool VV = VVM && WARM && !REPLAY && K == 8;  // VVM: the warm sim modes only
+  in.stale = VV && p.vv ? uni(p.vstale[tile]) : 0u;
+  if (!in.stale) {
+    in.v0 = ld4<POL>(grp);
+    in.v1 = ld4<POL>(grp + 64);
+  }
   in.k0 = ld4<POL>(grp + 128);
   in.k1 = ld4<POL>(grp + 192);
   in.A = ld1<POL>(tp + 1536u + lane);
@@ -100,9 +105,22 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
       in.w[j] = p.replay[(size_t)(2 * j) * p.Lpad + x.gc];
     }
   } else {
+    const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
+    if constexpr (VV) {
+      if (in.stale) {
+        // the vote register after last round's 8 sim votes is those votes:
+        // V_i = (previous round's slot 7 - i vote); V_7 is never read at k = 8
+        uint32_t pp[K];
+        draw_peers<K>(p, p.round - 1u, x.node, x.nl, nlA, nn, lane, pp);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) in.v0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) in.v1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
+        in.v1[3] = 0u;
+      }
+    }
     uint32_t peers[K];
-    draw_peers<K>(p, x.node, x.nl, uni(x.nl), (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - uni(x.nl) + 1u,
-                  lane, peers);
+    draw_peers<K>(p, p.round, x.node, x.nl, nlA, nn, lane, peers);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       // ABLATE (timing diagnostics only, results invalid): the node's own row, coalesced
@@ -114,7 +132,7 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
 
 // The round step of one loaded tile. WARM: consider planes all-ones (neither
 // loaded nor stored; sim votes only). POL: plane-stream cache policy.
-template <int K, bool REPLAY, bool WARM, int POL>
+template <int K, bool REPLAY, bool WARM, int POL, bool VVM = false>
 __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
                                              const TileIn<K, REPLAY, WARM>& in, uint32_t extra_bytes, SweepAcc& acc) {
   const LaneIdx x = lane_idx(p, tile, lane);
@@ -155,7 +173,11 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   // ---- the shift-register planes after K votes are final for every record
   // that survives the round: store them now (a record deleted this round is
   // rewritten below)
-  if (active) {
+  // a warm sim wave with no live-but-invalid record leaves its V planes
+  // unstored: next round (or av materialize) regathers them (kernels.h vv)
+  bool virt = false;
+  if constexpr (VVM && WARM && !REPLAY && K == 8) virt = p.vv && __ballot(keep != 0u) == 0ull;
+  if (active && !virt) {
     const uint32_t dead0 = ~(P0 | keep);
     u32x4 o0, o1;
 #pragma unroll
@@ -223,13 +245,17 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
   }
+  if constexpr (VVM && WARM && !REPLAY && K == 8) {
+    if (p.vv && lane == 0 && virt != (in.stale != 0u)) p.vstale[tile] = virt ? 1u : 0u;
+  }
   const uint32_t emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates);
 
   constexpr uint32_t plane_bytes = WARM ? 2u * 17u * 4u : 2u * kPlanes * 4u;
   constexpr uint32_t lane_bytes = plane_bytes + (REPLAY ? 8u : 4u) * K + 4u;
   acc.applied += applied;
   acc.died += (uint32_t)__popc(died);
-  acc.lane_bytes += active ? lane_bytes + extra_bytes : 0u;
+  // stale: 7 regathered words instead of the 8 V planes read; virt: V planes not written
+  acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale ? 4u : 0u) - (virt ? 32u : 0u) : 0u;
   acc.emitted_bytes += emitted;
 }
 
@@ -240,7 +266,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
 // (kModeWarm for a resident grid: the next tile's loads are issued before the
 // current tile is computed; 93 VGPRs, 5 waves per SIMD).
 template <int K, int MODE, int POL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeReplay ? 6 : 7))) void k_round_sweep(const RoundParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeReplay || MODE == kModeWarm ? 6 : 7))) void k_round_sweep(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave0 = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * 4u;
@@ -251,11 +277,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     // are in flight while tile t is computed
     TileIn<K, false, true> cur, nxt;
     uint32_t tile = wave0;
-    if (tile < tiles) load_tile<K, false, true, POL, false>(p, tile, lane, cur);
+    if (tile < tiles) load_tile<K, false, true, POL, false, true>(p, tile, lane, cur);
     for (; tile < tiles; tile += nwaves) {
       const uint32_t next = tile + nwaves;
-      if (next < tiles) load_tile<K, false, true, POL, false>(p, next, lane, nxt);
-      process_tile<K, false, true, POL>(p, tile, lane, cur, 0u, acc);
+      if (next < tiles) load_tile<K, false, true, POL, false, true>(p, next, lane, nxt);
+      process_tile<K, false, true, POL, true>(p, tile, lane, cur, 0u, acc);
       cur = nxt;
     }
   } else {
@@ -263,8 +289,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
       constexpr bool AB = MODE == kModeAblate;
       if constexpr (MODE == kModeWarm) {
         TileIn<K, false, true> in;
-        load_tile<K, false, true, POL, false>(p, tile, lane, in);
-        process_tile<K, false, true, POL>(p, tile, lane, in, 0u, acc);
+        load_tile<K, false, true, POL, false, true>(p, tile, lane, in);
+        process_tile<K, false, true, POL, true>(p, tile, lane, in, 0u, acc);
       } else if constexpr (MODE == kModeReplay) {
         TileIn<K, true, false> in;
         load_tile<K, true, false, POL, false>(p, tile, lane, in);
@@ -333,6 +359,31 @@ hipError_t launch_sweep_k(const RoundParams& p, bool replay, uint32_t blocks, hi
   return launch_mode<K, kModeCheck>(p, grid, s);
 }
 
+// Materialize stale V planes (kernels.h vv) before anything other than a warm
+// k = 8 sim round reads or writes the records: the vote register of a stale
+// tile is the last round's 8 gathered votes, V_i = slot 7 - i.
+__global__ __launch_bounds__(256) void k_vv_materialize(const RoundParams p) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t tile = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
+  if (tile >= (p.Lpad >> 6) || uni(p.vstale[tile]) == 0u) return;
+  const LaneIdx x = lane_idx(p, tile, lane);
+  const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
+  uint32_t pp[8];
+  draw_peers<8>(p, p.round - 1u, x.node, x.nl, nlA, nn, lane, pp);
+  u32x4 o0, o1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
+    o1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
+  }
+  if (x.active) {
+    u32x4* const grp = reinterpret_cast<u32x4*>(p.planes + (size_t)tile * (kPlanes * 64u)) + lane;
+    grp[0] = o0;
+    grp[64] = o1;
+  }
+  if (lane == 0) p.vstale[tile] = 0u;
+}
+
 template <int K>
 hipError_t occupancy_k(bool replay, int* bpc) {
   return replay ? hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, k_round_sweep<K, kModeReplay, 1>, 256, 0)
@@ -358,6 +409,13 @@ hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t
 #define AVK_SW(K) launch_sweep_k<K>(p, replay, blocks, s)
   AVK_SWEEP_SWITCH(k, AVK_SW)
 #undef AVK_SW
+}
+
+hipError_t launch_vv_materialize(const RoundParams& p, hipStream_t s) {
+  if (!p.vstale || !p.pref_prev) return hipErrorInvalidValue;
+  const uint32_t tiles = p.Lpad / 64u;
+  hipLaunchKernelGGL(k_vv_materialize, dim3((tiles + 3u) / 4u), dim3(256), 0, s, p);
+  return hipGetLastError();
 }
 
 hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cus) {

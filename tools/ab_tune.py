@@ -36,6 +36,8 @@ VARIANTS = {
     "w1_ntsc1": dict(kernel=2, sweep_blocks=0, store_policy=3),
     "res_sc1": dict(kernel=2, sweep_blocks=-2, store_policy=2),
     "w1_plain": dict(kernel=2, sweep_blocks=0, plane_nt=0),
+    "vv0": dict(kernel=2, virtual_votes=0),
+    "vv_all": dict(kernel=2, vv_min_bl=1),
 }
 
 
@@ -70,7 +72,7 @@ def main():
             opts = VARIANTS[v]
             e.set_option("kernel", opts["kernel"])
             e.set_option("ablate_gather", opts.get("ablate_gather", 0))
-            for opt in ("sweep_blocks", "store_policy", "plane_nt"):
+            for opt in ("sweep_blocks", "store_policy", "plane_nt", "virtual_votes", "vv_min_bl"):
                 if opt in opts:
                     e.set_option(opt, opts[opt])
             e.init_records(init_mode, init_param)

@@ -21,10 +21,15 @@ from bench import WORKLOADS  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--workload", default="c4")
 ap.add_argument("--rounds", type=int, default=12)
+ap.add_argument("--events-first", action="store_true", help="run the evented pass first")
+ap.add_argument("--option", action="append", default=[], help="engine option name=value (repeatable)")
 a = ap.parse_args()
 n, m, k, mode, param, byz, replay, _ = WORKLOADS[a.workload]
-for timing in (False, True):
+for timing in ((True, False) if a.events_first else (False, True)):
     e = avhip.Engine(n, m, k=k, byz_threshold=byz, log_capacity=1 << 26)
+    for o in a.option:
+        name, val = o.split("=")
+        e.set_option(name, int(val))
     e.init_records(mode, param)
     if replay:
         e.replay_prepare(a.rounds + 2)

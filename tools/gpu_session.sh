@@ -41,6 +41,7 @@ for s in "$@"; do
     abc3) step abc3 600 python tools/ab_tune.py --workload c3 --shards 1 --variants sweep,per_tile,ablate --json $OUT/abc3.json ;;
     abpol) step abpol 600 python tools/ab_tune.py --shards 1,8 --variants sweep_w1,sweep_res,w1_sc1,w1_ntsc1,res_sc1,w1_plain --json $OUT/abpol.json ;;
     abres) step abres 600 python tools/ab_tune.py --shards 1,2,4,8 --variants sweep,sweep_w1,sweep_res,ablate --json $OUT/abres.json ;;
+    abvv) step abvv 600 python tools/ab_tune.py --shards 1,2,4,8 --variants vv0,sweep,vv_all --json $OUT/abvv.json ;;
     gprobe) step gprobe 120 go-avalanche_amd/bin/gather_probe 20 ;;
     mprobe) step mprobe 120 go-avalanche_amd/bin/mix_probe ;;
     conv_c3) step conv_c3 900 python tools/run_to_finalization.py --workload c3 --json $OUT/conv_c3.json ;;
@@ -61,7 +62,7 @@ for s in "$@"; do
     calib_write) step calib_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/calib_write -o calib -- \
             go-avalanche_amd/bin/pmc_calib ;;
     pmc_sum) step pmc_sum 120 python tools/pmc_summary.py --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write \
-            --fetch $OUT/pmc_fetch --write $OUT/pmc_write --kernel k_round_sweep --read-x1 36 --out $OUT/pmc_traffic_c4.json ;;
+            --fetch $OUT/pmc_fetch --write $OUT/pmc_write --kernel k_round_sweep --read-x4 32 --read-x1 64 --write-x4 32 --write-x1 8 --out $OUT/pmc_traffic_c4.json ;;
     pmc_sq8) step pmc_sq8 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq8 -o ab -- \
             python3 tools/ab_tune.py --shards 8 --variants sweep_w1,ablate --rounds 3 ;;
     pmc_tcc8) step pmc_tcc8 300 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_tcc8 -o ab -- \
@@ -75,6 +76,10 @@ for s in "$@"; do
     pmc_conv_rd) step pmc_conv_rd 300 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_conv_rd -o conv -- \
             python3 tools/run_to_finalization.py --workload c4 --max-rounds 20 ;;
     gaps) step gaps 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps -o gap -- python3 tools/gap_probe.py --workload c4 ;;
+    gaps_vv0) step gaps_vv0 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps_vv0 -o gap -- python3 tools/gap_probe.py --workload c4 --option virtual_votes=0 ;;
+    gaps40) step gaps40 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps40 -o gap -- python3 tools/gap_probe.py --workload c4 --rounds 40 ;;
+    gaps_mk) step gaps_mk 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps_mk -o gap -- python3 tools/gap_probe.py --workload c4 --option round_marker=1 ;;
+    gaps_ef) step gaps_ef 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps_ef -o gap -- python3 tools/gap_probe.py --workload c4 --events-first ;;
     gaps2) step gaps2 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps2 -o gap -- python3 tools/gap_probe.py --workload c2 ;;
     profc2) step profc2 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc2 -o c2 -- \
             python3 bench.py --workload c2 --no-cpu-baseline ;;
