@@ -98,6 +98,9 @@ struct av_engine {
   bool c_monotone = true;
   bool plane_nt = true;  // tuning option "plane_nt" (A/B on MI355X: -8 % kernel time warm, -16 % cold)
   bool ablate_gather = false;  // diagnostics option "ablate_gather" (invalid results)
+  // diagnostics option "unsynced_shard": a node-sharded engine runs rounds with no exchange (other
+  // shards' preference rows keep their initial values; per-rank kernel timing only, invalid results)
+  bool unsynced_shard = false;
   // round kernels (option "kernel"): 2 = k_round_sweep (uncapped) / k_round_node (capped), k <= 8;
   // 1 = k_round_fast / k_round_capped (the first versions; any k, A/B baseline)
   int kernel = 2;
@@ -126,6 +129,17 @@ struct av_engine {
   // RCCL
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
+  // peer-push exchange (av_peer_init): every rank's three
+  // snapshot buffers and arrival slots mapped into this process over IPC
+  int peer_world = 0, peer_rank = 0;
+  uint32_t* peer_pref[3][avk::kMaxPeers + 1] = {};  // [buffer][rank]; own rank = the local buffer
+  uint32_t* arrive = nullptr;                        // [kMaxPeers + 1] arrival slots (local)
+  uint32_t* barrier_err = nullptr;
+  uint32_t barrier_seq = 0;
+  uint32_t barrier_timeout_ms = 30000;
+  std::vector<void*> peer_opened;                    // IPC mappings to close
+  avk::PeerPtrs peer_arrive{};
+  uint32_t** push_tbl = nullptr;                     // device [3][kMaxPeers]: peers' replicas of each buffer
 
   size_t round_replay_words() const { return (size_t)k * 2 * Lpad; }
 };
@@ -220,10 +234,39 @@ int materialize_votes(av_engine* e) {
   return AV_OK;
 }
 
+// Peer-push exchange: copy this rank's rows of snapshot buffer `b` into every
+// peer replica (a full resynchronisation of those rows).
+int push_own_rows(av_engine* e, int b) {
+  avk::PeerPtrs dst{};
+  uint32_t n = 0;
+  for (int r = 0; r < e->peer_world; ++r)
+    if (r != e->peer_rank) dst.p[n++] = e->peer_pref[b][r];
+  const uint64_t w0 = (uint64_t)e->n0 * e->BL, w1 = w0 + (uint64_t)e->NL * e->BL;
+  AV_HIP(avk::launch_push_rows(e->pref[b], dst, n, w0, w1, e->stream));
+  return AV_OK;
+}
+
+// Barrier across the peer ranks, on the engine stream (kernels.h).
+int peer_barrier(av_engine* e) {
+  AV_HIP(avk::launch_peer_barrier(e->peer_arrive, (uint32_t)e->peer_world, (uint32_t)e->peer_rank,
+                                  ++e->barrier_seq, e->barrier_err, e->barrier_timeout_ms, e->stream));
+  return AV_OK;
+}
+
+// Peer-push engines keep every replica of a snapshot buffer identical; a
+// write to this rank's rows outside a round would break that.
+int peer_local_write_check(const av_engine* e) {
+  AV_CHECK(e->peer_world <= 1, AV_ERR_UNSUPPORTED,
+           "record writes outside a round are not supported on a peer-push node-sharded engine");
+  return AV_OK;
+}
+
 int launch_one_round(av_engine* e, const uint32_t* replay) {
   AV_CHECK(e->round - e->log_base < 4096, AV_ERR_OVERFLOW,
            "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
-  AV_CHECK(e->NL == (uint32_t)e->N || e->comm != nullptr || e->N == e->n1 - e->n0, AV_ERR_UNSUPPORTED,
+  AV_CHECK(e->NL == (uint32_t)e->N || e->comm != nullptr || e->peer_world > 1 || e->N == e->n1 - e->n0 ||
+               e->unsynced_shard,
+           AV_ERR_UNSUPPORTED,
            "node-sharded engine needs av_comm_init before running rounds");
   avk::RoundParams p = round_params(e, replay);
   const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped;
@@ -241,6 +284,15 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     const int64_t tb = e->t0 + 32ll * b;
     const int64_t r = std::min<int64_t>(e->t1 - tb, 32);
     all_valid &= e->valid_host[b] == (r >= 32 ? ~0u : ((1u << r) - 1u));
+  }
+  // peer-push exchange: the sweep kernel's sim rounds push changed words; any
+  // other round is followed by a full push of this rank's rows (uniform across
+  // ranks: it depends only on the engine configuration and the call)
+  const bool peer = e->peer_world > 1;
+  const int nb = av_engine::nxt(e->cur);
+  if (peer && sweep && !replay) {
+    p.push_n = (uint32_t)e->peer_world - 1u;
+    p.push_dst = e->push_tbl + (size_t)nb * avk::kMaxPeers;
   }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (e->timing) {
@@ -267,6 +319,14 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   } else if (e->round_marker) {  // diagnostics: a timing-free event after every round
     if (!e->marker) AV_HIP(hipEventCreateWithFlags(&e->marker, hipEventDisableTiming));
     AV_HIP(hipEventRecord(e->marker, e->stream));
+  }
+  if (peer) {
+    if (!p.push_n) {
+      int rc = push_own_rows(e, nb);
+      if (rc != AV_OK) return rc;
+    }
+    int rc = peer_barrier(e);
+    if (rc != AV_OK) return rc;
   }
   if (e->comm) {
     const size_t count = (size_t)e->NL * e->BL;
@@ -338,6 +398,10 @@ int av_destroy(av_engine* e) {
     (void)hipEventDestroy(ev.second);
   }
   if (e->comm) (void)ncclCommDestroy(e->comm);
+  for (void* m : e->peer_opened) (void)hipIpcCloseMemHandle(m);
+  if (e->arrive) (void)hipFree(e->arrive);
+  if (e->barrier_err) (void)hipFree(e->barrier_err);
+  if (e->push_tbl) (void)hipFree(e->push_tbl);
   if (e->marker) (void)hipEventDestroy(e->marker);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->dlog, e->dlog_count, e->upd_count,
@@ -410,9 +474,11 @@ int av_create(const av_config* cfg, av_engine** out) {
   e->log_shards = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(waves, avk::kLogShards));
   e->log_cap = (uint32_t)std::max<int64_t>((cap + e->log_shards - 1) / e->log_shards, 64);
   if ((he = dev_alloc(&e->planes, plane_words)) != hipSuccess) return hip_fail(he, "alloc planes");
-  if ((he = dev_alloc(&e->pref[0], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
-  if ((he = dev_alloc(&e->pref[1], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
-  if ((he = dev_alloc(&e->pref[2], pref_words)) != hipSuccess) return hip_fail(he, "alloc pref");
+  // whole 2-MiB units: each snapshot buffer is an allocation of its own (IPC export, av_peer_handles)
+  const size_t pref_alloc = ((pref_words * 4 + (2u << 20) - 1) / (2u << 20)) * (2u << 20) / 4;
+  if ((he = dev_alloc(&e->pref[0], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
+  if ((he = dev_alloc(&e->pref[1], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
+  if ((he = dev_alloc(&e->pref[2], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->vstale, e->Lpad / 64)) != hipSuccess) return hip_fail(he, "alloc planes");
   (void)hipMemsetAsync(e->vstale, 0, (size_t)(e->Lpad / 64) * 4, e->stream);
   if ((he = dev_alloc(&e->valid, e->BL)) != hipSuccess) return hip_fail(he, "alloc valid");
@@ -518,6 +584,10 @@ int av_set_valid(av_engine* e, int64_t target, int32_t valid) {
 int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uint8_t* accepted, int64_t n,
                    uint8_t* added) {
   AV_ENTER(e);
+  {
+    int rc = peer_local_write_check(e);
+    if (rc != AV_OK) return rc;
+  }
   AV_CHECK(n >= 0 && (n == 0 || (targets && accepted && added)), AV_ERR_INVALID_ARG, "null argument");
   AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
   {
@@ -568,6 +638,10 @@ int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uin
 int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const uint32_t* errs, int64_t n,
                       int32_t* status_out) {
   AV_ENTER(e);
+  {
+    int rc = peer_local_write_check(e);
+    if (rc != AV_OK) return rc;
+  }
   AV_CHECK(n >= 0 && (n == 0 || (targets && errs && status_out)), AV_ERR_INVALID_ARG, "null argument");
   AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
   {
@@ -663,6 +737,10 @@ int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1
 
 int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, const uint32_t* in) {
   AV_ENTER(e);
+  {
+    int rc = peer_local_write_check(e);
+    if (rc != AV_OK) return rc;
+  }
   AV_CHECK(in && n0 >= e->n0 && n0 <= n1 && n1 <= e->n1 && t0 >= e->t0 && t0 <= t1 && t1 <= e->t1,
            AV_ERR_INVALID_ARG, "range outside this engine's shard");
   {
@@ -840,6 +918,11 @@ int av_replay_rounds(av_engine* e, int32_t rounds) {
 int av_synchronize(av_engine* e) {
   AV_ENTER(e);
   AV_HIP(hipStreamSynchronize(e->stream));
+  if (e->peer_world > 1) {
+    uint32_t err = 0;
+    AV_HIP(hipMemcpy(&err, e->barrier_err, 4, hipMemcpyDeviceToHost));
+    AV_CHECK(err == 0, AV_ERR_HIP, "peer barrier timed out (a rank stopped taking part in the rounds)");
+  }
   return AV_OK;
 }
 
@@ -1066,6 +1149,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     } else {
       e->sweep_blocks = (uint32_t)value;
     }
+  } else if (n == "unsynced_shard") {
+    e->unsynced_shard = value != 0;
   } else if (n == "round_marker") {
     e->round_marker = value != 0;
   } else if (n == "virtual_votes") {  // 0: always store the vote planes (A/B)
@@ -1145,6 +1230,77 @@ int av_comm_init(av_engine* e, int32_t world, int32_t rank, const uint8_t id[128
   AV_CHECK(r == ncclSuccess, AV_ERR_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
   AV_HIP(hipStreamSynchronize(e->stream));
   return AV_OK;
+}
+
+int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]) {
+  AV_ENTER(e);
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  static_assert(sizeof(hipIpcMemHandle_t) * 4 == AV_PEER_HANDLE_BYTES, "peer handle blob size");
+  if (!e->arrive) {  // zeroed before any peer can see it: the exchange of handles orders the two
+    AV_HIP(dev_alloc(&e->arrive, (size_t)(2u << 20) / 4));
+    AV_HIP(dev_alloc(&e->barrier_err, 1));
+    AV_HIP(hipMemset(e->arrive, 0, (size_t)(avk::kMaxPeers + 1) * 4));
+    AV_HIP(hipMemset(e->barrier_err, 0, 4));
+    AV_HIP(hipDeviceSynchronize());
+  }
+  void* bufs[4] = {e->pref[0], e->pref[1], e->pref[2], e->arrive};
+  for (int i = 0; i < 4; ++i) {
+    hipIpcMemHandle_t h;
+    AV_HIP(hipIpcGetMemHandle(&h, bufs[i]));
+    std::memcpy(out + i * sizeof(h), &h, sizeof(h));
+  }
+  return AV_OK;
+}
+
+int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handles) {
+  AV_ENTER(e);
+  AV_CHECK(handles && world >= 1 && world <= avk::kMaxPeers + 1 && rank >= 0 && rank < world, AV_ERR_INVALID_ARG,
+           "bad world/rank (at most %d ranks)", avk::kMaxPeers + 1);
+  AV_CHECK(e->N % world == 0 && (int64_t)e->NL * world == e->N && e->n0 == (int64_t)rank * e->NL,
+           AV_ERR_UNSUPPORTED, "node shards must be equal, contiguous and rank-ordered (N %% world == 0)");
+  AV_CHECK(e->t0 == 0 && e->t1 == e->M, AV_ERR_UNSUPPORTED, "node sharding needs the full target range");
+  AV_CHECK(e->comm == nullptr && e->peer_world == 0, AV_ERR_UNSUPPORTED, "exchange already initialised");
+  AV_CHECK(e->arrive != nullptr, AV_ERR_INVALID_ARG, "call av_peer_handles before av_peer_init");
+  for (int r = 0; r < world; ++r) {
+    void* ptrs[4] = {e->pref[0], e->pref[1], e->pref[2], e->arrive};
+    if (r != rank) {
+      for (int i = 0; i < 4; ++i) {
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + (size_t)r * AV_PEER_HANDLE_BYTES + i * sizeof(h), sizeof(h));
+        void* m = nullptr;
+        AV_HIP(hipIpcOpenMemHandle(&m, h, hipIpcMemLazyEnablePeerAccess));
+        e->peer_opened.push_back(m);
+        ptrs[i] = m;
+      }
+    }
+    for (int b = 0; b < 3; ++b) e->peer_pref[b][r] = static_cast<uint32_t*>(ptrs[b]);
+    e->peer_arrive.p[r] = static_cast<uint32_t*>(ptrs[3]);
+  }
+  {
+    uint32_t* tbl[3][avk::kMaxPeers] = {};
+    for (int b = 0; b < 3; ++b) {
+      int n = 0;
+      for (int r = 0; r < world; ++r)
+        if (r != rank) tbl[b][n++] = e->peer_pref[b][r];
+    }
+    AV_HIP(dev_alloc(&e->push_tbl, (size_t)3 * avk::kMaxPeers));
+    AV_HIP(hipMemcpy(e->push_tbl, tbl, sizeof(tbl), hipMemcpyHostToDevice));
+  }
+  e->peer_world = world;
+  e->peer_rank = rank;
+  e->world = world;
+  e->rank = rank;
+  if (world > 1) {
+    // every replica of every snapshot buffer identical from here on: each
+    // rank pushes its own rows of the three buffers, then all ranks meet
+    for (int b = 0; b < 3; ++b) {
+      int rc = push_own_rows(e, b);
+      if (rc != AV_OK) return rc;
+    }
+    int rc = peer_barrier(e);
+    if (rc != AV_OK) return rc;
+  }
+  return av_synchronize(e);
 }
 
 }  // extern "C"

@@ -30,6 +30,7 @@ constexpr int kPV = 0, kPC = 8, kPA = 16, kPK = 17;
 constexpr uint32_t kLogShards = 1024;   // update-log / counter shards
 constexpr uint32_t kMaxPoll = 4096;     // AvalancheMaxElementPoll, avalanche.go:17
 constexpr int kMaxK = 16;
+constexpr int kMaxPeers = 15;           // peer-push exchange: other ranks of a node-sharded network
 
 struct RoundParams {
   uint32_t* planes;
@@ -76,6 +77,14 @@ struct RoundParams {
   uint32_t vv;               // this round may leave V planes unstored (vstale)
   uint32_t* vstale;          // [tiles] 1: the tile's V planes are stale; V = votes of round - 1
   const uint32_t* pref_prev; // [N_pad][BL] snapshot of round - 1 (read by stale tiles)
+  // Peer-push exchange (node-sharded engines, k_round_sweep only):
+  // every replica of a snapshot buffer is identical between rounds, so the
+  // word a lane is about to overwrite in its own row of pref_out is also what
+  // every peer's replica holds; a lane whose published word changed stores the
+  // new word into each peer's replica (push_dst[i] = peer i's pref_out; a
+  // device table, read only by lanes that push).
+  uint32_t push_n;
+  uint32_t* const* push_dst;
 };
 
 // Division by the (runtime) block count BL without a hardware divide:
@@ -120,6 +129,20 @@ hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cu
 // Write back the V planes of stale tiles (p.vstale, p.pref_prev, p.round = the
 // round after the one that left them stale); k = 8 only.
 hipError_t launch_vv_materialize(const RoundParams& p, hipStream_t s);
+
+// Peer-push exchange helpers (kernels.hip). push_rows: copy words [w0, w1) of
+// a local snapshot buffer into the same range of every peer replica.
+struct PeerPtrs {
+  uint32_t* p[kMaxPeers + 1];
+};
+hipError_t launch_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, uint64_t w0, uint64_t w1,
+                            hipStream_t s);
+// Barrier across the ranks of a node-sharded network: lane i writes `seq`
+// into slot `rank` of rank i's arrival array (arrive[i], system scope), then
+// waits until every slot of its own array (arrive[rank]) has reached `seq`.
+// Gives up after ~timeout_ms and sets *err (later barriers then return at once).
+hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
+                               uint32_t timeout_ms, hipStream_t s);
 
 struct InitParams {
   uint32_t* planes;

@@ -658,6 +658,51 @@ hipError_t launch_read_records(const uint32_t* planes, uint32_t BL, uint32_t nl0
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Peer-push exchange of node-sharded engines. Replaces the
+// per-round all-gather of published-preference rows (main.go:168-192: every
+// responder answers from its current IsAccepted) when the ranks' snapshot
+// buffers are mapped into each other's address space (av_peer_init).
+// ---------------------------------------------------------------------------
+// Copy words [w0, w1) of a local snapshot buffer into every peer replica:
+// a full resynchronisation, used after rounds whose kernel does not push.
+__global__ __launch_bounds__(256) void k_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, uint64_t w0,
+                                                   uint64_t w1) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = w0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w1; i += stride) {
+    const uint32_t v = src[i];
+#pragma unroll
+    for (int r = 0; r < kMaxPeers; ++r)  // static indices: the pointers stay in SGPRs
+      if ((uint32_t)r < n_dst) dst.p[r][i] = v;
+  }
+}
+
+// One wave. Lane i (< world) stores seq into rank i's arrival slot `rank`
+// (release, system scope: this rank's earlier kernels and pushes are visible
+// first), then waits for its own slot i to reach seq (acquire, system scope).
+// Every lane leaves after at most `ticks` wall-clock ticks; a timeout sets *err
+// and every later barrier of the engine returns without waiting.
+__global__ __launch_bounds__(64) void k_peer_barrier(PeerPtrs arrive, const uint32_t* own, uint32_t world,
+                                                     uint32_t rank, uint32_t seq, uint32_t* err, uint64_t ticks) {
+  const uint32_t i = threadIdx.x;
+  uint32_t* mine = arrive.p[0];  // lane i's rank-i array, selected with static indices
+#pragma unroll
+  for (int r = 1; r <= kMaxPeers; ++r)
+    if ((uint32_t)r == i) mine = arrive.p[r];
+  if (i < world) __hip_atomic_store(mine + rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  const bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  if (i >= world || failed) return;
+  const uint32_t* slot = own + i;  // own == arrive.p[rank]
+  const uint64_t t0 = (uint64_t)wall_clock64();
+  while ((int32_t)(__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
+    if ((uint64_t)wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0, uint32_t tl1,
                                 const uint32_t* in, hipStream_t s) {
   const uint32_t nb = ((tl1 + 31u) >> 5) - (tl0 >> 5);
@@ -696,6 +741,26 @@ hipError_t launch_poll_sets(const uint32_t* planes, const uint32_t* valid, uint3
                             uint32_t t0, uint32_t* counts, const int64_t* offsets, int32_t* out, hipStream_t s) {
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_poll_sets, dim3(n), dim3(64), 0, s, planes, valid, BL, nl0, t0, counts, offsets, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, uint64_t w0, uint64_t w1,
+                            hipStream_t s) {
+  if (w1 <= w0 || !n_dst) return hipSuccess;
+  const uint64_t blocks = std::min<uint64_t>(4096u, (w1 - w0 + 255u) / 256u);
+  hipLaunchKernelGGL(k_push_rows, dim3((uint32_t)blocks), dim3(256), 0, s, src, dst, n_dst, w0, w1);
+  return hipGetLastError();
+}
+
+hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
+                               uint32_t timeout_ms, hipStream_t s) {
+  if (world > (uint32_t)kMaxPeers + 1u || rank >= world) return hipErrorInvalidValue;
+  int dev = 0, khz = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess) return e;
+  const uint64_t ticks = (uint64_t)timeout_ms * (uint64_t)(khz > 0 ? khz : 100000);
+  hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, s, arrive, arrive.p[rank], world, rank, seq, err, ticks);
   return hipGetLastError();
 }
 

@@ -239,8 +239,17 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     st4<POL>(tr, grp + 192, 3072u + lane * 16u, o3);
     st1<POL>(tr, tp + 1536u + lane, (1536u + lane) * 4u, A);
     const uint32_t prow = node * p.BL + b;  // < N * BL < 2^31
+    const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
+    if (p.push_n) {
+      // peer-push exchange (kernels.h): the word being overwritten is what
+      // every peer replica holds; push only a changed word
+      const uint32_t old = p.pref_out[prow];
+      if (pub != old) {
+        for (uint32_t r = 0; r < p.push_n; ++r) p.push_dst[r][prow] = pub;
+      }
+    }
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, 0x7FFFFFFF, kRsrcWord3);
-    st1<POL>(pr, p.pref_out + prow, prow * 4u, is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A);
+    st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
     // a record deleted this round keeps the vote/consider planes stored
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
@@ -255,7 +264,9 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   acc.applied += applied;
   acc.died += (uint32_t)__popc(died);
   // stale: 7 regathered words instead of the 8 V planes read; virt: V planes not written
-  acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale ? 4u : 0u) - (virt ? 32u : 0u) : 0u;
+  // push: + the 4-B read of the word being overwritten
+  acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale ? 4u : 0u) - (virt ? 32u : 0u) + (p.push_n ? 4u : 0u)
+                           : 0u;
   acc.emitted_bytes += emitted;
 }
 

@@ -65,6 +65,8 @@ class Config(C.Structure):
 
 
 # every symbol declared in include/avhip.h (non-inline)
+PEER_HANDLE_BYTES = 256  # include/avhip.h AV_PEER_HANDLE_BYTES
+
 EXPORTED = [
     "av_abi_version", "av_config_init", "av_create", "av_destroy", "av_strerror", "av_last_error",
     "av_init_records", "av_add_targets", "av_set_valid", "av_register_votes", "av_is_accepted",
@@ -72,6 +74,7 @@ EXPORTED = [
     "av_replay_rounds", "av_synchronize", "av_round_index", "av_updates_count", "av_fetch_updates",
     "av_update_log_overflowed", "av_applied_votes", "av_alg_bytes", "av_finalized_count", "av_live_records", "av_discard_updates", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
+    "av_peer_handles", "av_peer_init",
 ]
 
 _lib = None
@@ -126,6 +129,8 @@ def lib():
         "av_layout_info": (i32, [_vp, P(i64), P(i64), P(i64), P(i32)]),
         "av_comm_unique_id": (i32, [_vp]),
         "av_comm_init": (i32, [_vp, i32, i32, _vp]),
+        "av_peer_handles": (i32, [_vp, _vp]),
+        "av_peer_init": (i32, [_vp, i32, i32, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -375,6 +380,20 @@ class Engine:
         lanes, nl, bl, capped = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int32()
         _check(lib().av_layout_info(self._h, C.byref(lanes), C.byref(nl), C.byref(bl), C.byref(capped)))
         return {"lanes": lanes.value, "local_nodes": nl.value, "local_blocks": bl.value, "capped": bool(capped.value)}
+
+    def peer_handles(self) -> bytes:
+        """IPC handles of this rank's preference snapshots (av_peer_handles)."""
+        buf = (C.c_uint8 * PEER_HANDLE_BYTES)()
+        _check(lib().av_peer_handles(self._h, C.cast(buf, _vp)))
+        return bytes(buf)
+
+    def peer_init(self, world, rank, handles):
+        """Map every rank's snapshots (handles: the rank-ordered list of
+        peer_handles() blobs) and switch to the peer-push exchange."""
+        blob = b"".join(handles)
+        assert len(blob) == world * PEER_HANDLE_BYTES
+        buf = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        _check(lib().av_peer_init(self._h, world, rank, C.cast(buf, _vp)))
 
     def comm_init(self, world, rank, uid: bytes):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)

@@ -204,6 +204,22 @@ int av_layout_info(av_engine* e, int64_t* lanes, int64_t* local_nodes, int64_t* 
 int av_comm_unique_id(uint8_t out[128]);
 int av_comm_init(av_engine* e, int32_t world, int32_t rank, const uint8_t id[128]);
 
+/* ---- multi-GPU, peer-push exchange (node-sharded engines; replaces the
+ * per-round all-gather above). Same network split as av_comm_init. Each rank
+ * exports IPC handles of its preference snapshots (av_peer_handles), the
+ * caller exchanges the blobs (any host collective), and av_peer_init maps every
+ * peer's buffers. A round then stores only the published words that changed
+ * straight into every peer's replica (the responder of main.go:168-192 answers
+ * from IsAccepted, processor.go:125-130, of the round-start snapshot), followed
+ * by a device-side barrier across the ranks. Collective: every rank must make
+ * the same calls. Record writes outside a round (av_add_targets,
+ * av_register_votes, av_write_records) return AV_ERR_UNSUPPORTED on such an
+ * engine. */
+#define AV_PEER_HANDLE_BYTES 256
+int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]);
+/* handles: world * AV_PEER_HANDLE_BYTES bytes, rank-ordered (this rank's own blob is ignored) */
+int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handles);
+
 #ifdef __cplusplus
 }
 #endif
