@@ -56,13 +56,22 @@ WORKLOADS = {
 }
 
 
+PARALLELISM = {
+    "peers": "node-sharded, changed preference words pushed to peers over xGMI + device barrier per round",
+    "nodes": "node-sharded, RCCL all-gather of preference rows per round",
+    "targets": "target-sharded, no exchange",
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=14)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
-    ap.add_argument("--shard", default="targets", choices=["targets", "nodes"])
+    # peers: node shards + peer-push exchange; nodes: node shards +
+    # RCCL all-gather of the preference rows; targets: target shards, no exchange
+    ap.add_argument("--shard", default="peers", choices=["peers", "targets", "nodes"])
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xA7A1A9C4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
@@ -126,6 +135,23 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         obj = [avhip.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(world, rank, obj[0])
+    elif world > 1 and args.shard == "peers":
+        # map every rank's preference snapshots (IPC over xGMI); if any rank
+        # cannot, every rank falls back to target sharding (same network)
+        blobs = [None] * world
+        dist.all_gather_object(blobs, eng.peer_handles())
+        err = None
+        try:
+            eng.peer_init(world, rank, blobs)
+        except avhip.AvError as ex:
+            err = repr(ex)[:200]
+        errs = [None] * world
+        dist.all_gather_object(errs, err)
+        if any(errs):
+            eng.close()
+            args.shard = "targets"
+            args.shard_fallback = next(e for e in errs if e)
+            return measure(wl, args, world, rank, local_rank, steps, warmup)
     if replay:  # both passes' rounds (the roofline pass re-runs warmup + steps)
         eng.replay_prepare(3 * (warmup + steps))
     run = eng.replay_rounds if replay else eng.run_rounds
@@ -181,6 +207,19 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     # actually streamed, gathered vote words, published words, StatusUpdates)
     alg_bytes = (eng.alg_bytes() - bytes1) / max(launches, 1)
     kavg_ms = kern_ms / max(launches, 1)
+    replicas = None
+    if world > 1 and args.shard in ("peers", "nodes"):
+        # every rank's replica of the published preferences must be the same:
+        # hash a slice of every rank's node range as this rank sees it
+        import hashlib
+
+        hs = hashlib.sha256()
+        for r in range(world):
+            a = sharding.node_shard(n, world, r)[0]
+            hs.update(eng.read_pref(a, min(a + 2048, n)).tobytes())
+        digests = [None] * world
+        dist.all_gather_object(digests, hs.hexdigest())
+        replicas = len(set(digests)) == 1
     eng.close()
 
     if world > 1:
@@ -203,7 +242,7 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     return {
         "desc": desc, "n": n, "m": m, "k": k, "value": value, "elapsed": elapsed, "applied": applied,
         "emitted": emitted, "info": info, "kavg_ms": kavg_ms, "alg_bytes": alg_bytes, "achieved": achieved,
-        "kernel": kname, "log_overflow": log_overflow,
+        "kernel": kname, "log_overflow": log_overflow, "replicas_identical": replicas,
     }
 
 
@@ -241,8 +280,8 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.rehearse_one_gpu:
-        if args.shard != "targets":
-            raise SystemExit("--rehearse-one-gpu supports target sharding only (RCCL needs distinct GPUs)")
+        if args.shard == "nodes":
+            raise SystemExit("--rehearse-one-gpu: not with --shard nodes (RCCL needs distinct GPUs)")
         local_rank = 0
     torch.cuda.set_device(local_rank)
     if world > 1 and args.rehearse_one_gpu:
@@ -291,7 +330,7 @@ def main():
                 "workload": r["desc"],
                 "n_nodes": r["n"], "n_targets": r["m"], "k": r["k"],
                 "rounds": f"{args.warmup}..{args.warmup + args.steps - 1}",
-                "parallelism": f"{args.shard}-sharded x{world}" if world > 1 else "single GPU",
+                "parallelism": (PARALLELISM[args.shard] + f" x{world}") if world > 1 else "single GPU",
                 "layout": "bit-sliced: 25 u32 planes per 32 records; tile of 64 lanes contiguous",
                 "capped_poll_path": r["info"]["capped"],
             },
@@ -300,6 +339,10 @@ def main():
             "update_log_overflow": r["log_overflow"],
             "roofline": roofline(r, traffic),
         }
+        if r["replicas_identical"] is not None:
+            line["config"]["replicas_identical"] = r["replicas_identical"]
+        if getattr(args, "shard_fallback", None):
+            line["config"]["shard_fallback"] = "peer exchange unavailable: " + args.shard_fallback
         if secondary:
             line["secondary"] = secondary
         if not args.no_cpu_baseline and world == 1:

@@ -673,7 +673,7 @@ __global__ __launch_bounds__(256) void k_push_rows(const uint32_t* src, PeerPtrs
     const uint32_t v = src[i];
 #pragma unroll
     for (int r = 0; r < kMaxPeers; ++r)  // static indices: the pointers stay in SGPRs
-      if ((uint32_t)r < n_dst) dst.p[r][i] = v;
+      if ((uint32_t)r < n_dst) __hip_atomic_store(dst.p[r] + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -245,7 +245,10 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
       // every peer replica holds; push only a changed word
       const uint32_t old = p.pref_out[prow];
       if (pub != old) {
-        for (uint32_t r = 0; r < p.push_n; ++r) p.push_dst[r][prow] = pub;
+        // system-scope stores write through to the peer's memory (xGMI); the
+        // barrier after the round orders them before any peer reads them
+        for (uint32_t r = 0; r < p.push_n; ++r)
+          __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, 0x7FFFFFFF, kRsrcWord3);

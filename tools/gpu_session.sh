@@ -36,6 +36,12 @@ for s in "$@"; do
             --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --rehearse-one-gpu --no-secondary ;;
     rehearse4) step rehearse4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
             --master-addr 127.0.0.1 --master-port 29532 bench.py --gpus 4 --rehearse-one-gpu --no-secondary ;;
+    rehearse2p) step rehearse2p 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --rehearse-one-gpu --no-secondary --shard peers ;;
+    rehearse4p) step rehearse4p 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+            --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --rehearse-one-gpu --no-secondary --shard peers ;;
+    peertests) step peertests 600 python -u -m pytest tests/test_gpu_peer_push.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    nsprobe) step nsprobe 600 python tools/node_shard_probe.py --json $OUT/node_shard_probe.json ;;
     ab) step ab 900 python tools/ab_tune.py --json $OUT/ab.json ;;
     ab1) step ab1 600 python tools/ab_tune.py --shards 1 --json $OUT/ab1.json ;;
     abc3) step abc3 600 python tools/ab_tune.py --workload c3 --shards 1 --variants sweep,per_tile,ablate --json $OUT/abc3.json ;;

@@ -12,6 +12,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "go-avalanche_amd", "python"))
@@ -27,33 +28,42 @@ from bench import WORKLOADS  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shards", default="1,2,4,8")
-    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--rounds", type=int, default=14)
     ap.add_argument("--workload", default="c4")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
     N, M, K, init_mode, init_param, byz, replay, _ = WORKLOADS[args.workload]
     out = {}
+
+    def timed(e, rounds):
+        # bench.py's protocol: device warm-up pass, re-init, 2 warmup rounds,
+        # then `rounds` back-to-back rounds timed around a synchronize
+        e.init_records(init_mode, init_param)
+        e.run_rounds(2 + rounds)
+        e.synchronize()
+        e.discard_updates()
+        e.init_records(init_mode, init_param)
+        e.run_rounds(2)
+        e.synchronize()
+        e.discard_updates()
+        t0 = time.perf_counter()
+        e.run_rounds(rounds)
+        e.synchronize()
+        return (time.perf_counter() - t0) / rounds * 1e3
+
     for g in [int(x) for x in args.shards.split(",")]:
-        for vv in (1, 0):
-            e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz,
-                             node_range=sharding.node_shard(N, g, 0), log_capacity=1 << 26)
-            e.set_option("unsynced_shard", 1)
-            e.set_option("virtual_votes", vv)
-            e.init_records(init_mode, init_param)
-            e.run_rounds(3)
-            e.synchronize()
-            e.discard_updates()
-            ts = []
-            for _ in range(args.rounds):
-                e.set_timing(True)
-                e.run_rounds(1)
-                ms, n = e.kernel_stats()
-                e.set_timing(False)
-                ts.append(ms / max(n, 1))
+        for kind in ("nodes", "targets"):
+            if kind == "nodes":
+                e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz,
+                                 node_range=sharding.node_shard(N, g, 0), log_capacity=1 << 26)
+                e.set_option("unsynced_shard", 1)
+            else:
+                e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz,
+                                 target_range=sharding.target_shard(M, g, 0), log_capacity=1 << 26)
+            ms = [timed(e, args.rounds) for _ in range(3)]
             e.close()
-            key = f"{args.workload}_nodeshard{g}_vv{vv}"
-            out[key] = {"nodes": list(sharding.node_shard(N, g, 0)), "median_ms": statistics.median(ts),
-                        "min_ms": min(ts)}
+            key = f"{args.workload}_{kind}shard{g}"
+            out[key] = {"ms_per_round": ms, "median_ms": statistics.median(ms)}
             print(key, out[key], flush=True)
     if args.json:
         with open(args.json, "w") as f:
