@@ -1235,7 +1235,7 @@ int av_comm_init(av_engine* e, int32_t world, int32_t rank, const uint8_t id[128
 int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]) {
   AV_ENTER(e);
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
-  static_assert(sizeof(hipIpcMemHandle_t) * 4 == AV_PEER_HANDLE_BYTES, "peer handle blob size");
+  static_assert(sizeof(hipIpcMemHandle_t) * 4 + 64 == AV_PEER_HANDLE_BYTES, "peer handle blob size");
   if (!e->arrive) {  // zeroed before any peer can see it: the exchange of handles orders the two
     AV_HIP(dev_alloc(&e->arrive, (size_t)(2u << 20) / 4));
     AV_HIP(dev_alloc(&e->barrier_err, 1));
@@ -1249,6 +1249,10 @@ int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]) {
     AV_HIP(hipIpcGetMemHandle(&h, bufs[i]));
     std::memcpy(out + i * sizeof(h), &h, sizeof(h));
   }
+  // the device's PCI bus id: peers check that they can reach it (av_peer_init)
+  char bus[64] = {};
+  AV_HIP(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, e->cfg.device));
+  std::memcpy(out + 4 * sizeof(hipIpcMemHandle_t), bus, 64);
   return AV_OK;
 }
 
@@ -1264,6 +1268,22 @@ int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handl
   for (int r = 0; r < world; ++r) {
     void* ptrs[4] = {e->pref[0], e->pref[1], e->pref[2], e->arrive};
     if (r != rank) {
+      // a peer GPU this process can see must be reachable (xGMI peer access);
+      // one it cannot see (restricted visibility) is left to the IPC mapping
+      char bus[65] = {};
+      std::memcpy(bus, handles + (size_t)r * AV_PEER_HANDLE_BYTES + 4 * sizeof(hipIpcMemHandle_t), 64);
+      int pdev = -1;
+      if (bus[0] && hipDeviceGetByPCIBusId(&pdev, bus) == hipSuccess && pdev != e->cfg.device) {
+        int can = 0;
+        AV_HIP(hipDeviceCanAccessPeer(&can, e->cfg.device, pdev));
+        AV_CHECK(can, AV_ERR_UNSUPPORTED, "device %d cannot access peer device %d (%s)", e->cfg.device, pdev, bus);
+        hipError_t pe = hipDeviceEnablePeerAccess(pdev, 0);
+        AV_CHECK(pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled, AV_ERR_HIP,
+                 "hipDeviceEnablePeerAccess(%d): %s", pdev, hipGetErrorString(pe));
+        (void)hipGetLastError();
+      } else {
+        (void)hipGetLastError();
+      }
       for (int i = 0; i < 4; ++i) {
         hipIpcMemHandle_t h;
         std::memcpy(&h, handles + (size_t)r * AV_PEER_HANDLE_BYTES + i * sizeof(h), sizeof(h));

@@ -65,7 +65,7 @@ class Config(C.Structure):
 
 
 # every symbol declared in include/avhip.h (non-inline)
-PEER_HANDLE_BYTES = 256  # include/avhip.h AV_PEER_HANDLE_BYTES
+PEER_HANDLE_BYTES = 320  # include/avhip.h AV_PEER_HANDLE_BYTES
 
 EXPORTED = [
     "av_abi_version", "av_config_init", "av_create", "av_destroy", "av_strerror", "av_last_error",

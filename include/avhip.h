@@ -215,7 +215,7 @@ int av_comm_init(av_engine* e, int32_t world, int32_t rank, const uint8_t id[128
  * the same calls. Record writes outside a round (av_add_targets,
  * av_register_votes, av_write_records) return AV_ERR_UNSUPPORTED on such an
  * engine. */
-#define AV_PEER_HANDLE_BYTES 256
+#define AV_PEER_HANDLE_BYTES 320  /* 4 IPC handles + the device's PCI bus id */
 int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]);
 /* handles: world * AV_PEER_HANDLE_BYTES bytes, rank-ordered (this rank's own blob is ignored) */
 int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handles);
