@@ -72,6 +72,10 @@ struct av_engine {
   // smallest BL it is used at (option "vv_min_bl": below it the 7 extra
   // gathered rows cost more requests than the 64 B per lane of V planes save)
   uint32_t* vstale = nullptr;  // [tiles]
+  // deferred count planes (kernels.h klazy): option "count_lazy"
+  uint32_t* kpend = nullptr;   // [tiles]
+  bool k_pend = false;         // some tile may hold pending steps or flags
+  bool count_lazy = true;
   bool v_stale = false;        // some tile may be stale
   bool virtual_votes = true;
   uint32_t vv_min_bl = 16;
@@ -221,17 +225,36 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.bl_magic = e->bl_magic;
   p.bl_sh1 = e->bl_sh1;
   p.bl_sh2 = e->bl_sh2;
+  p.kpend = e->kpend;
+  p.klazy = 0u;
   return p;
 }
 
 // Write back the vote planes of tiles the last warm k = 8 sim round left
 // stale (kernels.h vv); every path that reads or writes records other than
 // such a round calls this first.
-int materialize_votes(av_engine* e) {
+int materialize_votes_only(av_engine* e) {
   if (!e->v_stale) return AV_OK;
   AV_HIP(avk::launch_vv_materialize(round_params(e, nullptr), e->stream));
   e->v_stale = false;
   return AV_OK;
+}
+
+// Apply the pending +8 steps of deferred count planes (kernels.h klazy);
+// every path that reads or writes counts other than a klazy round calls this
+// first.
+int materialize_counts(av_engine* e) {
+  if (!e->k_pend) return AV_OK;
+  AV_HIP(avk::launch_kl_materialize(round_params(e, nullptr), e->stream));
+  e->k_pend = false;
+  return AV_OK;
+}
+
+// Both deferred forms (vote planes, count planes) written back.
+int materialize_votes(av_engine* e) {
+  int rc = materialize_votes_only(e);
+  if (rc != AV_OK) return rc;
+  return materialize_counts(e);
 }
 
 // Peer-push exchange: copy this rank's rows of snapshot buffer `b` into every
@@ -274,11 +297,21 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   const bool vv = e->virtual_votes && sweep && e->k == 8 && !replay && e->c_monotone && e->warm_all &&
                   !e->ablate_gather && e->BL >= e->vv_min_bl;
   if (!vv) {
-    int rc = materialize_votes(e);
+    int rc = materialize_votes_only(e);
     if (rc != AV_OK) return rc;
   }
   p.vv = vv ? 1u : 0u;
   if (vv) e->v_stale = true;
+  // count planes may be deferred: the sweep's warm k = 8 sim modes, while no
+  // record can finalize (every true count < 120 at round start)
+  const bool klazy = e->count_lazy && sweep && e->k == 8 && !replay && e->c_monotone && e->warm_all &&
+                     !e->ablate_gather && e->count_bound < 120;
+  if (!klazy) {
+    int rc = materialize_counts(e);
+    if (rc != AV_OK) return rc;
+  }
+  p.klazy = klazy ? 1u : 0u;
+  if (klazy) e->k_pend = true;
   bool all_valid = true;
   for (uint32_t b = 0; b < e->BL; ++b) {
     const int64_t tb = e->t0 + 32ll * b;
@@ -403,7 +436,7 @@ int av_destroy(av_engine* e) {
   if (e->barrier_err) (void)hipFree(e->barrier_err);
   if (e->push_tbl) (void)hipFree(e->push_tbl);
   if (e->marker) (void)hipEventDestroy(e->marker);
-  void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
+  void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->kpend, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->dlog, e->dlog_count, e->upd_count,
                   e->applied, e->bytes, e->finalized, e->scratch_count, e->replay};
   for (void* b : bufs)
@@ -480,7 +513,9 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->pref[1], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->pref[2], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->vstale, e->Lpad / 64)) != hipSuccess) return hip_fail(he, "alloc planes");
+  if ((he = dev_alloc(&e->kpend, e->Lpad / 64)) != hipSuccess) return hip_fail(he, "alloc planes");
   (void)hipMemsetAsync(e->vstale, 0, (size_t)(e->Lpad / 64) * 4, e->stream);
+  (void)hipMemsetAsync(e->kpend, 0, (size_t)(e->Lpad / 64) * 4, e->stream);
   if ((he = dev_alloc(&e->valid, e->BL)) != hipSuccess) return hip_fail(he, "alloc valid");
   if ((he = dev_alloc(&e->byz, (e->N + 31) / 32)) != hipSuccess) return hip_fail(he, "alloc byz");
   if ((he = dev_alloc(&e->log, (size_t)e->log_cap * e->log_shards)) != hipSuccess) return hip_fail(he, "alloc log");
@@ -540,6 +575,10 @@ int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
   if (e->v_stale) {  // every plane is rewritten
     AV_HIP(hipMemsetAsync(e->vstale, 0, (size_t)(e->Lpad / 64) * 4, e->stream));
     e->v_stale = false;
+  }
+  if (e->k_pend) {
+    AV_HIP(hipMemsetAsync(e->kpend, 0, (size_t)(e->Lpad / 64) * 4, e->stream));
+    e->k_pend = false;
   }
   AV_CHECK(init_mode >= AV_INIT_NONE && init_mode <= AV_INIT_PAIRS, AV_ERR_INVALID_ARG, "bad init_mode");
   avk::InitParams p{};
@@ -1155,6 +1194,11 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->round_marker = value != 0;
   } else if (n == "virtual_votes") {  // 0: always store the vote planes (A/B)
     e->virtual_votes = value != 0;
+  } else if (n == "count_lazy") {  // 0: always store the count planes (A/B)
+    AV_ENTER(e);
+    int rc = materialize_counts(e);
+    if (rc != AV_OK) return rc;
+    e->count_lazy = value != 0;
   } else if (n == "vv_min_bl") {
     AV_CHECK(value >= 1 && value < (1ll << 31), AV_ERR_INVALID_ARG, "bad vv_min_bl");
     e->vv_min_bl = (uint32_t)value;

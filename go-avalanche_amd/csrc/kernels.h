@@ -85,7 +85,19 @@ struct RoundParams {
   // device table, read only by lanes that push).
   uint32_t push_n;
   uint32_t* const* push_dst;
+  // Deferred count planes (`kl`, k = 8, warm sim rounds in which no record can
+  // finalize): a tile all of whose polled records agreed with
+  // their accepted bit on all 8 votes gains exactly +8 on every polled count
+  // (vote.go:66-69) and nothing else changes in its K planes; it leaves them
+  // unstored and counts the pending +8 steps in kpend[tile] instead. The true
+  // count of a live, valid record is K + 8 * pending; dead or invalid records
+  // are untouched. kpend[tile]: bits 0..7 pending steps, bit 31 the tile's
+  // live records are exactly its valid targets' records (its K planes need not
+  // be read to find the polled set).
+  uint32_t klazy;            // this round may defer count planes
+  uint32_t* kpend;           // [tiles]
 };
+constexpr uint32_t kPendAllLive = 0x80000000u;
 
 // Division by the (runtime) block count BL without a hardware divide:
 // Granlund-Montgomery round-up magic, exact for every 32-bit n.
@@ -129,6 +141,8 @@ hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cu
 // Write back the V planes of stale tiles (p.vstale, p.pref_prev, p.round = the
 // round after the one that left them stale); k = 8 only.
 hipError_t launch_vv_materialize(const RoundParams& p, hipStream_t s);
+// Apply the pending +8 steps of deferred count planes (p.kpend) and clear them.
+hipError_t launch_kl_materialize(const RoundParams& p, hipStream_t s);
 
 // Peer-push exchange helpers (kernels.hip). push_rows: copy words [w0, w1) of
 // a local snapshot buffer into the same range of every peer replica.

@@ -56,6 +56,7 @@ struct TileIn {
   u32x4 v0, v1, k0, k1;
   uint32_t A, vmask, byzw;
   uint32_t stale;                // wave-uniform: V planes stale, v0/v1 regathered (kernels.h vstale)
+  uint32_t kw;                   // wave-uniform: kpend[tile] (kernels.h klazy); K planes not loaded if all-live
   uint32_t C[WARM ? 1 : 8];
   uint32_t w[K];                 // yes bits: err == 0 (vote.go:55)
   uint32_t cw[REPLAY ? K : 1];   // consider bits: int32(err) >= 0 (vote.go:56); sim votes: all-ones
@@ -89,8 +90,17 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
     in.v0 = ld4<POL>(grp);
     in.v1 = ld4<POL>(grp + 64);
   }
-  in.k0 = ld4<POL>(grp + 128);
-  in.k1 = ld4<POL>(grp + 192);
+  in.kw = 0u;
+  if constexpr (VV) {
+    if (p.klazy) in.kw = uni(p.kpend[tile]);
+  }
+  if (!(in.kw & kPendAllLive)) {
+    in.k0 = ld4<POL>(grp + 128);
+    in.k1 = ld4<POL>(grp + 192);
+  } else {
+    in.k0 = u32x4{0u, 0u, 0u, 0u};
+    in.k1 = u32x4{0u, 0u, 0u, 0u};
+  }
   in.A = ld1<POL>(tp + 1536u + lane);
   if constexpr (!WARM) {
 #pragma unroll
@@ -141,7 +151,8 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
   u32x4* const grp = reinterpret_cast<u32x4*>(tp) + lane;
   const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(tp, 0, kPlanes * 64 * 4, kRsrcWord3);
-  const u32x4 v0 = in.v0, v1 = in.v1, k0 = in.k0, k1 = in.k1;
+  const u32x4 v0 = in.v0, v1 = in.v1;
+  u32x4 k0 = in.k0, k1 = in.k1;
   uint32_t A = in.A;
   uint32_t C[8];
 #pragma unroll
@@ -166,7 +177,10 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     ns[i] = SYM ? 0u : WARM ? ~vi : (~vi & C[6 - i]);
   }
 
-  const uint32_t live0 = ~k1[3];                         // K7 = no live record
+  constexpr bool KL = VVM && WARM && !REPLAY && K == 8;  // deferred count planes possible (kernels.h klazy)
+  const bool klazy = KL && p.klazy;                      // wave-uniform: no record can finalize this round
+  const bool kunread = KL && (in.kw & kPendAllLive);     // K planes not loaded: live == valid
+  const uint32_t live0 = kunread ? in.vmask : ~k1[3];    // K7 = no live record
   const uint32_t P0 = live0 & vmask;                     // polled: live and IsValid (processor.go:95-103)
   const uint32_t keep = active ? (live0 & ~vmask) : 0u;  // live but !IsValid: untouched (processor.go:101-103)
 
@@ -210,9 +224,65 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   }
   uint32_t E[K], alive = P0, applied = 0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u;
   const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
-  const uint32_t nearfin = P0 & Kp[6] & Kp[5] & Kp[4] & Kp[3];  // count >= 120: may reach 128 (K <= 8)
+  // count >= 120: may reach 128 (K <= 8); never in a klazy round (engine bound)
+  const uint32_t nearfin = klazy ? 0u : P0 & Kp[6] & Kp[5] & Kp[4] & Kp[3];
   const bool det = __ballot(nearfin != 0u) != 0ull;
-  round_slots<K, SYM>(ys, ns, low3, nearfin, det, alive, A, E, c, F, applied);
+  const uint32_t A_in = A;
+  // Settled tiles (warm sim votes, K == 8, no record near 128): when every
+  // polled record's 7 old votes and 8 new votes all agree with its accepted
+  // bit, every 8-vote window of the round is unanimous, so each slot is a
+  // conclusive agreeing vote (vote.go:58-69: confidence += 2, no flip, no
+  // StatusUpdate) and the slot network can be skipped: c = 8, F = 0.
+  bool settled = false;
+  if constexpr (SYM && K == 8) {
+    if (!det) {
+      uint32_t agree = P0;
+#pragma unroll
+      for (int i = 0; i < 7 + K; ++i) agree &= ~(ys[i] ^ A);
+      settled = __ballot(agree != P0) == 0ull;
+    }
+  }
+  if (settled) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) E[j] = 0u;
+    c[3] = P0;
+    applied = 8u * (uint32_t)__popc(P0);
+  } else {
+    round_slots<K, SYM>(ys, ns, low3, nearfin, det, alive, A, E, c, F, applied);
+  }
+  // deferred count planes: every polled record agreed on all 8 votes (no flip,
+  // c == 8) -> K stays as stored and the tile's pending +8 steps grow by one
+  bool kdefer = false;
+  uint32_t pend = 0u;
+  if constexpr (KL) {
+    if (klazy) {
+      const uint32_t c8 = c[3] & ~(c[0] | c[1] | c[2]);
+      const bool lane_uniform = !active || (((F & P0) | (~c8 & P0)) == 0u);
+      kdefer = __ballot(!lane_uniform) == 0ull;
+      pend = in.kw & 0xFFu;
+      if (!kdefer) {
+        if (kunread) {  // late load: the tile leaves the deferred state
+          k0 = ld4<POL>(reinterpret_cast<const u32x4*>(tp) + lane + 128);
+          k1 = ld4<POL>(reinterpret_cast<const u32x4*>(tp) + lane + 192);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            Kp[i] = k0[i];
+            Kp[4 + i] = k1[i];
+          }
+        }
+        // true count = K + 8 * pend on the polled records: add pend to planes 3..6
+        uint32_t cy = 0u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t bi = ((pend >> i) & 1u) ? P0 : 0u;
+          const uint32_t t = Kp[3 + i] ^ bi;
+          const uint32_t si = t ^ cy;
+          cy = (t & cy) | (Kp[3 + i] & bi);
+          Kp[3 + i] = si;
+        }
+      }
+    }
+  }
   // count_new = F ? c : count + c on planes 0..6 (survivors stay <= 127); deleted: count 128 (K7 set)
   const uint32_t died = P0 & ~alive;
   {
@@ -228,16 +298,20 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     Kp[7] |= died;
   }
 
+  // klazy rounds: a tile whose A plane did not change does not rewrite it
+  const bool astore = !klazy || __ballot(active && A != A_in) != 0ull;
   if (active) {
-    u32x4 o2, o3;
+    if (!kdefer) {
+      u32x4 o2, o3;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      o2[i] = Kp[i];
-      o3[i] = Kp[4 + i];
+      for (int i = 0; i < 4; ++i) {
+        o2[i] = Kp[i];
+        o3[i] = Kp[4 + i];
+      }
+      st4<POL>(tr, grp + 128, 2048u + lane * 16u, o2);
+      st4<POL>(tr, grp + 192, 3072u + lane * 16u, o3);
     }
-    st4<POL>(tr, grp + 128, 2048u + lane * 16u, o2);
-    st4<POL>(tr, grp + 192, 3072u + lane * 16u, o3);
-    st1<POL>(tr, tp + 1536u + lane, (1536u + lane) * 4u, A);
+    if (astore) st1<POL>(tr, tp + 1536u + lane, (1536u + lane) * 4u, A);
     const uint32_t prow = node * p.BL + b;  // < N * BL < 2^31
     const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
     if (p.push_n) {
@@ -260,6 +334,16 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   if constexpr (VVM && WARM && !REPLAY && K == 8) {
     if (p.vv && lane == 0 && virt != (in.stale != 0u)) p.vstale[tile] = virt ? 1u : 0u;
   }
+  if constexpr (KL) {
+    if (klazy) {
+      // live records == valid targets in every lane (no live-but-invalid record):
+      // the next round need not read K to find the polled set
+      const bool all_live = __ballot(active && live0 != vmask) == 0ull;
+      const uint32_t kw = (kdefer ? pend + 1u : 0u) | (all_live ? kPendAllLive : 0u);
+      if (lane == 0 && kw != in.kw) p.kpend[tile] = kw;
+      if (lane == 0) acc.lane_bytes += kw != in.kw ? 8u : 4u;  // kpend word read (+ written)
+    }
+  }
   const uint32_t emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates);
 
   constexpr uint32_t plane_bytes = WARM ? 2u * 17u * 4u : 2u * kPlanes * 4u;
@@ -268,7 +352,10 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   acc.died += (uint32_t)__popc(died);
   // stale: 7 regathered words instead of the 8 V planes read; virt: V planes not written
   // push: + the 4-B read of the word being overwritten
-  acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale ? 4u : 0u) - (virt ? 32u : 0u) + (p.push_n ? 4u : 0u)
+  // kl: K planes neither read (kunread and deferred) nor written (deferred); A not rewritten
+  const uint32_t kbytes = (kunread && kdefer ? 32u : 0u) + (kdefer ? 32u : 0u);
+  acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale ? 4u : 0u) - (virt ? 32u : 0u) + (p.push_n ? 4u : 0u) -
+                                 kbytes - (astore ? 0u : 4u)
                            : 0u;
   acc.emitted_bytes += emitted;
 }
@@ -398,6 +485,47 @@ __global__ __launch_bounds__(256) void k_vv_materialize(const RoundParams p) {
   if (lane == 0) p.vstale[tile] = 0u;
 }
 
+// Apply deferred count planes (kernels.h klazy): + 8 * pending on the polled
+// (live, valid) records of each tile with pending steps, then clear them.
+__global__ __launch_bounds__(256) void k_kl_materialize(const RoundParams p) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t tile = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
+  if (tile >= (p.Lpad >> 6)) return;
+  const uint32_t kw = uni(p.kpend[tile]);
+  const uint32_t pend = kw & 0xFFu;
+  if (kw == 0u) return;
+  const LaneIdx x = lane_idx(p, tile, lane);
+  if (pend && x.active) {
+    u32x4* const grp = reinterpret_cast<u32x4*>(p.planes + (size_t)tile * (kPlanes * 64u)) + lane;
+    const u32x4 k0 = grp[128], k1 = grp[192];
+    uint32_t Kp[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Kp[i] = k0[i];
+      Kp[4 + i] = k1[i];
+    }
+    const uint32_t P0 = ~Kp[7] & p.valid[x.b];
+    uint32_t cy = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // + pend on count bits 3..6
+      const uint32_t bi = ((pend >> i) & 1u) ? P0 : 0u;
+      const uint32_t t = Kp[3 + i] ^ bi;
+      const uint32_t si = t ^ cy;
+      cy = (t & cy) | (Kp[3 + i] & bi);
+      Kp[3 + i] = si;
+    }
+    u32x4 o0, o1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o0[i] = Kp[i];
+      o1[i] = Kp[4 + i];
+    }
+    grp[128] = o0;
+    grp[192] = o1;
+  }
+  if (lane == 0) p.kpend[tile] = 0u;
+}
+
 template <int K>
 hipError_t occupancy_k(bool replay, int* bpc) {
   return replay ? hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, k_round_sweep<K, kModeReplay, 1>, 256, 0)
@@ -429,6 +557,13 @@ hipError_t launch_vv_materialize(const RoundParams& p, hipStream_t s) {
   if (!p.vstale || !p.pref_prev) return hipErrorInvalidValue;
   const uint32_t tiles = p.Lpad / 64u;
   hipLaunchKernelGGL(k_vv_materialize, dim3((tiles + 3u) / 4u), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_kl_materialize(const RoundParams& p, hipStream_t s) {
+  if (!p.kpend) return hipErrorInvalidValue;
+  const uint32_t tiles = p.Lpad / 64u;
+  hipLaunchKernelGGL(k_kl_materialize, dim3((tiles + 3u) / 4u), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

@@ -337,6 +337,7 @@ def test_c4_shape_properties():
     for kernel, warm_bytes in ((1, 15 * 176), (2, 140 + 14 * 136)):
         e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4)
         e.set_option("kernel", kernel)
+        e.set_option("count_lazy", 0)  # per-lane bytes with stored count planes (test_gpu_count_lazy.py)
         e.init_records(avhip.INIT_BERNOULLI, P80)
         lanes = e.layout_info()["lanes"]
         e.run_rounds(1)  # round 0: consider planes fill up (236 B per 32-record lane)

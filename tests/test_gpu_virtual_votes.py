@@ -96,6 +96,7 @@ def test_virtual_votes_bytes():
     once the tile is stale (7 regathered words instead of the 8 V planes)."""
     n, m = 4000, 1000
     e = avhip.Engine(n, m, k=8, seed=1, log_capacity=1 << 22)
+    e.set_option("count_lazy", 0)  # count planes stored every round (test_gpu_count_lazy.py)
     e.init_records(avhip.INIT_ACCEPTED, 0)
     lanes = e.layout_info()["lanes"]
     e.run_rounds(2)  # round 0 cold; round 1 warm, vv on, nothing stale yet
