@@ -68,7 +68,7 @@ for s in "$@"; do
     calib_write) step calib_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/calib_write -o calib -- \
             go-avalanche_amd/bin/pmc_calib ;;
     pmc_sum) step pmc_sum 120 python tools/pmc_summary.py --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write \
-            --fetch $OUT/pmc_fetch --write $OUT/pmc_write --kernel k_round_sweep --read-x4 32 --read-x1 64 --write-x4 32 --write-x1 8 --out $OUT/pmc_traffic_c4.json ;;
+            --fetch $OUT/pmc_fetch --write $OUT/pmc_write --kernel k_round_sweep --read-x4 14 --read-x1 64 --write-x4 14 --write-x1 6 --out $OUT/pmc_traffic_c4.json ;;
     pmc_sq8) step pmc_sq8 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq8 -o ab -- \
             python3 tools/ab_tune.py --shards 8 --variants sweep_w1,ablate --rounds 3 ;;
     pmc_tcc8) step pmc_tcc8 300 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_tcc8 -o ab -- \
