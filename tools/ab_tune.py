@@ -38,6 +38,7 @@ VARIANTS = {
     "w1_plain": dict(kernel=2, sweep_blocks=0, plane_nt=0),
     "vv0": dict(kernel=2, virtual_votes=0),
     "vv_all": dict(kernel=2, vv_min_bl=1),
+    "kl0": dict(kernel=2, count_lazy=0),
 }
 
 
@@ -72,7 +73,7 @@ def main():
             opts = VARIANTS[v]
             e.set_option("kernel", opts["kernel"])
             e.set_option("ablate_gather", opts.get("ablate_gather", 0))
-            for opt in ("sweep_blocks", "store_policy", "plane_nt", "virtual_votes", "vv_min_bl"):
+            for opt in ("sweep_blocks", "store_policy", "plane_nt", "virtual_votes", "vv_min_bl", "count_lazy"):
                 if opt in opts:
                     e.set_option(opt, opts[opt])
             e.init_records(init_mode, init_param)
