@@ -204,5 +204,71 @@ __device__ __forceinline__ void draw_peers(const RoundParams& p, uint32_t round,
   }
 }
 
+// Both draws a stale vv tile needs (kernels.h vv, k = 8): round - 1's peers
+// (to regather the vote register) and this round's, from ONE Philox pass over
+// the wave: lanes 0-31 produce round - 1's blocks, lanes 32-63 this round's (a
+// tile needs nn * 2 <= 32 producer lanes per draw). The distinctness of a
+// node's 8 candidates is decided on its two producer lanes (own 4 + partner's
+// 4: 6 + 16 compares) and handed out by ballot, instead of 28 compares per
+// draw on every lane. pick_peers then hands one draw to the node's lanes.
+// Same peers as draw_peers.
+struct PairDraw {
+  uint32_t prod[4];
+  unsigned long long bad;  // bit l: producer lane l saw a repeated candidate
+  bool fallback;           // wave-uniform: per-draw draw_peers instead
+};
+
+__device__ __forceinline__ PairDraw pair_draw(const RoundParams& p, uint32_t round, uint32_t nlA, uint32_t nn,
+                                              uint32_t lane) {
+  PairDraw d;
+  const uint32_t others = p.n_nodes - 1u;
+  d.fallback = p.peer_mode == 1 || 8u >= others || nn * 2u > 32u;
+  d.bad = 0ull;
+  if (d.fallback) return d;
+  // opaque copy of the lane index: keeps the compiler from hoisting the
+  // lane-derived Philox counters out of the tile loop and spilling them
+  uint32_t ln = lane;
+  asm volatile("" : "+v"(ln));
+  const uint32_t half = ln >> 5, q = ln & 31u;
+  const uint32_t pnode = p.n0 + nlA + min(q >> 1, nn - 1u);
+  uint32_t x[4];
+  philox(x, p.seed, pnode, round - 1u + half, q & 1u, kDomPeers);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t u = __umulhi(x[i], others);
+    d.prod[i] = u + (u >= pnode ? 1u : 0u);
+  }
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t part = (uint32_t)__shfl((int)d.prod[i], (int)(lane ^ 1u), 64);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ok &= d.prod[j] != part;
+#pragma unroll
+    for (int j = 0; j < i; ++j) ok &= d.prod[i] != d.prod[j];
+  }
+  d.bad = __ballot(!ok);
+  return d;
+}
+
+// which = 0: round - 1's peers, 1: round's (pair_draw's round)
+__device__ __forceinline__ void pick_peers(const RoundParams& p, const PairDraw& d, uint32_t which, uint32_t round,
+                                           uint32_t node, uint32_t nl, uint32_t nlA, uint32_t nn, uint32_t lane,
+                                           uint32_t (&peers)[8]) {
+  const uint32_t r = round - 1u + which;
+  if (d.fallback) {
+    draw_peers<8>(p, r, node, nl, nlA, nn, lane, peers);
+    return;
+  }
+  const uint32_t base = which * 32u + (nl - nlA) * 2u;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) peers[c] = (uint32_t)__shfl((int)d.prod[c & 3], (int)(base + (uint32_t)c / 4u), 64);
+  if ((d.bad >> base) & 3ull) {
+    const PeerList<8> g = sample_peers_general<8>(p.seed, node, r, p.n_nodes, p.peer_mode);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) peers[j] = g.v[j];
+  }
+}
+
 }  // namespace
 }  // namespace avk

@@ -116,21 +116,27 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
     }
   } else {
     const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
+    uint32_t peers[K];
+    bool drawn = false;
     if constexpr (VV) {
       if (in.stale) {
         // the vote register after last round's 8 sim votes is those votes:
         // V_i = (previous round's slot 7 - i vote); V_7 is never read at k = 8
-        uint32_t pp[K];
-        draw_peers<K>(p, p.round - 1u, x.node, x.nl, nlA, nn, lane, pp);
+        const PairDraw pd = pair_draw(p, p.round, nlA, nn, lane);
+        {
+          uint32_t pp[K];
+          pick_peers(p, pd, 0u, p.round, x.node, x.nl, nlA, nn, lane, pp);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) in.v0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
+          for (int i = 0; i < 4; ++i) in.v0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) in.v1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
-        in.v1[3] = 0u;
+          for (int i = 0; i < 3; ++i) in.v1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
+          in.v1[3] = 0u;
+        }
+        pick_peers(p, pd, 1u, p.round, x.node, x.nl, nlA, nn, lane, peers);
+        drawn = true;
       }
     }
-    uint32_t peers[K];
-    draw_peers<K>(p, p.round, x.node, x.nl, nlA, nn, lane, peers);
+    if (!drawn) draw_peers<K>(p, p.round, x.node, x.nl, nlA, nn, lane, peers);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       // ABLATE (timing diagnostics only, results invalid): the node's own row, coalesced

@@ -18,7 +18,8 @@ except Exception:  # pragma: no cover - torch is optional for the binding itself
     torch = None
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libavhip.so")
+# AVHIP_LIB: an alternative build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("AVHIP_LIB") or os.path.join(_PKG_ROOT, "lib", "libavhip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_PKG_ROOT), "include", "avhip.h")
 
 AV_OK = 0
