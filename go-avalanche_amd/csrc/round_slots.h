@@ -176,7 +176,8 @@ __device__ __forceinline__ void draw_peers(const RoundParams& p, uint32_t round,
   bool general = p.peer_mode == 1 || (uint32_t)K >= others || nn * NB > 64u;
   if (!general) {
     // producer lane q draws Philox block q % NB of the tile's node q / NB ...
-    const uint32_t q = lane;
+    uint32_t q = lane;
+    asm volatile("" : "+v"(q));  // opaque: keep the lane-derived counters inside the tile loop
     const uint32_t pnode = p.n0 + nlA + min(q / NB, nn - 1u);
     uint32_t x[4];
     philox(x, p.seed, pnode, round, q % NB, kDomPeers);
@@ -188,14 +189,31 @@ __device__ __forceinline__ void draw_peers(const RoundParams& p, uint32_t round,
     }
     // ... and every lane of that node takes its candidates with ds_bpermute
     const uint32_t base = (nl - nlA) * NB;
-    bool distinct = true;
+    if constexpr (K == 8) {
+      // distinctness on the two producer lanes (own 4 + partner's 4), one ballot
+      bool ok = true;
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-      peers[c] = (uint32_t)__shfl((int)prod[c & 3], (int)(base + (uint32_t)c / 4u), 64);
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t part = (uint32_t)__shfl((int)prod[i], (int)(q ^ 1u), 64);
 #pragma unroll
-      for (int d = 0; d < c; ++d) distinct &= peers[c] != peers[d];
+        for (int j = 0; j < 4; ++j) ok &= prod[j] != part;
+#pragma unroll
+        for (int j = 0; j < i; ++j) ok &= prod[i] != prod[j];
+      }
+      const unsigned long long bad = __ballot(!ok);
+#pragma unroll
+      for (int c = 0; c < K; ++c) peers[c] = (uint32_t)__shfl((int)prod[c & 3], (int)(base + (uint32_t)c / 4u), 64);
+      general = ((bad >> base) & 3ull) != 0ull;
+    } else {
+      bool distinct = true;
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        peers[c] = (uint32_t)__shfl((int)prod[c & 3], (int)(base + (uint32_t)c / 4u), 64);
+#pragma unroll
+        for (int d = 0; d < c; ++d) distinct &= peers[c] != peers[d];
+      }
+      general = !distinct;
     }
-    general = !distinct;
   }
   if (general) {
     const PeerList<K> r = sample_peers_general<K>(p.seed, node, round, p.n_nodes, p.peer_mode);
