@@ -14,16 +14,34 @@ metric : vote-record updates/s = regsiterVote applications on live records
          (vote.go:54) per second, whole job (all ranks). triples/s (node, target,
          round) = updates/s / k is reported beside it.
 workload : C4 of BASELINE.json (the north_star's 1M nodes x 1k targets) — k=8,
-         IsAccepted() ~ Bernoulli(0.8), honest, synthetic (seeded), rounds
-         W..W+K-1 (< 17: every record stays live). With N GPUs the same network
-         is split by target blocks (no per-round exchange; strong scaling) or,
-         with --shard nodes, by nodes with an RCCL all-gather of the published
-         preferences every round. At N=1 the line also carries configs[1] (C2:
-         replayed vote streams, 4096 poll cap binding) under "secondary".
+         IsAccepted() ~ Bernoulli(0.8), honest, synthetic (seeded).
+window : BASELINE.md fixes C4 at its all-live rounds (no record can finalize
+         before round 16 at k = 8: 7 warm-up votes + 128 agreeing ones). The
+         step sequence is therefore a chain of 16-round *epochs*: step p is
+         round p % 16 of a fresh network, the records re-initialised (untimed,
+         outside the timed segments) at every epoch start. `--warmup W` runs
+         steps 0..W-1 untimed, `--steps K` times steps W..W+K-1 — whatever W
+         and K are, every timed round has every record live. A timed stretch
+         that crosses an epoch boundary is timed as two segments, each
+         bracketed by barrier + synchronize; their times add up.
+         Every StatusUpdate of the timed rounds is stored in the device log
+         (sized for the window); an overflow is a hard failure (exit 3, no
+         number printed).
+multi-GPU : N ranks split the same network (strong scaling): node shards with
+         the peer-push exchange (default) or an RCCL all-gather, or target
+         shards.
+
+The line carries the round kernel's roofline: SURVEY.md
+§8(d)'s algorithmic bytes per launch (9.125 B per live (node, target, round)
++ 20 B per StatusUpdate) over the kernel's HIP-event time, the bytes the
+bit-sliced kernel actually moves, and — from the committed rocprofv3 PMC
+summary of this bench window and these kernel sources, when it matches — the
+HBM traffic and the instruction-issue fractions that bind the round.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -42,6 +60,9 @@ from avhip import sharding  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 P80 = int(0.8 * 2**32)
 BYZ20 = int(0.2 * 2**32)
+EPOCH = 16  # all-live rounds of a fresh network at k = 8 (finalization needs >= 134 votes)
+S8D_TRIPLE_BYTES = {False: 9.125, True: 10.125}  # sim / replay, per live (node, target, round)
+S8D_UPDATE_BYTES = 20.0                           # per emitted StatusUpdate
 
 WORKLOADS = {
     # name: (nodes, targets, k, init_mode, init_param, byz_threshold, replay, description)
@@ -55,19 +76,26 @@ WORKLOADS = {
            "C5: 10M nodes x 256 targets, k=8, Bernoulli(0.8), honest"),
 }
 
-
 PARALLELISM = {
     "peers": "node-sharded, changed preference words pushed to peers over xGMI + device barrier per round",
     "nodes": "node-sharded, RCCL all-gather of preference rows per round",
     "targets": "target-sharded, no exchange",
 }
 
+KERNEL_SRC = [os.path.join(ROOT, "go-avalanche_amd", "csrc", f) for f in
+              ("round_sweep.hip", "round_node.hip", "kernels.hip", "round_common.h", "round_slots.h", "kernels.h",
+               "engine.cpp")]
+
+
+class BenchFailure(SystemExit):
+    pass
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=14)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
     # peers: node shards + peer-push exchange; nodes: node shards +
     # RCCL all-gather of the preference rows; targets: target shards, no exchange
@@ -81,138 +109,219 @@ def parse():
                     help="round kernel generation (A/B only; default: the engine's choice)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="N>1 rehearsal on a 1-GPU box: every rank on device 0, gloo for the host-side "
-                         "barrier/reductions (target sharding only; not a measurement)")
+                         "barrier/reductions (not a measurement)")
+    ap.add_argument("--no-roofline-pass", action="store_true",
+                    help="skip the HIP-event pass (rocprofv3 PMC runs: one window only)")
     return ap.parse_args()
 
 
+def src_digest():
+    h = hashlib.sha256()
+    for p in KERNEL_SRC:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(wl, seed, budget_s):
-    """Oracle ("port": C restatement of the reference semantics) on host cores,
-    on a bounded sample of the same workload: fewer nodes, same targets/k."""
+    """Oracle ("port": the C restatement of the reference semantics,
+    oracle/avalanche_oracle.c) on host cores, on a bounded sample of the same
+    workload: fewer nodes, same targets/k, the same all-live rounds."""
     from oracle import cabi
 
     n, m, k, init_mode, init_param, byz, replay, _ = WORKLOADS[wl]
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    threads = max(1, min(threads, 16, avail))
     ns = min(n, 80000 if wl != "c2" else 400)
-    sim = cabi.Sim(ns, m, k, seed=seed, byz_threshold=byz, init_mode=init_mode, init_param=init_param)
+    sim = cabi.Sim(ns, m, k, seed=seed, byz_threshold=byz, init_mode=init_mode, init_param=init_param,
+                   threads=threads)
     applied = 0
     dt = 0.0
     rounds = 0
-    while dt < budget_s and rounds < 16:
+    while dt < budget_s and rounds < EPOCH:
         errs = cabi.gen_replay_errs(seed, rounds, 0, ns, m, k) if replay else None  # input, untimed
         ts = time.perf_counter()
-        _, a = sim.run_round(errs, threads=threads)
+        _, a = sim.run_round(errs, threads=threads, collect=False)
         dt += time.perf_counter() - ts
         applied += a
         rounds += 1
     sim.close()
     return {"value": applied / dt, "unit": "vote-record updates/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/avalanche_oracle.c Sim, {ns} nodes x {m} targets, k={k}, {rounds} rounds "
-                      f"({applied} regsiterVote applications, {dt:.1f}s, OpenMP over nodes)"}
+            "cpu_model": cpu_model(),
+            "sample": f"oracle/avalanche_oracle.c (C restatement of vote.go/processor.go, the parity oracle), "
+                      f"{ns} nodes x {m} targets, k={k}, rounds 0..{rounds - 1} ({applied} regsiterVote "
+                      f"applications, {dt:.1f}s, OpenMP over nodes, {threads} threads on {cpu_model()})"}
+
+
+class Runner:
+    """One engine (this rank's shard of a workload) stepped through the epoch
+    chain: step p is round p % EPOCH of a fresh network."""
+
+    def __init__(self, wl, args, world, rank, local_rank, log_capacity):
+        self.wl = wl
+        n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
+        self.n, self.m, self.k, self.replay, self.desc = n, m, k, replay, desc
+        self.init = (init_mode, init_param)
+        self.world, self.rank = world, rank
+        if args.shard == "targets" and world > 1 and m > 4096:
+            raise SystemExit("target sharding needs M <= 4096 (poll cap couples targets); use --shard nodes")
+        kw = dict(k=k, seed=args.seed, byz_threshold=byz, device=local_rank)
+        if world > 1 and args.shard == "targets":
+            kw["target_range"] = sharding.target_shard(m, world, rank)
+        elif world > 1:
+            kw["node_range"] = sharding.node_shard(n, world, rank)
+        self.eng = eng = avhip.Engine(n, m, log_capacity=log_capacity, **kw)
+        if args.plane_nt is not None:
+            eng.set_option("plane_nt", args.plane_nt)
+        if args.kernel is not None:
+            eng.set_option("kernel", args.kernel)
+        eng.init_records(*self.init)
+        self.pos = 0  # step index of the next round
+        self.shard = args.shard
+        self.fallback = None
+        if world > 1 and args.shard == "nodes":
+            obj = [avhip.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            eng.comm_init(world, rank, obj[0])
+        elif world > 1 and args.shard == "peers":
+            # map every rank's preference snapshots (IPC over xGMI); if any rank
+            # cannot, every rank falls back to target sharding (same network)
+            blobs = [None] * world
+            dist.all_gather_object(blobs, eng.peer_handles())
+            err = None
+            try:
+                eng.peer_init(world, rank, blobs)
+            except avhip.AvError as ex:
+                err = repr(ex)[:200]
+            errs = [None] * world
+            dist.all_gather_object(errs, err)
+            if any(errs):
+                eng.close()
+                self.fallback = next(e for e in errs if e)
+        self.info = eng.layout_info() if self.fallback is None else None
+
+    def close(self):
+        self.eng.close()
+
+    def reset(self):
+        """Start a fresh epoch (untimed): records re-initialised, log emptied."""
+        self.eng.synchronize()
+        self.eng.discard_updates()
+        self.eng.init_records(*self.init)
+        self.pos = 0
+
+    def _run(self, rounds):
+        if self.replay:
+            self.eng.replay_prepare(rounds)  # untimed: callers prepare before a timed segment
+            self.eng.replay_rounds(rounds)
+        else:
+            self.eng.run_rounds(rounds)
+
+    def steps(self, count, timed):
+        """Run `count` steps from the current position. timed: every segment
+        inside one epoch is bracketed by barrier + synchronize and its wall
+        time summed. Returns (seconds, applied, emitted, segments)."""
+        eng = self.eng
+        elapsed, applied, emitted, segs = 0.0, 0, 0, 0
+        while count > 0:
+            if self.pos % EPOCH == 0 and self.pos > 0:
+                self.reset()
+            seg = min(EPOCH - self.pos % EPOCH, count)
+            eng.synchronize()
+            eng.discard_updates()
+            a0 = eng.applied_votes()
+            if self.replay:
+                eng.replay_prepare(seg)
+            if timed:
+                if self.world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            if self.replay:
+                eng.replay_rounds(seg)
+            else:
+                eng.run_rounds(seg)
+            if timed:
+                eng.synchronize()
+                torch.cuda.synchronize()
+                if self.world > 1:
+                    dist.barrier()
+                elapsed += time.perf_counter() - t0
+            else:
+                eng.synchronize()
+            if eng.log_overflowed():
+                raise BenchFailure(f"bench: StatusUpdate log overflowed in {self.wl} steps "
+                                   f"{self.pos}..{self.pos + seg - 1}: updates were not stored; no number reported")
+            emitted += eng.updates_count()
+            applied += eng.applied_votes() - a0
+            self.pos += seg
+            count -= seg
+            segs += 1
+        return elapsed, applied, emitted, segs
+
+    def goto(self, pos):
+        """Untimed: bring the engine to step `pos` of a fresh chain."""
+        self.reset()
+        self.steps(pos, timed=False)
 
 
 def measure(wl, args, world, rank, local_rank, steps, warmup):
-    """Build the workload's engine (this rank's shard), run `warmup` untimed and
-    `steps` timed rounds; return whole-job numbers (max time, summed work) and
-    rank-local kernel numbers."""
+    """This rank's shard of workload `wl`: device warm-up (one untimed epoch),
+    `warmup` untimed steps, `steps` timed steps; then a second pass over the
+    same steps with HIP events around every round kernel (roofline)."""
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
-    if args.shard == "targets" and world > 1 and m > 4096:
-        raise SystemExit("target sharding needs M <= 4096 (poll cap couples targets); use --shard nodes")
-    kw = dict(k=k, seed=args.seed, byz_threshold=byz, device=local_rank)
-    if world > 1 and args.shard == "targets":
-        kw["target_range"] = sharding.target_shard(m, world, rank)
-    elif world > 1:
-        kw["node_range"] = sharding.node_shard(n, world, rank)
-    # StatusUpdates per timed round reach ~15% of the records under C3's flip-flop voters
-    est_updates = int((1.0 if byz else 0.25) * n * m) + (1 << 20)
-    eng = avhip.Engine(n, m, log_capacity=min(est_updates, 1 << 29), **kw)
-    if args.plane_nt is not None:
-        eng.set_option("plane_nt", args.plane_nt)
-    if args.kernel is not None:
-        eng.set_option("kernel", args.kernel)
-    eng.init_records(init_mode, init_param)
-    if world > 1 and args.shard == "nodes":
-        obj = [avhip.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        eng.comm_init(world, rank, obj[0])
-    elif world > 1 and args.shard == "peers":
-        # map every rank's preference snapshots (IPC over xGMI); if any rank
-        # cannot, every rank falls back to target sharding (same network)
-        blobs = [None] * world
-        dist.all_gather_object(blobs, eng.peer_handles())
-        err = None
-        try:
-            eng.peer_init(world, rank, blobs)
-        except avhip.AvError as ex:
-            err = repr(ex)[:200]
-        errs = [None] * world
-        dist.all_gather_object(errs, err)
-        if any(errs):
-            eng.close()
-            args.shard = "targets"
-            args.shard_fallback = next(e for e in errs if e)
-            return measure(wl, args, world, rank, local_rank, steps, warmup)
-    if replay:  # both passes' rounds (the roofline pass re-runs warmup + steps)
-        eng.replay_prepare(3 * (warmup + steps))
-    run = eng.replay_rounds if replay else eng.run_rounds
-    info = eng.layout_info()
-
+    # the log holds every StatusUpdate of one epoch segment (~0.2 N*M at most in
+    # the all-live rounds of these workloads: C4 rounds 0-1 ~1e8 each, C3 ~3e7 per
+    # round); 16 B of device memory per entry (singles + dense records)
+    log_cap = min(int(0.5 * n * m) + (1 << 20), 1 << 31)
+    run = Runner(wl, args, world, rank, local_rank, log_cap)
+    if run.fallback is not None:
+        args.shard = "targets"
+        args.shard_fallback = run.fallback
+        return measure(wl, args, world, rank, local_rank, steps, warmup)
+    eng = run.eng
     # ---- device warm-up (untimed): after process start the GPU runs these
-    # kernels up to ~15 % slower for the first ~20-30 ms of sustained load,
-    # whatever the launch pattern (tools/gap_probe.py --events-first, DESIGN.md
-    # §4); one untimed pass of the same rounds, then the records start over
-    run(warmup + steps)
-    eng.synchronize()
-    eng.discard_updates()
-    eng.init_records(init_mode, init_param)
+    # kernels up to ~15 % slower for the first ~20-30 ms of sustained load
+    # (tools/gap_probe.py --events-first, DESIGN.md §4): one untimed epoch
+    run.steps(EPOCH, timed=False)
+    # ---- warmup steps (untimed), then the timed steps
+    run.goto(warmup)
+    elapsed, applied, emitted, segs = run.steps(steps, timed=True)
 
-    # ---- warmup (untimed), then empty the StatusUpdate log. Discarded on the
-    # device, not fetched: sorting round 0-1's ~10^8 updates on the host took
-    # ~4.7 s, long enough for the idle GPU to lose the warm-up above (the timed
-    # rounds then ran at 0.70-0.82 ms instead of 0.65; profiles/r01 trace)
-    run(warmup)
-    eng.synchronize()
-    eng.discard_updates()
-    applied0 = eng.applied_votes()
-
-    # ---- timed region (no per-launch events: their queue packets add ~10 us between kernels)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(steps)
-    eng.synchronize()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    log_overflow = eng.log_overflowed()  # updates past the device log's capacity were counted, not stored
-    applied = eng.applied_votes() - applied0
-    emitted = eng.updates_count()
-
-    # ---- roofline pass: the same work again (records re-initialized, warmup,
-    # `steps` rounds), every launch bracketed by HIP events on the engine's stream
-    eng.discard_updates()
-    eng.init_records(init_mode, init_param)
-    run(warmup)
-    eng.synchronize()
-    eng.discard_updates()
-    bytes1 = eng.alg_bytes()
-    eng.set_timing(True)
-    run(steps)
-    eng.synchronize()
-    eng.set_timing(False)
-    kern_ms, launches = eng.kernel_stats()
-    # algorithmic bytes per launch, counted by the round kernel itself (planes
-    # actually streamed, gathered vote words, published words, StatusUpdates)
-    alg_bytes = (eng.alg_bytes() - bytes1) / max(launches, 1)
-    kavg_ms = kern_ms / max(launches, 1)
+    # ---- roofline pass: the same steps again, every round kernel bracketed by
+    # HIP events on the engine's stream
+    kern_ms = launches = 0
+    moved = 0
+    if not args.no_roofline_pass:
+        run.goto(warmup)
+        b0 = eng.alg_bytes()
+        eng.set_timing(True)
+        _, applied2, emitted2, _ = run.steps(steps, timed=False)
+        eng.set_timing(False)
+        kern_ms, launches = eng.kernel_stats()
+        moved = eng.alg_bytes() - b0
+        if (applied2, emitted2) != (applied, emitted):
+            raise BenchFailure(f"bench: roofline pass differs from the timed pass ({applied2}, {emitted2}) vs "
+                               f"({applied}, {emitted})")
     replicas = None
     if world > 1 and args.shard in ("peers", "nodes"):
         # every rank's replica of the published preferences must be the same:
         # hash a slice of every rank's node range as this rank sees it
-        import hashlib
-
         hs = hashlib.sha256()
         for r in range(world):
             a = sharding.node_shard(n, world, r)[0]
@@ -220,7 +329,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         digests = [None] * world
         dist.all_gather_object(digests, hs.hexdigest())
         replicas = len(set(digests)) == 1
-    eng.close()
+    info = run.info
+    run.close()
 
     if world > 1:
         st = torch.tensor([elapsed, float(applied), float(emitted)], dtype=torch.float64,
@@ -229,20 +339,22 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tot = st[1:3].clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        elapsed, applied, emitted = float(tmax), float(tot[0]), float(tot[1])
-    value = applied / elapsed
-    # roofline of this rank's round kernel: algorithmic bytes per
-    # launch as counted by the kernel (per 32-record lane at k=8: 236 B cold,
-    # 172 B warm, 136 B with recomputed vote registers; + the StatusUpdate log)
-    # / its HIP-event average launch time.
-    achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
+        elapsed, applied_all, emitted_all = float(tmax), float(tot[0]), float(tot[1])
+    else:
+        applied_all, emitted_all = applied, emitted
+    kavg_ms = kern_ms / launches if launches else None
     gen2 = k <= 8 and args.kernel != 1
     kname = (("k_round_node" if gen2 else "k_round_capped") if info["capped"]
              else ("k_round_sweep" if gen2 else "k_round_fast")) + f"<{k},{'true' if replay else 'false'}>"
+    # SURVEY.md §8(d) bytes of this rank's launches: every applied vote is one
+    # live (node, target, round) triple / k; + 20 B per emitted StatusUpdate
+    s8d = (applied / k * S8D_TRIPLE_BYTES[replay] + emitted * S8D_UPDATE_BYTES) / launches if launches else None
     return {
-        "desc": desc, "n": n, "m": m, "k": k, "value": value, "elapsed": elapsed, "applied": applied,
-        "emitted": emitted, "info": info, "kavg_ms": kavg_ms, "alg_bytes": alg_bytes, "achieved": achieved,
-        "kernel": kname, "log_overflow": log_overflow, "replicas_identical": replicas,
+        "wl": wl, "desc": desc, "n": n, "m": m, "k": k, "elapsed": elapsed, "applied": applied_all,
+        "emitted": emitted_all, "value": applied_all / elapsed, "segments": segs, "info": info,
+        "kavg_ms": kavg_ms, "launches": launches, "s8d_bytes": s8d,
+        "moved_bytes": moved / launches if launches else None, "kernel": kname, "replicas_identical": replicas,
+        "first_round": warmup % EPOCH,
     }
 
 
@@ -266,10 +378,49 @@ def allgather_probe(world, local_rank, total_bytes=1_000_000 * 128, reps=5):
             "note": "C4 node-sharded round exchange (1M x 1000 bits), torch.distributed all_gather_into_tensor"}
 
 
-def roofline(r, traffic=None):
-    return {"bound": "hbm", "achieved": r["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": r["achieved"] / HBM_PEAK_GBS, "traffic": traffic, "kernel": r["kernel"],
-            "kernel_ms_avg": r["kavg_ms"], "alg_bytes_per_launch": r["alg_bytes"]}
+def load_pmc(wl, window, world):
+    """The committed rocprofv3 PMC summary of this bench window (tools/
+    pmc_summary.py), used only if it was measured on these kernel sources."""
+    path = os.path.join(ROOT, "profiles", "r02", f"pmc_{wl}.json")
+    if world != 1 or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    if d.get("src_sha") != src_digest() or d.get("window") != window:
+        return None
+    return d
+
+
+def roofline(r, window=None, world=1):
+    """Roofline of the round kernel. achieved/frac: SURVEY.md
+    §8(d)'s algorithmic bytes per launch / the HIP-event launch time. The
+    bit-sliced kernel moves fewer bytes than that 4-B-per-record model, so frac
+    can exceed 1; bytes_moved is what the kernel actually streams and gathers.
+    pmc (when the committed profile matches the sources and window): the HBM
+    traffic from FETCH_SIZE/WRITE_SIZE and the instruction-issue fractions."""
+    if r["kavg_ms"] is None:
+        return None
+    t = r["kavg_ms"] * 1e-3
+    ach = r["s8d_bytes"] / t / 1e9
+    out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+           "traffic": None, "kernel": r["kernel"], "kernel_ms_avg": r["kavg_ms"], "launches": r["launches"],
+           "alg_bytes_s8d": r["s8d_bytes"],
+           "bytes_moved": r["moved_bytes"], "frac_moved": r["moved_bytes"] / t / 1e9 / HBM_PEAK_GBS,
+           "note": "achieved = SURVEY.md §8(d) bytes (9.125 B per live node-target-round + 20 B per "
+                   "StatusUpdate) / kernel time; the bit-sliced kernel moves bytes_moved instead (DESIGN.md §3)"}
+    pmc = load_pmc(r["wl"], window, world) if window else None
+    if pmc:
+        out["traffic"] = pmc.get("hbm_bytes_per_launch")
+        if pmc.get("issue"):
+            iss = pmc["issue"]
+            out["issue"] = iss
+            # the binding resource: whichever of HBM traffic / VALU issue / SALU issue is closest to its peak
+            cands = {"hbm": (out["traffic"] or 0) / t / 1e9 / HBM_PEAK_GBS,
+                     "valu_issue": iss.get("frac_valu", 0.0), "salu_issue": iss.get("frac_salu", 0.0)}
+            out["binding"] = max(cands, key=cands.get)
+            out["binding_fracs"] = cands
+        out["pmc_source"] = pmc.get("source")
+    return out
 
 
 def main():
@@ -289,29 +440,35 @@ def main():
     elif world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    r = measure(args.workload, args, world, rank, local_rank, args.steps, args.warmup)
-    secondary = None
-    if world > 1 and not args.rehearse_one_gpu and not args.no_secondary:
-        # the exchange a node-sharded C4 round would need: every rank's published-
-        # preference rows (N/G x 128 B) all-gathered over xGMI (RCCL through
-        # torch.distributed); recorded for the node- vs target-sharding choice
-        # (DESIGN.md §5), not part of the timed value
-        try:
-            secondary = {"xgmi_allgather": allgather_probe(world, local_rank)}
-        except Exception as exc:  # a diagnostic: never costs the measured line
-            secondary = {"xgmi_allgather": {"error": repr(exc)[:200]}}
-    if world == 1 and not args.no_secondary and args.workload != "c2":
-        c2 = measure("c2", args, world, rank, local_rank, 14, 2)
-        secondary = {"c2": {"workload": c2["desc"], "value": c2["value"], "unit": "vote-record updates/s",
-                            "ms_per_step": c2["elapsed"] / 14 * 1e3, "rounds": "2..15",
-                            "roofline": roofline(c2)}}
+    try:
+        r = measure(args.workload, args, world, rank, local_rank, args.steps, args.warmup)
+        secondary = {}
+        if not args.no_secondary:
+            if world > 1 and not args.rehearse_one_gpu:
+                # the exchange a node-sharded C4 round would need with an all-gather:
+                # every rank's published-preference rows (N/G x 128 B) over xGMI
+                # (RCCL through torch.distributed); a diagnostic, not the timed value
+                try:
+                    secondary["xgmi_allgather"] = allgather_probe(world, local_rank)
+                except Exception as exc:
+                    secondary["xgmi_allgather"] = {"error": repr(exc)[:200]}
+            others = ["c3"] + (["c2"] if world == 1 else [])
+            for wl in others:
+                if wl == args.workload:
+                    continue
+                s = measure(wl, args, world, rank, local_rank, args.steps, args.warmup)
+                secondary[wl] = {"workload": s["desc"], "value": s["value"], "unit": "vote-record updates/s",
+                                 "ms_per_step": s["elapsed"] / args.steps * 1e3, "updates_emitted": int(s["emitted"]),
+                                 "rounds": f"steps {args.warmup}..{args.warmup + args.steps - 1} of 16-round epochs",
+                                 "roofline": roofline(s, f"{args.warmup}+{args.steps}", world)}
+    except BenchFailure as ex:
+        if rank == 0:
+            print(str(ex), file=sys.stderr, flush=True)
+        raise SystemExit(3)
 
     if rank == 0:
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
-        if world == 1 and os.path.exists(pmc_path):
-            with open(pmc_path) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+        window = f"{args.warmup}+{args.steps}"
+        first = r["first_round"]
         line = {
             "metric": "vote-record updates/sec (node·target·round) at 1/2/4/8 GPU; % HBM roofline",
             "value": r["value"],
@@ -319,7 +476,6 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "device_warmup_rounds": args.warmup + args.steps,
             "ms_per_step": r["elapsed"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
@@ -329,15 +485,17 @@ def main():
             "config": {
                 "workload": r["desc"],
                 "n_nodes": r["n"], "n_targets": r["m"], "k": r["k"],
-                "rounds": f"{args.warmup}..{args.warmup + args.steps - 1}",
+                "rounds": f"steps {args.warmup}..{args.warmup + args.steps - 1} = round (step % 16) of 16-round "
+                          f"epochs (all records live; records re-initialised untimed at each epoch start); "
+                          f"timed rounds start at round {first}, {r['segments']} timed segment(s)",
                 "parallelism": (PARALLELISM[args.shard] + f" x{world}") if world > 1 else "single GPU",
                 "layout": "bit-sliced: 25 u32 planes per 32 records; tile of 64 lanes contiguous",
                 "capped_poll_path": r["info"]["capped"],
             },
             "triples_per_s": r["value"] / r["k"],
             "updates_emitted": int(r["emitted"]),
-            "update_log_overflow": r["log_overflow"],
-            "roofline": roofline(r, traffic),
+            "update_log_overflow": False,
+            "roofline": roofline(r, window, world),
         }
         if r["replicas_identical"] is not None:
             line["config"]["replicas_identical"] = r["replicas_identical"]

@@ -138,12 +138,26 @@ struct av_engine {
   int peer_world = 0, peer_rank = 0;
   uint32_t* peer_pref[3][avk::kMaxPeers + 1] = {};  // [buffer][rank]; own rank = the local buffer
   uint32_t* arrive = nullptr;                        // [kMaxPeers + 1] arrival slots (local)
-  uint32_t* barrier_err = nullptr;
+  // barrier timeout flag in pinned host memory (the barrier kernel stores it
+  // with system scope): the host reads it without synchronizing the stream
+  uint32_t* barrier_err = nullptr;                   // device view of barrier_err_host
+  volatile uint32_t* barrier_err_host = nullptr;
+  bool failed = false;                               // sticky: a peer barrier timed out
+  bool peer_fine = true;  // option "peer_fine": snapshot buffers fine-grained once exported (xGMI coherence)
+  size_t pref_alloc_words = 0;
   uint32_t barrier_seq = 0;
   uint32_t barrier_timeout_ms = 30000;
   std::vector<void*> peer_opened;                    // IPC mappings to close
   avk::PeerPtrs peer_arrive{};
   uint32_t** push_tbl = nullptr;                     // device [3][kMaxPeers]: peers' replicas of each buffer
+
+  // per-local-node Processor.round (processor.go:15,40-42): a field only the
+  // caller changes (avalanche_test.go:302); allocated on the first set
+  std::vector<int64_t> proc_round;
+  // device scratch kept across calls (StatusUpdate delivery, digests)
+  void* fetch_scratch = nullptr;
+  size_t fetch_scratch_bytes = 0;
+  unsigned long long* digest = nullptr;  // [3]
 
   size_t round_replay_words() const { return (size_t)k * 2 * Lpad; }
 };
@@ -284,6 +298,47 @@ int peer_local_write_check(const av_engine* e) {
   return AV_OK;
 }
 
+// A peer barrier that timed out (a rank stopped taking part) leaves the
+// ranks' snapshot replicas unordered: every later round and every result of
+// this engine is refused (sticky), AV_ERR_PEER.
+int peer_failed(av_engine* e) {
+  if (e->peer_world > 1 && !e->failed && e->barrier_err_host && *e->barrier_err_host) e->failed = true;
+  if (e->failed)
+    return fail(AV_ERR_PEER, "peer barrier timed out (a rank stopped taking part in the rounds): the exchange is "
+                             "broken, results of this engine are invalid");
+  return AV_OK;
+}
+
+#define AV_PEER_CHECK(e)          \
+  do {                            \
+    int _rc = peer_failed(e);     \
+    if (_rc != AV_OK) return _rc; \
+  } while (0)
+
+// For calls that return results: every round enqueued so far (and its
+// barrier) completes first, then the flag decides.
+#define AV_PEER_SYNC_CHECK(e)                                      \
+  do {                                                             \
+    if ((e)->peer_world > 1) AV_HIP(hipStreamSynchronize((e)->stream)); \
+    int _rc = peer_failed(e);                                      \
+    if (_rc != AV_OK) return _rc;                                  \
+  } while (0)
+
+// Growable device scratch owned by the engine.
+int engine_scratch(av_engine* e, size_t bytes, void** out) {
+  if (bytes > e->fetch_scratch_bytes) {
+    if (e->fetch_scratch) AV_HIP(hipFree(e->fetch_scratch));
+    e->fetch_scratch = nullptr;
+    e->fetch_scratch_bytes = 0;
+    hipError_t he = hipMalloc(&e->fetch_scratch, bytes);
+    AV_CHECK(he == hipSuccess, he == hipErrorOutOfMemory ? AV_ERR_OOM : AV_ERR_HIP, "scratch (%zu B): %s", bytes,
+             hipGetErrorString(he));
+    e->fetch_scratch_bytes = bytes;
+  }
+  *out = e->fetch_scratch;
+  return AV_OK;
+}
+
 int launch_one_round(av_engine* e, const uint32_t* replay) {
   AV_CHECK(e->round - e->log_base < 4096, AV_ERR_OVERFLOW,
            "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
@@ -416,6 +471,7 @@ const char* av_strerror(int code) {
     case AV_ERR_OVERFLOW: return "buffer overflow";
     case AV_ERR_UNSUPPORTED: return "unsupported configuration";
     case AV_ERR_RCCL: return "RCCL error";
+    case AV_ERR_PEER: return "peer exchange failed";
     default: return "unknown error";
   }
 }
@@ -433,7 +489,9 @@ int av_destroy(av_engine* e) {
   if (e->comm) (void)ncclCommDestroy(e->comm);
   for (void* m : e->peer_opened) (void)hipIpcCloseMemHandle(m);
   if (e->arrive) (void)hipFree(e->arrive);
-  if (e->barrier_err) (void)hipFree(e->barrier_err);
+  if (e->barrier_err_host) (void)hipHostFree(const_cast<uint32_t*>(e->barrier_err_host));
+  if (e->fetch_scratch) (void)hipFree(e->fetch_scratch);
+  if (e->digest) (void)hipFree(e->digest);
   if (e->push_tbl) (void)hipFree(e->push_tbl);
   if (e->marker) (void)hipEventDestroy(e->marker);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->kpend, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
@@ -509,6 +567,7 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->planes, plane_words)) != hipSuccess) return hip_fail(he, "alloc planes");
   // whole 2-MiB units: each snapshot buffer is an allocation of its own (IPC export, av_peer_handles)
   const size_t pref_alloc = ((pref_words * 4 + (2u << 20) - 1) / (2u << 20)) * (2u << 20) / 4;
+  e->pref_alloc_words = pref_alloc;
   if ((he = dev_alloc(&e->pref[0], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->pref[1], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->pref[2], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
@@ -756,21 +815,24 @@ int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const 
 
 int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint32_t* out) {
   AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
   AV_CHECK(out && n0 >= e->n0 && n0 <= n1 && n1 <= e->n1 && t0 >= e->t0 && t0 <= t1 && t1 <= e->t1,
            AV_ERR_INVALID_ARG, "range outside this engine's shard");
-  {
-    int rc = materialize_votes(e);
-    if (rc != AV_OK) return rc;
-  }
   const size_t n = (size_t)(n1 - n0) * (size_t)(t1 - t0);
   if (!n) return AV_OK;
-  Scratch s;
-  AV_HIP(s.ensure(n * 4));
-  AV_HIP(avk::launch_read_records(e->planes, e->BL, (uint32_t)(n0 - e->n0), (uint32_t)(n1 - e->n0),
-                                  (uint32_t)(t0 - e->t0), (uint32_t)(t1 - e->t0), static_cast<uint32_t*>(s.p),
-                                  e->stream));
-  AV_HIP(hipMemcpyAsync(out, s.p, n * 4, hipMemcpyDeviceToHost, e->stream));
+  // the deferred forms (stale vote planes, pending count steps) are read
+  // through, not written back: a read leaves the next round's fast paths on
+  avk::RoundParams p = round_params(e, nullptr);
+  p.vv = e->v_stale ? 1u : 0u;
+  p.klazy = e->k_pend ? 1u : 0u;
+  void* buf = nullptr;
+  int rc = engine_scratch(e, n * 4, &buf);
+  if (rc != AV_OK) return rc;
+  AV_HIP(avk::launch_read_records_virtual(p, (uint32_t)(n0 - e->n0), (uint32_t)(n1 - e->n0), (uint32_t)(t0 - e->t0),
+                                          (uint32_t)(t1 - e->t0), static_cast<uint32_t*>(buf), e->stream));
+  AV_HIP(hipMemcpyAsync(out, buf, n * 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
+  AV_PEER_CHECK(e);
   return AV_OK;
 }
 
@@ -803,7 +865,7 @@ int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t
 }
 
 int av_is_accepted(av_engine* e, int64_t node, int64_t target, int32_t* out) {
-  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(e && out, AV_ERR_INVALID_ARG, "null argument");
   *out = 0;
   if (!local_node(e, node) || !local_target(e, target)) return AV_OK;  // no record -> false
   uint32_t w = 0;
@@ -814,7 +876,7 @@ int av_is_accepted(av_engine* e, int64_t node, int64_t target, int32_t* out) {
 }
 
 int av_get_confidence(av_engine* e, int64_t node, int64_t target, uint16_t* out) {
-  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(e && out, AV_ERR_INVALID_ARG, "null argument");
   if (!local_node(e, node) || !local_target(e, target)) return fail(AV_ERR_NOT_FOUND, "VoteRecord not found");
   uint32_t w = 0;
   int rc = av_read_records(e, node, node + 1, target, target + 1, &w);
@@ -825,7 +887,7 @@ int av_get_confidence(av_engine* e, int64_t node, int64_t target, uint16_t* out)
 }
 
 int av_get_invs(av_engine* e, int64_t node, int64_t* out_targets, int64_t cap, int64_t* n_out) {
-  AV_CHECK(n_out && (cap == 0 || out_targets), AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(e && n_out && (cap == 0 || out_targets), AV_ERR_INVALID_ARG, "null argument");
   *n_out = 0;
   AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node not in this shard");
   std::vector<uint32_t> w((size_t)(e->t1 - e->t0));
@@ -847,6 +909,7 @@ int av_get_invs(av_engine* e, int64_t node, int64_t* out_targets, int64_t cap, i
 int av_get_invs_batch(av_engine* e, int64_t n0, int64_t n1, int64_t* offsets, int32_t* targets, int64_t cap,
                       int64_t* total) {
   AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
   AV_CHECK(offsets && total && (cap == 0 || targets), AV_ERR_INVALID_ARG, "null argument");
   AV_CHECK(n0 >= e->n0 && n0 <= n1 && n1 <= e->n1, AV_ERR_INVALID_ARG, "node range outside this engine's shard");
   const uint32_t n = (uint32_t)(n1 - n0);
@@ -878,6 +941,7 @@ int av_get_invs_batch(av_engine* e, int64_t n0, int64_t n1, int64_t* offsets, in
 
 int av_run_rounds(av_engine* e, int32_t rounds) {
   AV_ENTER(e);
+  AV_PEER_CHECK(e);
   AV_CHECK(rounds >= 0, AV_ERR_INVALID_ARG, "rounds < 0");
   for (int32_t r = 0; r < rounds; ++r) {
     int rc = launch_one_round(e, nullptr);
@@ -888,6 +952,7 @@ int av_run_rounds(av_engine* e, int32_t rounds) {
 
 int av_replay_round_errs(av_engine* e, const uint32_t* errs) {
   AV_ENTER(e);
+  AV_PEER_CHECK(e);
   AV_CHECK(errs, AV_ERR_INVALID_ARG, "null argument");
   e->c_monotone = false;
   const int64_t TL = e->t1 - e->t0;
@@ -942,6 +1007,7 @@ int av_replay_prepare(av_engine* e, int32_t rounds) {
 
 int av_replay_rounds(av_engine* e, int32_t rounds) {
   AV_ENTER(e);
+  AV_PEER_CHECK(e);
   AV_CHECK(rounds >= 0, AV_ERR_INVALID_ARG, "rounds < 0");
   AV_CHECK(e->round >= e->replay_first && e->round + rounds <= e->replay_first + e->replay_ready,
            AV_ERR_INVALID_ARG, "replay stream not prepared for these rounds");
@@ -957,17 +1023,34 @@ int av_replay_rounds(av_engine* e, int32_t rounds) {
 int av_synchronize(av_engine* e) {
   AV_ENTER(e);
   AV_HIP(hipStreamSynchronize(e->stream));
-  if (e->peer_world > 1) {
-    uint32_t err = 0;
-    AV_HIP(hipMemcpy(&err, e->barrier_err, 4, hipMemcpyDeviceToHost));
-    AV_CHECK(err == 0, AV_ERR_HIP, "peer barrier timed out (a rank stopped taking part in the rounds)");
-  }
+  AV_PEER_CHECK(e);
   return AV_OK;
 }
 
 int av_round_index(av_engine* e, int64_t* out) {
   AV_CHECK(e && out, AV_ERR_INVALID_ARG, "null argument");
   *out = e->round;
+  return AV_OK;
+}
+
+int av_get_round(av_engine* e, int64_t node, int64_t* out) {
+  AV_CHECK(e && out, AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
+  *out = e->proc_round.empty() ? 0 : e->proc_round[(size_t)(node - e->n0)];
+  return AV_OK;
+}
+
+int av_set_round(av_engine* e, int64_t node, int64_t round) {
+  AV_CHECK(e, AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
+  if (e->proc_round.empty()) e->proc_round.assign(e->NL, 0);
+  e->proc_round[(size_t)(node - e->n0)] = round;
+  return AV_OK;
+}
+
+int av_log_base_round(av_engine* e, int64_t* out) {
+  AV_CHECK(e && out, AV_ERR_INVALID_ARG, "null argument");
+  *out = e->log_base;
   return AV_OK;
 }
 
@@ -984,6 +1067,7 @@ int clear_log(av_engine* e) {
 
 int av_updates_count(av_engine* e, int64_t* n) {
   AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
   AV_CHECK(n, AV_ERR_INVALID_ARG, "null argument");
   std::vector<uint32_t> counts(avk::kLogShards);
   AV_HIP(hipMemcpyAsync(counts.data(), e->upd_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
@@ -1004,79 +1088,136 @@ int av_update_log_overflowed(av_engine* e, int32_t* out) {
   return AV_OK;
 }
 
+// Pending log state: per-shard counters copied to the host.
+struct LogCounts {
+  std::vector<uint32_t> singles, dense, upd;
+  uint32_t ovf = 0;
+  int64_t total = 0, n_singles = 0, n_records = 0;
+  std::vector<uint64_t> soff, doff;
+};
+
+int read_log_counts(av_engine* e, LogCounts& c) {
+  c.singles.assign(avk::kLogShards, 0);
+  c.dense.assign(avk::kLogShards, 0);
+  c.upd.assign(avk::kLogShards, 0);
+  AV_HIP(hipMemcpyAsync(c.singles.data(), e->log_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpyAsync(c.dense.data(), e->dlog_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpyAsync(c.upd.data(), e->upd_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpyAsync(&c.ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  c.soff.assign(avk::kLogShards, 0);
+  c.doff.assign(avk::kLogShards, 0);
+  for (uint32_t i = 0; i < avk::kLogShards; ++i) {
+    c.total += c.upd[i];
+    c.soff[i] = (uint64_t)c.n_singles;
+    c.n_singles += std::min<uint32_t>(c.singles[i], e->log_cap);
+    c.doff[i] = (uint64_t)c.n_records;
+    c.n_records += std::min<uint32_t>(c.dense[i], e->dlog_cap);
+  }
+  return AV_OK;
+}
+
 int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
   AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
   AV_CHECK(n_out && (cap == 0 || out), AV_ERR_INVALID_ARG, "null argument");
-  std::vector<uint32_t> counts(avk::kLogShards), dcounts(avk::kLogShards), upd(avk::kLogShards);
-  uint32_t ovf = 0;
-  AV_HIP(hipMemcpyAsync(counts.data(), e->log_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
-  AV_HIP(hipMemcpyAsync(dcounts.data(), e->dlog_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
-  AV_HIP(hipMemcpyAsync(upd.data(), e->upd_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
-  AV_HIP(hipMemcpyAsync(&ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
-  AV_HIP(hipStreamSynchronize(e->stream));
-  int64_t total = 0, singles = 0, records = 0;
-  std::vector<uint64_t> offs(avk::kLogShards), doffs(avk::kLogShards);
-  for (uint32_t i = 0; i < avk::kLogShards; ++i) {
-    total += upd[i];
-    offs[i] = (uint64_t)singles;
-    singles += std::min<uint32_t>(counts[i], e->log_cap);
-    doffs[i] = (uint64_t)records;
-    records += std::min<uint32_t>(dcounts[i], e->dlog_cap);
-  }
+  LogCounts c;
+  int rc = read_log_counts(e, c);
+  if (rc != AV_OK) return rc;
+  const int64_t total = c.total, singles = c.n_singles, records = c.n_records;
   *n_out = total;
-  if (ovf) {
-    int rc = clear_log(e);
+  if (c.ovf) {
+    rc = clear_log(e);
     if (rc != AV_OK) return rc;
     return fail(AV_ERR_OVERFLOW, "device StatusUpdate log overflowed (%lld updates, capacity %lld per shard)",
                 (long long)total, (long long)e->log_cap);
   }
   AV_CHECK(total <= cap, AV_ERR_OVERFLOW, "cap too small: %lld updates pending", (long long)total);
   if (total > 0) {
-    Scratch sc;
+    // device: singles and expanded dense records side by side, radix-sorted
+    // into the canonical (round, node, slot, target) order, then one copy out
     const uint32_t K = (uint32_t)e->k, dw = avk::dense_words(K);
-    AV_HIP(sc.ensure((size_t)(singles + dw * records) * 8 + 2 * avk::kLogShards * 8));
-    auto* dsingles = static_cast<uint64_t*>(sc.p);
-    auto* drecords = dsingles + singles;
-    auto* doff1 = drecords + dw * records;
-    auto* doff3 = doff1 + avk::kLogShards;
-    AV_HIP(hipMemcpyAsync(doff1, offs.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
-    AV_HIP(hipMemcpyAsync(doff3, doffs.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
-    AV_HIP(avk::launch_compact_log(e->log, e->log_count, doff1, e->log_cap, e->log_shards, 1, dsingles, e->stream));
-    AV_HIP(avk::launch_compact_log(e->dlog, e->dlog_count, doff3, e->dlog_cap, e->log_shards, dw, drecords,
-                                   e->stream));
-    AV_HIP(hipMemcpyAsync(out, dsingles, (size_t)singles * 8, hipMemcpyDeviceToHost, e->stream));
-    std::vector<uint64_t> rec((size_t)records * dw);
-    AV_HIP(hipMemcpyAsync(rec.data(), drecords, rec.size() * 8, hipMemcpyDeviceToHost, e->stream));
-    AV_HIP(hipStreamSynchronize(e->stream));
-    // expand dense lane records (kernels.h): key (the block's first target,
-    // slot 0), E_0..E_{k-1}, final A, deletion mask; A after slot j = final A
-    // ^ parity of the later slots' updates
-    int64_t n = singles;
-    for (int64_t r = 0; r < records; ++r) {
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(rec.data() + (size_t)r * dw);
-      const uint64_t key = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-      const uint32_t died = w[3 + K];
-      uint32_t par = 0;
-      for (int j = (int)K - 1; j >= 0; --j) {
-        const uint32_t aj = w[2 + K] ^ par;
-        par ^= w[2 + j];
-        for (uint32_t em = w[2 + j]; em && n < total; em &= em - 1u) {
-          const uint32_t bit = (uint32_t)__builtin_ctz(em);
-          const uint64_t a = (aj >> bit) & 1u;
-          const uint64_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
-          out[n++] = key + ((uint64_t)j << 24) + ((uint64_t)bit << 2) + st;
-        }
-      }
+    size_t scan_bytes = 0, sort_bytes = 0;
+    AV_HIP(avk::launch_dense_expand(nullptr, (uint64_t)records, K, nullptr, nullptr, nullptr, &scan_bytes, nullptr,
+                                    e->stream));
+    // sort on the key bits that vary: [2, 52 + width of the largest round_rel)
+    // (status bits need no ordering: (round, node, slot, target) is unique)
+    const int64_t max_rel = std::max<int64_t>(e->round - 1 - e->log_base, 0);
+    int end_bit = 52;
+    while (end_bit < 64 && (max_rel >> (end_bit - 52)) != 0) ++end_bit;
+    AV_HIP(avk::launch_sort_updates(nullptr, &sort_bytes, nullptr, nullptr, (uint64_t)total, 2, end_bit, e->stream));
+    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+    const size_t b_words = up((size_t)total * 8), b_rec = up((size_t)records * dw * 8),
+                 b_cnt = up((size_t)records * 8 + 8), b_off = up(2 * avk::kLogShards * 8);
+    const size_t bytes = 2 * b_words + b_rec + 2 * b_cnt + b_off + up(scan_bytes) + up(sort_bytes);
+    void* base = nullptr;
+    rc = engine_scratch(e, bytes, &base);
+    if (rc != AV_OK) return rc;
+    char* q = static_cast<char*>(base);
+    auto* words = reinterpret_cast<uint64_t*>(q);
+    q += b_words;
+    auto* sorted = reinterpret_cast<uint64_t*>(q);
+    q += b_words;
+    auto* recs = reinterpret_cast<uint64_t*>(q);
+    q += b_rec;
+    auto* cnt = reinterpret_cast<uint64_t*>(q);
+    q += b_cnt;
+    auto* offs = reinterpret_cast<uint64_t*>(q);
+    q += b_cnt;
+    auto* soff = reinterpret_cast<uint64_t*>(q);
+    auto* doff = soff + avk::kLogShards;
+    q += b_off;
+    void* scan_tmp = q;
+    q += up(scan_bytes);
+    void* sort_tmp = q;
+    AV_HIP(hipMemcpyAsync(soff, c.soff.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
+    AV_HIP(hipMemcpyAsync(doff, c.doff.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
+    AV_HIP(avk::launch_compact_log(e->log, e->log_count, soff, e->log_cap, e->log_shards, 1, words, e->stream));
+    if (records) {
+      AV_HIP(avk::launch_compact_log(e->dlog, e->dlog_count, doff, e->dlog_cap, e->log_shards, dw, recs, e->stream));
+      AV_HIP(avk::launch_dense_expand(recs, (uint64_t)records, K, cnt, offs, scan_tmp, &scan_bytes, words + singles,
+                                      e->stream));
+      // the expansion must produce exactly the counted updates
+      uint64_t last[2] = {0, 0};
+      AV_HIP(hipMemcpyAsync(&last[0], offs + records - 1, 8, hipMemcpyDeviceToHost, e->stream));
+      AV_HIP(hipMemcpyAsync(&last[1], cnt + records - 1, 8, hipMemcpyDeviceToHost, e->stream));
+      AV_HIP(hipStreamSynchronize(e->stream));
+      AV_CHECK((int64_t)(singles + last[0] + last[1]) == total, AV_ERR_HIP,
+               "StatusUpdate log inconsistent (%lld of %lld)", (long long)(singles + last[0] + last[1]),
+               (long long)total);
+    } else {
+      AV_CHECK(singles == total, AV_ERR_HIP, "StatusUpdate log inconsistent (%lld of %lld)", (long long)singles,
+               (long long)total);
     }
-    AV_CHECK(n == total, AV_ERR_HIP, "StatusUpdate log inconsistent (%lld of %lld)", (long long)n,
-             (long long)total);
-    std::sort(out, out + total);
+    AV_HIP(avk::launch_sort_updates(sort_tmp, &sort_bytes, words, sorted, (uint64_t)total, 2, end_bit, e->stream));
+    AV_HIP(hipMemcpyAsync(out, sorted, (size_t)total * 8, hipMemcpyDeviceToHost, e->stream));
+    AV_HIP(hipStreamSynchronize(e->stream));
   }
   return clear_log(e);
 }
 
+int av_updates_digest(av_engine* e, uint64_t out[3]) { return av_updates_digest_range(e, 0, e ? e->N : 0, out); }
+
+int av_updates_digest_range(av_engine* e, int64_t n0, int64_t n1, uint64_t out[3]) {
+  AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
+  AV_CHECK(out && n0 >= 0 && n0 <= n1 && n1 <= e->N, AV_ERR_INVALID_ARG, "bad argument");
+  uint32_t ovf = 0;
+  AV_HIP(hipMemcpyAsync(&ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
+  if (!e->digest) AV_HIP(dev_alloc(&e->digest, 3));
+  AV_HIP(avk::launch_log_digest(e->log, e->log_count, e->log_cap, e->dlog, e->dlog_count, e->dlog_cap,
+                                e->log_shards, (uint32_t)e->k, (uint32_t)n0, (uint32_t)n1, e->digest, e->stream));
+  unsigned long long d[3] = {0, 0, 0};
+  AV_HIP(hipMemcpyAsync(d, e->digest, sizeof(d), hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  AV_CHECK(!ovf, AV_ERR_OVERFLOW, "device StatusUpdate log overflowed: the digest would miss updates");
+  for (int i = 0; i < 3; ++i) out[i] = (uint64_t)d[i];
+  return AV_OK;
+}
+
 int av_applied_votes(av_engine* e, int64_t* out) {
   AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
   std::vector<unsigned long long> c(avk::kLogShards);
   AV_HIP(hipMemcpyAsync(c.data(), e->applied, avk::kLogShards * 8, hipMemcpyDeviceToHost, e->stream));
@@ -1099,12 +1240,14 @@ static int sum_counter(av_engine* e, const unsigned long long* dev, int64_t* out
 
 int av_finalized_count(av_engine* e, int64_t* out) {
   AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
   return sum_counter(e, e->finalized, out);
 }
 
 int av_live_records(av_engine* e, int32_t honest_only, int64_t* out) {
   AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
   AV_HIP(hipMemsetAsync(e->scratch_count, 0, 8, e->stream));
   AV_HIP(avk::launch_count_live(e->planes, e->valid, e->byz, (uint32_t)e->n0, e->BL, e->L, honest_only,
@@ -1123,6 +1266,7 @@ int av_discard_updates(av_engine* e) {
 
 int av_alg_bytes(av_engine* e, int64_t* out) {
   AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
   std::vector<unsigned long long> c(avk::kLogShards);
   AV_HIP(hipMemcpyAsync(c.data(), e->bytes, avk::kLogShards * 8, hipMemcpyDeviceToHost, e->stream));
@@ -1135,6 +1279,7 @@ int av_alg_bytes(av_engine* e, int64_t* out) {
 
 int av_read_pref(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint8_t* out) {
   AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
   AV_CHECK(out && n0 >= 0 && n0 <= n1 && n1 <= e->N && t0 >= e->t0 && t0 <= t1 && t1 <= e->t1,
            AV_ERR_INVALID_ARG, "bad range");
   const size_t rows = (size_t)(n1 - n0);
@@ -1150,6 +1295,17 @@ int av_read_pref(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, u
       const int64_t tl = t - e->t0;
       out[r * W + (t - t0)] = (uint8_t)((w[r * e->BL + (tl >> 5)] >> (tl & 31)) & 1u);
     }
+  return AV_OK;
+}
+
+int av_read_pref_words(av_engine* e, int64_t n0, int64_t n1, uint32_t* out) {
+  AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
+  AV_CHECK(out && n0 >= 0 && n0 <= n1 && n1 <= e->N, AV_ERR_INVALID_ARG, "bad range");
+  const size_t words = (size_t)(n1 - n0) * e->BL;
+  if (!words) return AV_OK;
+  AV_HIP(hipMemcpyAsync(out, e->pref[e->cur] + (size_t)n0 * e->BL, words * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
   return AV_OK;
 }
 
@@ -1202,6 +1358,12 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   } else if (n == "vv_min_bl") {
     AV_CHECK(value >= 1 && value < (1ll << 31), AV_ERR_INVALID_ARG, "bad vv_min_bl");
     e->vv_min_bl = (uint32_t)value;
+  } else if (n == "peer_fine") {  // before av_peer_handles: fine-grained snapshot buffers (default 1)
+    AV_CHECK(!e->arrive, AV_ERR_INVALID_ARG, "peer_fine must be set before av_peer_handles");
+    e->peer_fine = value != 0;
+  } else if (n == "barrier_timeout_ms") {
+    AV_CHECK(value >= 1 && value <= 3600000, AV_ERR_INVALID_ARG, "bad barrier_timeout_ms");
+    e->barrier_timeout_ms = (uint32_t)value;
   } else if (n == "warm_skip") {  // may only be switched off (it is a proven invariant, not a hint)
     if (!value) e->c_monotone = false;
   } else {
@@ -1281,10 +1443,38 @@ int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]) {
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
   static_assert(sizeof(hipIpcMemHandle_t) * 4 + 64 == AV_PEER_HANDLE_BYTES, "peer handle blob size");
   if (!e->arrive) {  // zeroed before any peer can see it: the exchange of handles orders the two
-    AV_HIP(dev_alloc(&e->arrive, (size_t)(2u << 20) / 4));
-    AV_HIP(dev_alloc(&e->barrier_err, 1));
+    // Snapshot buffers that peers store into over xGMI are fine-grained: this
+    // device's L2 keeps such lines only within a kernel (the system-scope
+    // acquire at every kernel start drops them), so a round never reads a
+    // stale L2 copy of a row a peer pushed during the previous round. Coarse-
+    // grained memory would let a line read two rounds earlier (the 3-deep
+    // rotation) survive in L2. Option "peer_fine" 0: keep the
+    // coarse-grained buffers (A/B only).
+    if (e->peer_fine) {
+      AV_HIP(hipStreamSynchronize(e->stream));
+      for (int b = 0; b < 3; ++b) {
+        uint32_t* fine = nullptr;
+        AV_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&fine), e->pref_alloc_words * 4,
+                                     hipDeviceMallocFinegrained));
+        AV_HIP(hipMemcpy(fine, e->pref[b], e->pref_alloc_words * 4, hipMemcpyDeviceToDevice));
+        AV_HIP(hipFree(e->pref[b]));
+        e->pref[b] = fine;
+      }
+      AV_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&e->arrive), (size_t)(2u << 20),
+                                   hipDeviceMallocFinegrained));
+    } else {
+      AV_HIP(dev_alloc(&e->arrive, (size_t)(2u << 20) / 4));
+    }
+    // the timeout flag lives in pinned host memory: the host sees it without
+    // synchronizing the stream (av_run_rounds refuses to enqueue once it is set)
+    void* hp = nullptr;
+    AV_HIP(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    e->barrier_err_host = static_cast<volatile uint32_t*>(hp);
+    *e->barrier_err_host = 0u;
+    void* dp = nullptr;
+    AV_HIP(hipHostGetDevicePointer(&dp, hp, 0));
+    e->barrier_err = static_cast<uint32_t*>(dp);
     AV_HIP(hipMemset(e->arrive, 0, (size_t)(avk::kMaxPeers + 1) * 4));
-    AV_HIP(hipMemset(e->barrier_err, 0, 4));
     AV_HIP(hipDeviceSynchronize());
   }
   void* bufs[4] = {e->pref[0], e->pref[1], e->pref[2], e->arrive};

@@ -197,6 +197,27 @@ hipError_t launch_add_targets(const AddParams& p, hipStream_t s);
 
 hipError_t launch_read_records(const uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1,
                                uint32_t tl0, uint32_t tl1, uint32_t* out, hipStream_t s);
+// Canonical words without writing back deferred state (kernels.hip
+// k_read_records_v): p = the engine's round parameters with p.vv = "some tile
+// may be stale" and p.klazy = "some tile may hold pending count steps".
+hipError_t launch_read_records_virtual(const RoundParams& p, uint32_t nl0, uint32_t nl1, uint32_t tl0, uint32_t tl1,
+                                       uint32_t* out, hipStream_t s);
+
+// Device-side StatusUpdate delivery (log_ops.hip).
+// Digest {count, sum, xor} of splitmix64(packed word) over every pending update
+// of nodes [node0, node1).
+hipError_t launch_log_digest(const uint64_t* log, const uint32_t* counts, uint32_t cap, const uint64_t* dlog,
+                             const uint32_t* dcounts, uint32_t dcap, uint32_t shards, uint32_t k, uint32_t node0,
+                             uint32_t node1, unsigned long long* out, hipStream_t s);
+// Expand n compacted dense records into packed words at out (scratch: n u64
+// counts + n u64 offsets; temp == nullptr: *temp_bytes = the scan's scratch size).
+hipError_t launch_dense_expand(const uint64_t* recs, uint64_t n, uint32_t k, uint64_t* counts_scratch,
+                               uint64_t* offsets, void* temp, size_t* temp_bytes, uint64_t* out, hipStream_t s);
+// Radix sort of packed update words on bits [begin_bit, end_bit) (temp ==
+// nullptr: size query).
+hipError_t launch_sort_updates(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
+                               int begin_bit, int end_bit, hipStream_t s);
+
 hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0,
                                 uint32_t tl1, const uint32_t* in, hipStream_t s);
 hipError_t launch_refresh_pref(const uint32_t* planes, uint32_t* pref, const uint32_t* byz, uint32_t n0,

@@ -422,6 +422,66 @@ __global__ void k_read_records(const uint32_t* planes, uint32_t BL, uint32_t nl0
   out[i] = v | (c << 8) | (((k << 1) | a) << 16);
 }
 
+// The same canonical words, one thread per 32-record lane, WITHOUT writing
+// back the deferred forms the warm rounds leave behind (kernels.h vv / klazy):
+// a stale tile's vote register is regathered from the previous snapshot
+// (p.pref_prev) with round p.round - 1's peers, and a tile's pending +8 count
+// steps are added to its polled (live, valid) records. Reads (IsAccepted,
+// GetConfidence, GetInvsForNextPoll, dumps) then leave the next round's fast
+// paths in place. p.vv / p.klazy: some tile may be stale / hold pending steps.
+__global__ __launch_bounds__(256) void k_read_records_v(const RoundParams p, uint32_t nl0, uint32_t nl1, uint32_t tl0,
+                                                        uint32_t tl1, uint32_t* out) {
+  const uint32_t b0 = tl0 >> 5, NB = ((tl1 + 31u) >> 5) - b0, W = tl1 - tl0;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (nl1 - nl0) * NB) return;
+  const uint32_t nl = nl0 + i / NB, b = b0 + i % NB;
+  const uint32_t g = nl * p.BL + b, tile = g >> 6;
+  St s;
+  load_state(p.planes, g, s);
+  if (p.vv && p.vstale[tile]) {  // V_i = the vote of round - 1's slot 7 - i (k = 8)
+    uint32_t pp[8];
+    sample_peers<8>(p.seed, p.n0 + nl, p.round - 1u, p.n_nodes, p.peer_mode, pp);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s.V[q] = p.pref_prev[pp[7 - q] * p.BL + b];
+  }
+  if (p.klazy) {
+    const uint32_t pend = p.kpend[tile] & 0xFFu;
+    if (pend) {  // + 8 * pend on the polled records: pend added to count bits 3..6
+      const uint32_t P0 = ~s.K[7] & p.valid[b];
+      uint32_t cy = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t bi = ((pend >> q) & 1u) ? P0 : 0u;
+        const uint32_t t = s.K[3 + q] ^ bi;
+        const uint32_t si = t ^ cy;
+        cy = (t & cy) | (s.K[3 + q] & bi);
+        s.K[3 + q] = si;
+      }
+    }
+  }
+  const uint32_t lo = max(tl0, b * 32u), hi = min(tl1, b * 32u + 32u);
+  uint32_t* dst = out + (size_t)(nl - nl0) * W;
+  for (uint32_t tl = lo; tl < hi; ++tl) {
+    const uint32_t bit = tl & 31u;
+    const uint32_t a = (s.A >> bit) & 1u;
+    uint32_t word;
+    if ((s.K[7] >> bit) & 1u) {
+      word = 0xFFFE0000u | (a << 16);
+    } else {
+      uint32_t v = 0, c = 0, k = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        v |= ((s.V[q] >> bit) & 1u) << q;
+        c |= ((s.C[q] >> bit) & 1u) << q;
+      }
+#pragma unroll
+      for (int q = 0; q < 7; ++q) k |= ((s.K[q] >> bit) & 1u) << q;
+      word = v | (c << 8) | (((k << 1) | a) << 16);
+    }
+    dst[tl - tl0] = word;
+  }
+}
+
 __global__ void k_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0,
                                 uint32_t tl1, const uint32_t* in) {
   const uint32_t b0 = tl0 >> 5, b1 = (tl1 + 31u) >> 5, NB = b1 - b0, W = tl1 - tl0;
@@ -658,6 +718,15 @@ hipError_t launch_read_records(const uint32_t* planes, uint32_t BL, uint32_t nl0
   return hipGetLastError();
 }
 
+hipError_t launch_read_records_virtual(const RoundParams& p, uint32_t nl0, uint32_t nl1, uint32_t tl0, uint32_t tl1,
+                                       uint32_t* out, hipStream_t s) {
+  const uint32_t nb = ((tl1 + 31u) >> 5) - (tl0 >> 5);
+  const uint32_t n = (nl1 - nl0) * nb;
+  if (!n || tl1 <= tl0) return hipSuccess;
+  hipLaunchKernelGGL(k_read_records_v, dim3((n + 255) / 256), dim3(256), 0, s, p, nl0, nl1, tl0, tl1, out);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // Peer-push exchange of node-sharded engines. Replaces the
 // per-round all-gather of published-preference rows (main.go:168-192: every
@@ -681,7 +750,9 @@ __global__ __launch_bounds__(256) void k_push_rows(const uint32_t* src, PeerPtrs
 // (release, system scope: this rank's earlier kernels and pushes are visible
 // first), then waits for its own slot i to reach seq (acquire, system scope).
 // Every lane leaves after at most `ticks` wall-clock ticks; a timeout sets *err
-// and every later barrier of the engine returns without waiting.
+// (pinned host memory) and every later barrier of the engine returns without
+// waiting; the host refuses further rounds and results (engine.cpp
+// peer_failed, AV_ERR_PEER).
 __global__ __launch_bounds__(64) void k_peer_barrier(PeerPtrs arrive, const uint32_t* own, uint32_t world,
                                                      uint32_t rank, uint32_t seq, uint32_t* err, uint64_t ticks) {
   const uint32_t i = threadIdx.x;
@@ -690,13 +761,13 @@ __global__ __launch_bounds__(64) void k_peer_barrier(PeerPtrs arrive, const uint
   for (int r = 1; r <= kMaxPeers; ++r)
     if ((uint32_t)r == i) mine = arrive.p[r];
   if (i < world) __hip_atomic_store(mine + rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  const bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  const bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
   if (i >= world || failed) return;
   const uint32_t* slot = own + i;  // own == arrive.p[rank]
   const uint64_t t0 = (uint64_t)wall_clock64();
   while ((int32_t)(__hip_atomic_load(slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
     if ((uint64_t)wall_clock64() - t0 > ticks) {
-      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // host-visible (pinned)
       return;
     }
     __builtin_amdgcn_s_sleep(2);

@@ -1,0 +1,161 @@
+// StatusUpdate delivery on the device (processor.go:111's *[]StatusUpdate
+// out-parameter): the round kernels leave their updates in a sharded log of
+// single packed words and dense lane records (kernels.h); these kernels
+//  * expand the dense records into packed words (A after slot j = the final
+//    A plane ^ parity of the later slots' updates; vote.go:77-91 statuses),
+//  * put the singles and the expanded words into the canonical (round, node,
+//    slot, target) order with a device radix sort (rocPRIM via hipCUB) — the
+//    packed word sorts exactly in that order (include/avhip.h),
+//  * or reduce them to an order-independent digest (count, sum and xor of
+//    splitmix64(word)) that the oracle computes the same way
+//    (oracle/avalanche_oracle.c avo_mix64), for full-size parity checks that
+//    do not copy billions of updates to the host.
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include "kernels.h"
+#include "round_common.h"
+
+namespace avk {
+namespace {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t wave_add64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, d, 64);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_xor64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v ^= (uint64_t)__shfl_xor((unsigned long long)v, d, 64);
+  return v;
+}
+
+// Words of one dense record (kernels.h): w[0..1] key, w[2..1+K] E_j, w[2+K]
+// final A plane, w[3+K] died. Calls f(word) for each of its updates.
+template <typename F>
+__device__ __forceinline__ void for_each_dense(const uint32_t* w, uint32_t K, F&& f) {
+  const uint64_t key = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  const uint32_t A = w[2 + K], died = w[3 + K];
+  uint32_t par = 0u;
+  for (int j = (int)K - 1; j >= 0; --j) {
+    const uint32_t aj = A ^ par;
+    const uint32_t e = w[2 + j];
+    par ^= e;
+    for (uint32_t em = e; em; em &= em - 1u) {
+      const uint32_t bit = (uint32_t)__builtin_ctz(em);
+      const uint64_t a = (aj >> bit) & 1u;
+      const uint64_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
+      f(key + ((uint64_t)j << 24) + ((uint64_t)bit << 2) + st);
+    }
+  }
+}
+
+__device__ __forceinline__ bool in_nodes(uint64_t w, uint32_t node0, uint32_t node1) {
+  const uint32_t node = (uint32_t)(w >> 28) & 0xFFFFFFu;
+  return node >= node0 && node < node1;
+}
+
+// Digest of every pending update of nodes [node0, node1): blockIdx.y = shard;
+// the x-blocks stride over the shard's singles, then over its dense records.
+__global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const uint32_t* counts, uint32_t cap,
+                                                    const uint64_t* dlog, const uint32_t* dcounts, uint32_t dcap,
+                                                    uint32_t K, uint32_t node0, uint32_t node1,
+                                                    unsigned long long* out) {
+  const uint32_t shard = blockIdx.y;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t s = 0, x = 0, c = 0;
+  const uint32_t n = min(counts[shard], cap);
+  const uint64_t* src = log + (size_t)shard * cap;
+  for (uint32_t i = t; i < n; i += stride) {
+    const uint64_t w = src[i];
+    if (!in_nodes(w, node0, node1)) continue;
+    const uint64_t h = mix64(w);
+    s += h;
+    x ^= h;
+    ++c;
+  }
+  const uint32_t DW = dense_words(K);
+  const uint32_t nd = min(dcounts[shard], dcap);
+  const uint64_t* dsrc = dlog + (size_t)shard * dcap * DW;
+  for (uint32_t i = t; i < nd; i += stride) {
+    const uint32_t* rw = reinterpret_cast<const uint32_t*>(dsrc + (size_t)i * DW);
+    if (!in_nodes((uint64_t)rw[0] | ((uint64_t)rw[1] << 32), node0, node1)) continue;
+    for_each_dense(reinterpret_cast<const uint32_t*>(dsrc + (size_t)i * DW), K, [&](uint64_t wd) {
+      const uint64_t h = mix64(wd);
+      s += h;
+      x ^= h;
+      ++c;
+    });
+  }
+  c = wave_add64(c);
+  s = wave_add64(s);
+  x = wave_xor64(x);
+  if ((threadIdx.x & 63u) == 0 && c) {
+    atomicAdd(&out[0], (unsigned long long)c);
+    atomicAdd(&out[1], (unsigned long long)s);
+    atomicXor(&out[2], (unsigned long long)x);
+  }
+}
+
+// Updates held by each dense record (popcount of its E_j).
+__global__ __launch_bounds__(256) void k_dense_counts(const uint64_t* recs, uint64_t n, uint32_t K, uint64_t* cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(recs + i * dense_words(K));
+  uint32_t c = 0;
+  for (uint32_t j = 0; j < K; ++j) c += (uint32_t)__popc(w[2 + j]);
+  cnt[i] = c;
+}
+
+// Expand record i at out[off[i] ...] (off: exclusive scan of k_dense_counts).
+__global__ __launch_bounds__(256) void k_dense_expand(const uint64_t* recs, uint64_t n, uint32_t K,
+                                                      const uint64_t* off, uint64_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t* dst = out + off[i];
+  for_each_dense(reinterpret_cast<const uint32_t*>(recs + i * dense_words(K)), K, [&](uint64_t wd) { *dst++ = wd; });
+}
+
+}  // namespace
+
+hipError_t launch_log_digest(const uint64_t* log, const uint32_t* counts, uint32_t cap, const uint64_t* dlog,
+                             const uint32_t* dcounts, uint32_t dcap, uint32_t shards, uint32_t k, uint32_t node0,
+                             uint32_t node1, unsigned long long* out, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(out, 0, 3 * sizeof(unsigned long long), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_log_digest, dim3(16, shards), dim3(256), 0, s, log, counts, cap, dlog, dcounts, dcap, k, node0,
+                     node1, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_dense_expand(const uint64_t* recs, uint64_t n, uint32_t k, uint64_t* counts_scratch,
+                               uint64_t* offsets, void* temp, size_t* temp_bytes, uint64_t* out, hipStream_t s) {
+  if (!temp) {  // size query for the scan
+    return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, counts_scratch, offsets, n, s);
+  }
+  if (!n) return hipSuccess;
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(k_dense_counts, dim3((uint32_t)blocks), dim3(256), 0, s, recs, n, k, counts_scratch);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, counts_scratch, offsets, n, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_dense_expand, dim3((uint32_t)blocks), dim3(256), 0, s, recs, n, k, offsets, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sort_updates(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
+                               int begin_bit, int end_bit, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortKeys(temp, *temp_bytes, in, out, n, begin_bit, end_bit, s);
+}
+
+}  // namespace avk

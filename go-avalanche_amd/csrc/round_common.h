@@ -382,7 +382,10 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
     }
   }
   if (__ballot(ovf) != 0ull) note_overflow(p, lane);
-  return 8u * tot_s + 8u * DW * tot_d;
+  // bytes actually stored (wave-uniform): entries past a full shard were dropped
+  const uint32_t st_s = base >= p.log_cap ? 0u : min(tot_s, p.log_cap - base);
+  const uint32_t st_d = dbase >= p.dlog_cap ? 0u : min(tot_d, p.dlog_cap - dbase);
+  return 8u * st_s + 8u * DW * st_d;
 }
 
 // Per-wave counters: regsiterVote applications (the metric numerator) and the

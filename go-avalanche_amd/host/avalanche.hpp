@@ -9,7 +9,7 @@
 //   Processor::IsAccepted            processor.go:125-130 -> av_is_accepted
 //   Processor::GetConfidence         processor.go:133-140 -> av_get_confidence (throws where Go panics)
 //   Processor::GetInvsForNextPoll    processor.go:144-170 -> av_get_invs
-//   Processor::GetRound              processor.go:40-42
+//   Processor::GetRound              processor.go:40-42   -> av_get_round (per-node field, av_set_round)
 // A Processor is a view (engine, node) over one batched Engine, so N
 // Processors share one HBM-resident state and one batched round driver
 // (Network::RunRounds = the example's poll loop for every node at once).
@@ -164,6 +164,9 @@ class Processor {
   Processor(std::shared_ptr<Engine> engine, NodeID node, Connman* connman = nullptr);
 
   int64_t GetRound() const;                                                              // :40-42
+  // the reference test's `p.round++` (avalanche_test.go:302): Processor.round
+  // is a field only its owner changes
+  void SetRound(int64_t round);
   bool AddTargetToReconcile(const Target& t);                                            // :45-58
   bool RegisterVotes(NodeID id, const Response& resp, std::vector<StatusUpdate>* updates);  // :61-122
   bool IsAccepted(const Target& t) const;                                                // :125-130

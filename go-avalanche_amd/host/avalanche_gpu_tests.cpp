@@ -224,7 +224,13 @@ void network_rounds() {
   for (uint64_t u : ups) EXPECT(av_update_status(u) == AV_STATUS_FINALIZED);
   Processor p0(engine, 0);
   EXPECT(p0.GetInvsForNextPoll().empty());
-  EXPECT(p0.GetRound() == 20);
+  // GetRound is the Processor's own field (processor.go:40-42), not the
+  // engine's batched-round counter: rounds leave it alone, its owner sets it
+  EXPECT(p0.GetRound() == 0);
+  p0.SetRound(p0.GetRound() + 1);  // avalanche_test.go:302 `p.round++`
+  EXPECT(p0.GetRound() == 1);
+  EXPECT(Processor(engine, 1).GetRound() == 0);
+  EXPECT(engine->Round() == 20);
 }
 
 }  // namespace

@@ -93,7 +93,13 @@ std::vector<uint64_t> Engine::FetchUpdates() {
 Processor::Processor(std::shared_ptr<Engine> engine, NodeID node, Connman* connman)
     : engine_(std::move(engine)), node_(node), connman_(connman) {}
 
-int64_t Processor::GetRound() const { return engine_->Round(); }
+int64_t Processor::GetRound() const {
+  int64_t r = 0;
+  check(av_get_round(engine_->handle(), node_, &r));
+  return r;
+}
+
+void Processor::SetRound(int64_t round) { check(av_set_round(engine_->handle(), node_, round)); }
 
 bool Processor::AddTargetToReconcile(const Target& t) {
   if (!t.IsValid()) return false;  // processor.go:46-48

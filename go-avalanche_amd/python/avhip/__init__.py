@@ -25,6 +25,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_PKG_ROOT), "include", "avhip.h")
 AV_OK = 0
 AV_ERR_NOT_FOUND = -4
 AV_ERR_OVERFLOW = -5
+AV_ERR_PEER = -8
 
 STATUS_INVALID, STATUS_REJECTED, STATUS_ACCEPTED, STATUS_FINALIZED = 0, 1, 2, 3
 PEERS_RANDOM, PEERS_ROUND_ROBIN = 0, 1
@@ -46,6 +47,10 @@ class VoteRecordNotFound(AvError):
 
 class LogOverflow(AvError):
     pass
+
+
+class PeerExchangeFailed(AvError):
+    """A rank missed a peer barrier: the engine refuses further rounds and results."""
 
 
 class Config(C.Structure):
@@ -75,7 +80,8 @@ EXPORTED = [
     "av_replay_rounds", "av_synchronize", "av_round_index", "av_updates_count", "av_fetch_updates",
     "av_update_log_overflowed", "av_applied_votes", "av_alg_bytes", "av_finalized_count", "av_live_records", "av_discard_updates", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
-    "av_peer_handles", "av_peer_init",
+    "av_peer_handles", "av_peer_init", "av_get_round", "av_set_round", "av_log_base_round", "av_updates_digest",
+    "av_updates_digest_range", "av_read_pref_words",
 ]
 
 _lib = None
@@ -132,6 +138,12 @@ def lib():
         "av_comm_init": (i32, [_vp, i32, i32, _vp]),
         "av_peer_handles": (i32, [_vp, _vp]),
         "av_peer_init": (i32, [_vp, i32, i32, _vp]),
+        "av_get_round": (i32, [_vp, i64, P(i64)]),
+        "av_set_round": (i32, [_vp, i64, i64]),
+        "av_log_base_round": (i32, [_vp, P(i64)]),
+        "av_updates_digest": (i32, [_vp, _vp]),
+        "av_updates_digest_range": (i32, [_vp, i64, i64, _vp]),
+        "av_read_pref_words": (i32, [_vp, i64, i64, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -149,6 +161,8 @@ def _check(rc):
         raise VoteRecordNotFound(rc, msg)
     if rc == AV_ERR_OVERFLOW:
         raise LogOverflow(rc, msg)
+    if rc == AV_ERR_PEER:
+        raise PeerExchangeFailed(rc, msg)
     raise AvError(rc, msg)
 
 
@@ -194,7 +208,6 @@ class Engine:
         self.n_nodes, self.n_targets, self.k = n_nodes, n_targets, k
         self.node_range = (cfg.node_begin, cfg.node_end) if node_range else (0, n_nodes)
         self.target_range = (cfg.target_begin, cfg.target_end) if target_range else (0, n_targets)
-        self._log_base = 0
 
     def close(self):
         if getattr(self, "_h", None):
@@ -284,6 +297,15 @@ class Engine:
     def synchronize(self):
         _check(lib().av_synchronize(self._h))
 
+    def get_round(self, node):
+        """Processor.GetRound of `node` (processor.go:40-42): a caller-set field."""
+        out = C.c_int64(0)
+        _check(lib().av_get_round(self._h, node, C.byref(out)))
+        return out.value
+
+    def set_round(self, node, rnd):
+        _check(lib().av_set_round(self._h, node, rnd))
+
     @property
     def round(self):
         out = C.c_int64(0)
@@ -296,16 +318,41 @@ class Engine:
         _check(lib().av_updates_count(self._h, C.byref(out)))
         return out.value
 
+    def log_base_round(self):
+        """Round the pending log's round fields count from (kept by the engine:
+        a fetch, a discard or an overflowed fetch moves it)."""
+        out = C.c_int64(0)
+        _check(lib().av_log_base_round(self._h, C.byref(out)))
+        return out.value
+
     def fetch_updates(self, decode=True):
-        """All StatusUpdates since the previous fetch in canonical order."""
+        """All StatusUpdates since the previous fetch in canonical order
+        (sorted on the device)."""
         n = self.updates_count()
         buf = np.zeros(max(1, n), np.uint64)
         got = C.c_int64(0)
-        base = self._log_base
+        base = self.log_base_round()
         _check(lib().av_fetch_updates(self._h, _ptr(buf), buf.size, C.byref(got)))
-        self._log_base = self.round
         buf = buf[: got.value]
         return decode_updates(buf, base) if decode else buf
+
+    def updates_digest(self, n0=None, n1=None):
+        """(count, sum, xor) of splitmix64 over the pending packed updates (not
+        cleared), of nodes [n0, n1) if given."""
+        out = np.zeros(3, np.uint64)
+        if n0 is None:
+            _check(lib().av_updates_digest(self._h, _ptr(out)))
+        else:
+            _check(lib().av_updates_digest_range(self._h, n0, n1, _ptr(out)))
+        return tuple(int(v) for v in out)
+
+    def read_pref_words(self, n0=0, n1=None):
+        """Round-start published rows as stored: uint32[n1-n0, BL] bitsets."""
+        n1 = self.n_nodes if n1 is None else n1
+        bl = self.layout_info()["local_blocks"]
+        out = np.zeros((n1 - n0, bl), np.uint32)
+        _check(lib().av_read_pref_words(self._h, n0, n1, _ptr(out)))
+        return out
 
     def applied_votes(self):
         out = C.c_int64(0)
@@ -329,7 +376,6 @@ class Engine:
 
     def discard_updates(self):
         _check(lib().av_discard_updates(self._h))
-        self._log_base = self.round
 
     def alg_bytes(self):
         out = C.c_int64(0)

@@ -16,7 +16,9 @@
  *   av_get_confidence   <- (*Processor).GetConfidence           processor.go:133-140
  *   av_get_invs         <- (*Processor).GetInvsForNextPoll      processor.go:144-170
  *   av_get_invs_batch   <- GetInvsForNextPoll of many Processors processor.go:144-170
- *   av_round_index      <- (*Processor).GetRound                processor.go:40-42
+ *   av_get_round        <- (*Processor).GetRound                processor.go:40-42
+ *   av_set_round        <- the caller's `p.round = ...`          avalanche_test.go:302 (Processor.round is a
+ *                          field nothing in the Processor advances: processor.go:15,40-42)
  *   av_set_valid        <- Target.IsValid / isWorthyPolling     avalanche.go:89-90, processor.go:185-187
  *   av_run_rounds       <- the example's poll loop for every node at once
  *                          (main.go:110-137 + responder main.go:168-192,
@@ -24,6 +26,7 @@
  *                          / Connman.NodesIDs net.go:25-31 replaced by
  *                          counter-RNG k-peer sampling)
  *   av_fetch_updates    <- the *[]StatusUpdate out-parameter     processor.go:61,111
+ *                          (device-side canonical ordering: radix sort of the packed words)
  */
 #ifndef AVHIP_H
 #define AVHIP_H
@@ -45,6 +48,7 @@ extern "C" {
 #define AV_ERR_OVERFLOW (-5)    /* update log or caller buffer too small */
 #define AV_ERR_UNSUPPORTED (-6)
 #define AV_ERR_RCCL (-7)
+#define AV_ERR_PEER (-8)        /* peer-push exchange broken (a rank missed a barrier); sticky */
 
 /* Status (avalanche.go:42-56, iota order) */
 #define AV_STATUS_INVALID 0
@@ -151,7 +155,14 @@ int av_replay_prepare(av_engine* e, int32_t rounds);
 /* ... and consume them (asynchronous). */
 int av_replay_rounds(av_engine* e, int32_t rounds);
 int av_synchronize(av_engine* e);
+/* Batched rounds run so far (the engine's round counter: the RNG counter of
+ * the peer draw, R1). Not the reference's GetRound: see av_get_round. */
 int av_round_index(av_engine* e, int64_t* out);
+/* Processor.GetRound of one node (processor.go:40-42): a per-Processor field
+ * that only its owner changes (the reference test sets it, avalanche_test.go:
+ * 302); 0 until av_set_round. Not advanced by rounds. */
+int av_get_round(av_engine* e, int64_t node, int64_t* out);
+int av_set_round(av_engine* e, int64_t node, int64_t round);
 
 /* ---- outputs ---- */
 int av_updates_count(av_engine* e, int64_t* n);
@@ -162,6 +173,16 @@ int av_update_log_overflowed(av_engine* e, int32_t* out);
  * log. AV_ERR_OVERFLOW if the device log or `cap` overflowed (*n_out holds the
  * required count when cap is too small). */
 int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out);
+/* The round the pending log's round fields count from (the engine round at
+ * the last fetch/discard): round of a fetched word = this + av_update_round_rel. */
+int av_log_base_round(av_engine* e, int64_t* out);
+/* Order-independent digest of every pending StatusUpdate without fetching
+ * (or clearing) them: out = {count, sum, xor} of splitmix64(packed word).
+ * AV_ERR_OVERFLOW if the log overflowed. Full-size parity checks compare it
+ * with the oracle's digest of the same round. */
+int av_updates_digest(av_engine* e, uint64_t out[3]);
+/* The same over the updates of nodes [n0, n1) only. */
+int av_updates_digest_range(av_engine* e, int64_t n0, int64_t n1, uint64_t out[3]);
 /* Number of regsiterVote applications (vote.go:54) since creation. */
 int av_applied_votes(av_engine* e, int64_t* out);
 /* Records deleted after finalization by round kernels since creation. */
@@ -179,6 +200,9 @@ int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1
 int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, const uint32_t* in);
 /* Round-start published preference (0/1) for nodes [n0,n1) x targets [t0,t1). */
 int av_read_pref(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint8_t* out);
+/* Round-start published preference rows of nodes [n0,n1) as stored: [n][BL]
+ * u32 bitsets of this engine's target range (bit t % 32 of word t / 32). */
+int av_read_pref_words(av_engine* e, int64_t n0, int64_t n1, uint32_t* out);
 /* Device peer sampling dump: peers of nodes [n0,n1) in round `round`, [n][k]. */
 int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t* out);
 
@@ -190,7 +214,10 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  * "sweep_blocks"   : workgroups of the sweep grid (0 = one wave per tile,
  *                    -1 = the engine's choice (default), -2 = every resident
  *                    workgroup once, walking the tiles).
- * "store_policy"   : 2 = write-through (sc1) plane stores, 3 = nt sc1 (A/B). */
+ * "store_policy"   : 2 = write-through (sc1) plane stores, 3 = nt sc1 (A/B).
+ * "peer_fine" (0/1): snapshot buffers fine-grained once exported (default 1;
+ *                    set before av_peer_handles).
+ * "barrier_timeout_ms": peer barrier timeout (default 30000). */
 int av_set_option(av_engine* e, const char* name, int64_t value);
 
 /* ---- measurement ---- */

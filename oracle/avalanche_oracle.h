@@ -77,6 +77,11 @@ avo_vote_record avo_unpack(uint32_t w);
 void avo_transition_batch(const uint32_t* words_in, const uint32_t* errs, int64_t n,
                           uint32_t* words_out, uint8_t* changed, uint8_t* status);
 
+/* The oracle's branch-free form of the same step (used by the batched sim
+ * when the poll cap cannot bind); status[i] = appended Status, -1 = none. */
+void avo_transition_batch_branchfree(const uint32_t* words_in, const uint32_t* errs, int64_t n, uint32_t* words_out,
+                                     int8_t* status);
+
 /* ---- Processor (processor.go:12-187) over M dense target slots ---- */
 typedef struct avo_processor avo_processor;
 avo_processor* avo_processor_new(int64_t n_targets);
@@ -92,6 +97,8 @@ int avo_processor_is_accepted(const avo_processor* p, int64_t t);              /
 int avo_processor_get_confidence(const avo_processor* p, int64_t t, uint16_t* out); /* :133-140; -1 = panic */
 int64_t avo_processor_get_invs(const avo_processor* p, const uint8_t* valid, int64_t* out, int64_t cap); /* :144-170 */
 uint32_t avo_processor_dump_word(const avo_processor* p, int64_t t);
+int64_t avo_processor_get_round(const avo_processor* p);          /* :40-42 */
+void avo_processor_set_round(avo_processor* p, int64_t round);    /* the owner's p.round = ... */
 
 /* ---- Batched-round harness ---- */
 typedef struct {
@@ -107,8 +114,11 @@ typedef struct {
 
 typedef struct avo_sim avo_sim;
 avo_sim* avo_sim_new(const avo_sim_config* cfg);
+avo_sim* avo_sim_new_threads(const avo_sim_config* cfg, int32_t threads); /* OpenMP population */
 void avo_sim_free(avo_sim* s);
 void avo_sim_set_valid(avo_sim* s, int64_t t, int valid);
+int64_t avo_sim_get_round(const avo_sim* s, int64_t node); /* node's Processor.GetRound */
+void avo_sim_set_round(avo_sim* s, int64_t node, int64_t round);
 int64_t avo_sim_round_index(const avo_sim* s);
 /* One round. replay_errs: NULL (sim mode: votes from peers' published
  * preferences) or [n_nodes][k][n_targets] err words. Updates are written as
@@ -120,8 +130,29 @@ int avo_sim_round(avo_sim* s, const uint32_t* replay_errs, int64_t* updates, int
  * published rows; other rows are installed with avo_sim_set_pref_rows. */
 int avo_sim_round_range(avo_sim* s, int64_t n0, int64_t n1, const uint32_t* replay_errs, int64_t* updates,
                         int64_t cap, int64_t* n_out, int32_t threads, int64_t* applied_votes);
+/* General form: nodes [n0, n1); updates == NULL collects no rows; digest (if
+ * not NULL) = {count, sum, xor} of avo_mix64(avo_pack_update(round_rel, ...))
+ * over the round's StatusUpdates (order-independent; the engine computes the
+ * same over its device log, av_updates_digest). */
+int avo_sim_round_ex(avo_sim* s, int64_t n0, int64_t n1, const uint32_t* replay_errs, int64_t* updates,
+                     int64_t cap, int64_t* n_out, int32_t threads, int64_t* applied_votes, uint64_t digest[3],
+                     uint32_t round_rel);
+/* 1: every round takes the literal per-vote path (GetInvsForNextPoll +
+ * RegisterVotes per slot); 0 (default): the branch-free per-node form when the
+ * poll cap cannot bind. Both are the same restatement; tests compare them. */
+void avo_sim_set_literal(avo_sim* s, int literal);
+/* One node's literal round against an external snapshot (pref_words
+ * [n_nodes][ceil(m/32)] bitsets, byz_words [ceil(n/32)]): words[m] canonical
+ * record words in/out; digest accumulates its StatusUpdates; returns the
+ * applied votes. The sampled full-size check of the engine. */
+int64_t avo_node_round_ext(uint64_t seed, int64_t n_nodes, int32_t k, int32_t peer_mode, int64_t node,
+                           int64_t round, int64_t m, const uint32_t* pref_words, const uint32_t* byz_words,
+                           const uint8_t* valid, uint32_t* words, uint64_t digest[3], uint32_t round_rel);
+uint64_t avo_pack_update(uint32_t round_rel, int64_t node, int32_t slot, int64_t t, int32_t status);
+uint64_t avo_mix64(uint64_t x);
 void avo_sim_set_pref_rows(avo_sim* s, int64_t n0, int64_t n1, const uint8_t* rows);
 void avo_sim_dump(const avo_sim* s, uint32_t* out /* [N][M] canonical words */);
+void avo_sim_dump_range(const avo_sim* s, int64_t n0, int64_t n1, uint32_t* out /* [n1-n0][M] */, int32_t threads);
 void avo_sim_pref(const avo_sim* s, uint8_t* out /* [N][M] published preference */);
 int avo_sim_is_byzantine(const avo_sim* s, int64_t node);
 /* Mutators used by the golden-fixture interpreter */
@@ -133,6 +164,7 @@ int avo_sim_register_votes(avo_sim* s, int64_t node, const int64_t* targets, con
 void avo_sample_peers(uint64_t seed, int64_t node, int64_t round, int64_t n_nodes, int32_t k,
                       int32_t mode, int64_t* out);
 int avo_is_byzantine(uint64_t seed, int64_t node, uint32_t threshold);
+void avo_byz_words(uint64_t seed, int64_t n_nodes, uint32_t threshold, uint32_t* out /* [ceil(n/32)] bits */);
 int avo_initial_accept(uint64_t seed, int32_t mode, uint32_t param, int64_t node, int64_t t);
 uint32_t avo_replay_err(uint64_t seed, int64_t node, int64_t round, int32_t slot, int64_t t);
 void avo_gen_replay_errs(uint64_t seed, int64_t round, int64_t n0, int64_t n1, int64_t n_targets,

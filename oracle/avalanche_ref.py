@@ -100,6 +100,9 @@ class Processor:
         self.decision: dict[int, bool] = {}  # harness extension for rule R2
         self.round = 0
 
+    def get_round(self) -> int:  # processor.go:40-42
+        return self.round
+
     def add_target_to_reconcile(self, t: Target) -> bool:  # processor.go:45-58
         if not t.valid:
             return False

@@ -50,6 +50,26 @@ def lib():
         L.avo_processor_free.argtypes = [C.c_void_p]
         L.avo_sim_new.restype = C.c_void_p
         L.avo_sim_new.argtypes = [C.POINTER(SimConfig)]
+        L.avo_sim_new_threads.restype = C.c_void_p
+        L.avo_sim_new_threads.argtypes = [C.POINTER(SimConfig), C.c_int32]
+        L.avo_sim_round_ex.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
+                                       C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_int64), C.c_void_p,
+                                       C.c_uint32]
+        L.avo_sim_dump_range.argtypes = [C.c_void_p, C.c_int64, C.c_int64, u32p, C.c_int32]
+        L.avo_pack_update.restype = C.c_uint64
+        L.avo_pack_update.argtypes = [C.c_uint32, C.c_int64, C.c_int32, C.c_int64, C.c_int32]
+        L.avo_transition_batch_branchfree.argtypes = [u32p, u32p, C.c_int64, u32p,
+                                                      np.ctypeslib.ndpointer(np.int8, flags="C_CONTIGUOUS")]
+        L.avo_node_round_ext.restype = C.c_int64
+        L.avo_node_round_ext.argtypes = [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int64, C.c_int64,
+                                         C.c_int64, u32p, u32p, u8p, u32p, C.c_void_p, C.c_uint32]
+        L.avo_byz_words.argtypes = [C.c_uint64, C.c_int64, C.c_uint32, u32p]
+        L.avo_sim_get_round.restype = C.c_int64
+        L.avo_sim_get_round.argtypes = [C.c_void_p, C.c_int64]
+        L.avo_sim_set_round.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
+        L.avo_sim_set_literal.argtypes = [C.c_void_p, C.c_int]
+        L.avo_mix64.restype = C.c_uint64
+        L.avo_mix64.argtypes = [C.c_uint64]
         L.avo_sim_free.argtypes = [C.c_void_p]
         L.avo_sim_set_valid.argtypes = [C.c_void_p, C.c_int64, C.c_int]
         L.avo_sim_round_index.restype = C.c_int64
@@ -91,6 +111,45 @@ def transition_batch(words: np.ndarray, errs: np.ndarray):
     return out, changed, status
 
 
+def pack_update(round_rel, node, slot, t, status):
+    return lib().avo_pack_update(round_rel, node, slot, t, status)
+
+
+def update_digest(words):
+    """(count, sum, xor) of avo_mix64 over packed update words (numpy, same as the C side)."""
+    z = np.asarray(words, np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = z ^ (z >> np.uint64(31))
+    return int(z.size), int(z.sum(dtype=np.uint64)), int(np.bitwise_xor.reduce(z)) if z.size else 0
+
+
+def transition_batch_branchfree(words: np.ndarray, errs: np.ndarray):
+    words = np.ascontiguousarray(words, np.uint32)
+    errs = np.ascontiguousarray(errs, np.uint32)
+    out = np.empty_like(words)
+    status = np.empty(words.shape, np.int8)
+    lib().avo_transition_batch_branchfree(words, errs, words.size, out, status)
+    return out, status
+
+
+def byz_words(seed, n_nodes, threshold):
+    out = np.zeros((n_nodes + 31) // 32, np.uint32)
+    lib().avo_byz_words(seed, n_nodes, threshold, out)
+    return out
+
+
+def node_round_ext(seed, n_nodes, k, peer_mode, node, rnd, m, pref_words, byz_words, valid, words, digest,
+                   round_rel=0):
+    """One node's literal round against the engine's snapshot (avo_node_round_ext).
+    words (uint32[m]) is updated in place; digest (uint64[3]) accumulates."""
+    assert words.dtype == np.uint32 and words.flags["C_CONTIGUOUS"] and digest.dtype == np.uint64
+    return lib().avo_node_round_ext(seed, n_nodes, k, peer_mode, node, rnd, m,
+                                    np.ascontiguousarray(pref_words, np.uint32),
+                                    np.ascontiguousarray(byz_words, np.uint32), np.ascontiguousarray(valid, np.uint8),
+                                    words, digest.ctypes.data_as(C.c_void_p), round_rel)
+
+
 def sample_peers(seed, node, rnd, n_nodes, k, mode=0):
     out = np.zeros(k, np.int64)
     lib().avo_sample_peers(seed, node, rnd, n_nodes, k, mode, out)
@@ -107,10 +166,10 @@ class Sim:
     """Batched-round harness over one restated Processor per node."""
 
     def __init__(self, n_nodes, n_targets, k=8, seed=0xA7A1A9C4, peer_mode=0, byz_threshold=0,
-                 init_mode=3, init_param=0x80000000):
+                 init_mode=3, init_param=0x80000000, threads=1):
         self.cfg = SimConfig(n_nodes, n_targets, k, peer_mode, seed, byz_threshold, init_mode, init_param)
         self.n, self.m, self.k = n_nodes, n_targets, k
-        self._h = lib().avo_sim_new(C.byref(self.cfg))
+        self._h = lib().avo_sim_new_threads(C.byref(self.cfg), threads)
 
     def close(self):
         if self._h:
@@ -122,6 +181,16 @@ class Sim:
     @property
     def round(self):
         return lib().avo_sim_round_index(self._h)
+
+    def get_round(self, node):
+        return lib().avo_sim_get_round(self._h, node)
+
+    def set_round(self, node, rnd):
+        lib().avo_sim_set_round(self._h, node, rnd)
+
+    def set_literal(self, literal=True):
+        """Force the literal per-vote path (cross-check of the branch-free one)."""
+        lib().avo_sim_set_literal(self._h, int(literal))
 
     def set_valid(self, t, valid):
         lib().avo_sim_set_valid(self._h, t, int(valid))
@@ -138,8 +207,10 @@ class Sim:
         lib().avo_sim_register_votes(self._h, node, targets, errs, len(targets), ot, os_, C.byref(n))
         return list(zip(ot[: n.value].tolist(), os_[: n.value].tolist()))
 
-    def run_round(self, replay_errs=None, threads=1):
-        """Returns (updates int64[n,5] (round,node,slot,target,status), applied_votes)."""
+    def run_round(self, replay_errs=None, threads=1, collect=True, round_rel=0):
+        """Returns (updates int64[n,5] (round,node,slot,target,status), applied_votes).
+        collect=False: no rows; returns (digest (count, sum, xor) of the round's
+        packed updates with round field `round_rel`, applied_votes)."""
         n = C.c_int64(0)
         applied = C.c_int64(0)
         rp = None
@@ -147,10 +218,15 @@ class Sim:
             replay_errs = np.ascontiguousarray(replay_errs, np.uint32)
             assert replay_errs.shape == (self.n, self.k, self.m)
             rp = replay_errs.ctypes.data_as(C.c_void_p)
+        dig = np.zeros(3, np.uint64)
+        if not collect:
+            lib().avo_sim_round_ex(self._h, 0, self.n, rp, None, 0, C.byref(n), threads, C.byref(applied),
+                                   dig.ctypes.data_as(C.c_void_p), round_rel)
+            return tuple(int(v) for v in dig), applied.value
         cap = self.n * self.m * 2 + 16
         buf = np.empty((cap, 5), np.int64)
-        rc = lib().avo_sim_round(self._h, rp, buf.ctypes.data_as(C.c_void_p), cap, C.byref(n), threads,
-                                 C.byref(applied))
+        rc = lib().avo_sim_round_ex(self._h, 0, self.n, rp, buf.ctypes.data_as(C.c_void_p), cap, C.byref(n),
+                                    threads, C.byref(applied), dig.ctypes.data_as(C.c_void_p), round_rel)
         assert rc == 0, "oracle update buffer too small"
         return buf[: n.value].copy(), applied.value
 
@@ -169,9 +245,10 @@ class Sim:
         rows = np.ascontiguousarray(rows, np.uint8)
         lib().avo_sim_set_pref_rows(self._h, n0, n0 + rows.shape[0], rows)
 
-    def dump(self):
-        out = np.empty((self.n, self.m), np.uint32)
-        lib().avo_sim_dump(self._h, out)
+    def dump(self, n0=0, n1=None, threads=1):
+        n1 = self.n if n1 is None else n1
+        out = np.empty((n1 - n0, self.m), np.uint32)
+        lib().avo_sim_dump_range(self._h, n0, n1, out, threads)
         return out
 
     def pref(self):

@@ -85,6 +85,12 @@ class Ops:
     def confidence(self, h, expect, line):
         self.ops.append({"op": "confidence", "hash": h, "expect": expect, "line": line})
 
+    def get_round(self, expect, line):
+        self.ops.append({"op": "get_round", "expect": expect, "line": line})
+
+    def inc_round(self, line):
+        self.ops.append({"op": "inc_round", "line": line})
+
 
 def block_register():
     """TestBlockRegister, avalanche_test.go:93-252. Block 65 = staticTestBlockMap
@@ -156,12 +162,16 @@ def multi_block_register():
     a, b = 65, 66
     both = [[0, b], [0, a]]
     o = Ops()
+    o.get_round(0, 268)  # round := p.GetRound() of a NewProcessor (processor.go:28-37 leaves it 0)
     o.is_accepted(a, False, 290)
     o.is_accepted(b, False, 291)
     o.add(a, True, 294)
     o.poll_count(1, 295)
     o.poll_contains(a, 296)
     o.register(0, [[0, a]], [], 298)
+    o.get_round(0, 298)  # registering votes does not advance it
+    o.inc_round(302)     # p.round++
+    o.get_round(1, 302)
     o.add(b, True, 303)
     o.poll_count(2, 304)
     for _ in range(4):
@@ -173,6 +183,7 @@ def multi_block_register():
     o.poll_contains(b, 347)
     o.register(0, [[0, b]], [[b, FINALIZED]], 351)
     o.poll_count(0, 362)
+    o.get_round(1, 362)
     return {"name": "TestMultiBlockRegister", "source": "avalanche_test.go:254-363 (minus :307-313)",
             "targets": {str(a): {"accepted": True, "valid": True}, str(b): {"accepted": True, "valid": True}},
             "ops": o.ops}

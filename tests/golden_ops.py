@@ -26,7 +26,8 @@ def run_vote_record(fx, make_record):
 
 def run_processor(fx, proc):
     """proc implements add(hash)->bool, register(node, votes[[err, hash]...]) -> [(hash, status)],
-    is_accepted(hash)->bool, confidence(hash)->int (raise NotFound), invs()->[hash]."""
+    is_accepted(hash)->bool, confidence(hash)->int (raise NotFound), invs()->[hash],
+    get_round()->int, inc_round() (the test's p.round++)."""
     for i, op in enumerate(fx["ops"]):
         where = f"{fx['name']} op {i} (avalanche_test.go:{op['line']})"
         kind = op["op"]
@@ -43,5 +44,9 @@ def run_processor(fx, proc):
             assert got == op["expect_updates"], f"{where}: got {got}"
         elif kind == "confidence":
             assert proc.confidence(op["hash"]) == op["expect"], where
+        elif kind == "get_round":
+            assert proc.get_round() == op["expect"], where
+        elif kind == "inc_round":
+            proc.inc_round()
         else:
             raise AssertionError(f"unknown op {kind}")

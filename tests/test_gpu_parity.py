@@ -237,6 +237,12 @@ class EngineProc:
     def invs(self):
         return self.eng.get_invs(0).tolist()
 
+    def get_round(self):
+        return self.eng.get_round(0)
+
+    def inc_round(self):
+        self.eng.set_round(0, self.eng.get_round(0) + 1)
+
 
 @pytest.mark.parametrize("which", [0, 1])
 def test_processor_golden_gpu(golden, which):

@@ -137,3 +137,74 @@ def _world1_main(q):
         q.put("ok")
     except Exception as ex:
         q.put(f"error: {ex!r}")
+
+
+def _absent_main(world, rank, d, q):
+    """Rank 1 maps the exchange and then never takes part in a round."""
+    try:
+        import avhip
+
+        n, m = 128, 64
+        per = n // world
+        e = avhip.Engine(n, m, k=8, seed=3, node_range=(rank * per, (rank + 1) * per), device=0)
+        e.init_records(3, P80)
+        e.set_option("barrier_timeout_ms", 1500)
+        tmp = os.path.join(d, f"h{rank}.tmp")
+        with open(tmp, "wb") as f:
+            f.write(e.peer_handles())
+        os.rename(tmp, os.path.join(d, f"h{rank}.bin"))
+        t0 = time.time()
+        paths = [os.path.join(d, f"h{r}.bin") for r in range(world)]
+        while not all(os.path.exists(p) for p in paths):
+            if time.time() - t0 > 60:
+                raise TimeoutError("peer handles did not arrive")
+            time.sleep(0.05)
+        handles = [open(p, "rb").read() for p in paths]
+        e.peer_init(world, rank, handles)
+        done = os.path.join(d, "rank0.done")
+        if rank == 1:  # absent: wait (engine mapped) until rank 0 has seen the failure
+            while not os.path.exists(done) and time.time() - t0 < 90:
+                time.sleep(0.05)
+            e.close()
+            q.put((rank, "ok"))
+            return
+        e.run_rounds(1)  # its barrier waits for rank 1, which never arrives
+        seen = []
+        for name, call in [("synchronize", e.synchronize), ("run_rounds", lambda: e.run_rounds(1)),
+                           ("read_records", e.read_records), ("fetch_updates", e.fetch_updates),
+                           ("applied_votes", e.applied_votes)]:
+            try:
+                call()
+                seen.append(f"{name}: accepted")
+            except avhip.PeerExchangeFailed:
+                seen.append(f"{name}: refused")
+        open(done, "w").close()
+        e.close()
+        q.put((rank, "ok" if all(s.endswith("refused") for s in seen) else f"error: {seen}"))
+    except Exception as ex:
+        open(os.path.join(d, "rank0.done"), "w").close()
+        q.put((rank, f"error: {ex!r}"))
+
+
+def test_peer_barrier_timeout_fails_engine(tmp_path):
+    """A rank that never arrives at the round barrier: the barrier gives up
+    after its timeout and every later round and result of the engine is
+    refused with AV_ERR_PEER (sticky), instead of running rounds unordered."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_absent_main, args=(2, r, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    deadline = time.time() + 100
+    while len(res) < 2 and time.time() < deadline:
+        try:
+            r, msg = q.get(timeout=1)
+            res[r] = msg
+        except Exception:
+            pass
+    for p in procs:
+        p.join(timeout=max(1, deadline - time.time()))
+        if p.is_alive():
+            p.kill()
+    assert res == {0: "ok", 1: "ok"}, res

@@ -67,6 +67,12 @@ class CProc:
         w = self.words()
         return [t for t in range(self.m) if (int(w[t]) >> 17) < 128][:4096]
 
+    def get_round(self):
+        return self.sim.get_round(0)
+
+    def inc_round(self):
+        self.sim.set_round(0, self.sim.get_round(0) + 1)
+
 
 class PyProc:
     def __init__(self, fx):
@@ -92,6 +98,12 @@ class PyProc:
 
     def invs(self):
         return self.p.get_invs_for_next_poll()
+
+    def get_round(self):
+        return self.p.get_round()
+
+    def inc_round(self):
+        self.p.round += 1
 
 
 # ---------------------------------------------------------------- golden vectors
@@ -258,4 +270,66 @@ def test_oracle_threads_deterministic(oracle):
         u1, n1 = a.run_round(threads=1)
         u2, n2 = b.run_round(threads=4)
         assert np.array_equal(u1, u2) and n1 == n2
+    assert np.array_equal(a.dump(), b.dump())
+
+
+def test_branchfree_step_vs_literal_exhaustive(oracle):
+    """The oracle's branch-free step (the batched sim's fast form) equals the
+    literal avo_register_vote (vote.go:54-75) on every reachable record state
+    and every err class, including the finalizing step (count 127 -> 128)."""
+    w = reachable_words()
+    for e in REPR_ERRS:
+        errs = np.full(w.shape, e, np.uint32)
+        exp, ch, st = oracle.transition_batch(w, errs)
+        got, gst = oracle.transition_batch_branchfree(w, errs)
+        assert np.array_equal(got, exp), hex(e)
+        assert np.array_equal(gst, np.where(ch.astype(bool), st.astype(np.int8), -1)), hex(e)
+
+
+BF_CASES = [
+    dict(n=300, m=517, k=8, seed=5, init_mode=4, byz=int(0.2 * 2**32)),
+    dict(n=64, m=200, k=8, seed=3, init_mode=2),
+    dict(n=40, m=96, k=5, seed=8, init_mode=3, init_param=int(0.8 * 2**32), peer_mode=1),
+    dict(n=9, m=33, k=8, seed=4, init_mode=1, byz=int(0.45 * 2**32)),
+    dict(n=20, m=4500, k=8, seed=6, init_mode=2),   # M > 4096: cap binds -> literal path per node
+    dict(n=30, m=300, k=8, seed=9, init_mode=3, replay=True),
+]
+
+
+@pytest.mark.parametrize("case", BF_CASES, ids=lambda c: f"n{c['n']}m{c['m']}k{c['k']}")
+def test_sim_branchfree_vs_literal(oracle, case):
+    """The batched sim's branch-free per-node form == the literal per-vote
+    path (GetInvsForNextPoll + RegisterVotes per slot) through finalization,
+    validity flips and replayed neutral votes."""
+    kw = dict(seed=case["seed"], peer_mode=case.get("peer_mode", 0), byz_threshold=case.get("byz", 0),
+              init_mode=case["init_mode"], init_param=case.get("init_param", 0x80000000))
+    a = oracle.Sim(case["n"], case["m"], case["k"], threads=3, **kw)
+    b = oracle.Sim(case["n"], case["m"], case["k"], **kw)
+    b.set_literal()
+    for r in range(22):
+        if r == 4:
+            a.set_valid(2, False)
+            b.set_valid(2, False)
+        if r == 9:
+            a.set_valid(2, True)
+            b.set_valid(2, True)
+        errs = oracle.gen_replay_errs(case["seed"], r, 0, case["n"], case["m"], case["k"]) if case.get("replay") else None
+        ua, na = a.run_round(errs, threads=3)
+        ub, nb = b.run_round(errs)
+        assert na == nb and np.array_equal(ua, ub), r
+    assert np.array_equal(a.dump(), b.dump())
+
+
+def test_digest_mode_matches_rows(oracle):
+    kw = dict(seed=11, byz_threshold=int(0.2 * 2**32), init_mode=4)
+    a = oracle.Sim(200, 300, 8, **kw)
+    b = oracle.Sim(200, 300, 8, **kw)
+    for r in range(6):
+        u, na = a.run_round(threads=2)
+        d, nb = b.run_round(threads=2, collect=False, round_rel=3)
+        words = ((np.uint64(3) << np.uint64(52)) | (u[:, 1].astype(np.uint64) << np.uint64(28))
+                 | (u[:, 2].astype(np.uint64) << np.uint64(24)) | (u[:, 3].astype(np.uint64) << np.uint64(2))
+                 | u[:, 4].astype(np.uint64))
+        assert na == nb and d == oracle.update_digest(words), r
+        assert int(words[0]) == oracle.pack_update(3, int(u[0, 1]), int(u[0, 2]), int(u[0, 3]), int(u[0, 4]))
     assert np.array_equal(a.dump(), b.dump())

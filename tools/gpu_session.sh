@@ -28,7 +28,8 @@ step() {  # name, timeout-seconds, command...
 for s in "$@"; do
   case $s in
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step pytest_gpu 1500 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    tests) step pytest_gpu 1500 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    testsnew) step pytest_new 1200 python -u -m pytest tests/test_gpu_delivery.py tests/test_gpu_fullsize.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py ;;
     rccl2) step rccl2 240 python tools/rccl_two_rank_probe.py ;;
