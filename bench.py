@@ -83,8 +83,8 @@ PARALLELISM = {
 }
 
 KERNEL_SRC = [os.path.join(ROOT, "go-avalanche_amd", "csrc", f) for f in
-              ("round_sweep.hip", "round_node.hip", "kernels.hip", "round_common.h", "round_slots.h", "kernels.h",
-               "engine.cpp")]
+              ("round_sweep.hip", "round_node.hip", "kernels.hip", "log_ops.hip", "round_common.h", "round_slots.h",
+               "kernels.h", "engine.cpp")]
 
 
 class BenchFailure(SystemExit):
@@ -147,7 +147,8 @@ def cpu_baseline(wl, seed, budget_s):
         avail = os.cpu_count() or 1
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
     threads = max(1, min(threads, 16, avail))
-    ns = min(n, 80000 if wl != "c2" else 400)
+    # ~10-20 s of CPU work on a 16-core host (the branch-free oracle runs ~6e9 updates/s there)
+    ns = min(n, 500_000 if wl != "c2" else 1000)
     sim = cabi.Sim(ns, m, k, seed=seed, byz_threshold=byz, init_mode=init_mode, init_param=init_param,
                    threads=threads)
     applied = 0
@@ -307,7 +308,11 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     # HIP events on the engine's stream
     kern_ms = launches = 0
     moved = 0
+    applied2 = emitted2 = 0
     if not args.no_roofline_pass:
+        # the same steps of fresh epochs; the peer draws follow the engine's
+        # absolute round counter, so the StatusUpdate count differs slightly
+        # from the timed pass (the applied votes do not: every record is live)
         run.goto(warmup)
         b0 = eng.alg_bytes()
         eng.set_timing(True)
@@ -315,9 +320,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         eng.set_timing(False)
         kern_ms, launches = eng.kernel_stats()
         moved = eng.alg_bytes() - b0
-        if (applied2, emitted2) != (applied, emitted):
-            raise BenchFailure(f"bench: roofline pass differs from the timed pass ({applied2}, {emitted2}) vs "
-                               f"({applied}, {emitted})")
+        if applied2 != applied:
+            raise BenchFailure(f"bench: roofline pass applied {applied2} votes, the timed pass {applied}")
     replicas = None
     if world > 1 and args.shard in ("peers", "nodes"):
         # every rank's replica of the published preferences must be the same:
@@ -346,9 +350,10 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     gen2 = k <= 8 and args.kernel != 1
     kname = (("k_round_node" if gen2 else "k_round_capped") if info["capped"]
              else ("k_round_sweep" if gen2 else "k_round_fast")) + f"<{k},{'true' if replay else 'false'}>"
-    # SURVEY.md §8(d) bytes of this rank's launches: every applied vote is one
-    # live (node, target, round) triple / k; + 20 B per emitted StatusUpdate
-    s8d = (applied / k * S8D_TRIPLE_BYTES[replay] + emitted * S8D_UPDATE_BYTES) / launches if launches else None
+    # SURVEY.md §8(d) bytes of this rank's launches in the roofline pass: every
+    # applied vote is one live (node, target, round) triple / k; + 20 B per
+    # emitted StatusUpdate
+    s8d = (applied2 / k * S8D_TRIPLE_BYTES[replay] + emitted2 * S8D_UPDATE_BYTES) / launches if launches else None
     return {
         "wl": wl, "desc": desc, "n": n, "m": m, "k": k, "elapsed": elapsed, "applied": applied_all,
         "emitted": emitted_all, "value": applied_all / elapsed, "segments": segs, "info": info,

@@ -51,6 +51,46 @@ __device__ __forceinline__ uint32_t cap_select(uint32_t live, uint32_t lane, uin
   return lowest_bits(live, kMaxPoll - excl);
 }
 
+// The state loads of one lane beyond its K4-7 group and A plane (V, K0-3,
+// C, the replayed vote planes, or the peer gather).
+template <int K, bool REPLAY, bool NT>
+struct NodeLane {
+  u32x4 v0, v1, k0;
+  uint32_t C[8];
+  uint32_t w[K], cw[REPLAY ? K : 1];
+};
+
+template <int K, bool REPLAY, bool NT>
+__device__ __forceinline__ void node_lane_load(const RoundParams& p, uint32_t* tp, u32x4* grp, uint32_t tl, uint32_t g,
+                                               uint32_t bc, uint32_t node, uint32_t nl, uint32_t lane,
+                                               NodeLane<K, REPLAY, NT>& in) {
+  in.v0 = pld4<NT>(grp);
+  in.v1 = pld4<NT>(grp + 64);
+  in.k0 = pld4<NT>(grp + 128);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) in.C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
+  if constexpr (REPLAY) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      in.cw[j] = p.replay[(size_t)(2 * j + 1) * p.Lpad + g];
+      in.w[j] = p.replay[(size_t)(2 * j) * p.Lpad + g];
+    }
+  } else {
+    uint32_t peers[K];
+    draw_peers<K>(p, p.round, node, nl, nl, 1u, lane, peers);  // every lane of the workgroup is the same node
+#pragma unroll
+    for (int j = 0; j < K; ++j) in.w[j] = p.pref_in[peers[j] * p.BL + bc];  // < N * BL < 2^31 (engine check)
+  }
+}
+
+// One workgroup per node, one lane per 32-record block. Only the first
+// kMaxPoll live valid records of the node are polled (processor.go:165-167),
+// so the lanes of blocks b >= kMaxPoll / 32 (C2: 185 of 313) are polled only
+// when dead or invalid records come before them. Those lanes load their K4-7
+// group and A plane only; after the workgroup prefix count, a wave with a
+// polled record loads the rest (rare), a wave without one just republishes A
+// (24 B per lane instead of ~270). Lanes of blocks b < kMaxPoll / 32 can
+// always be polled and issue every load at once.
 template <int K, bool REPLAY, bool NT, int MAXT>
 __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
   __shared__ uint32_t wsum[2][16];
@@ -61,69 +101,71 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
   const uint32_t bc = active ? b : p.BL - 1u;  // inactive lanes read a valid lane, never store
   const uint32_t g = nl * p.BL + bc;
   const uint32_t node = p.n0 + nl;
+  const bool early = b < kMaxPoll / 32u;  // wave-uniform (128 lanes = 2 waves)
 
   // ---- state (tile layout of kernels.h: per-lane dwordx4 V/K groups, dword C/A planes)
   uint32_t* const tp = p.planes + (size_t)(g >> 6) * (kPlanes * 64u);
   const uint32_t tl = g & 63u;
   u32x4* const grp = reinterpret_cast<u32x4*>(tp) + tl;
-  const u32x4 v0 = pld4<NT>(grp), v1 = pld4<NT>(grp + 64), k0 = pld4<NT>(grp + 128), k1 = pld4<NT>(grp + 192);
+  const u32x4 k1 = pld4<NT>(grp + 192);
   uint32_t A = pld<NT>(tp + 1536u + tl);
-  uint32_t C[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
   const uint32_t vmask = active ? p.valid[bc] : 0u;
+  NodeLane<K, REPLAY, NT> in;
+  if (early) node_lane_load<K, REPLAY, NT>(p, tp, grp, tl, g, bc, node, nl, lane, in);
+
+  const uint32_t live0 = ~k1[3];
+  const uint32_t P0 = live0 & vmask;  // live and IsValid (processor.go:95-103)
+  const uint32_t polled = cap_select(P0, lane, wave, wsum, 0u);
+  const bool heavy = early || __ballot(polled != 0u) != 0ull;  // wave-uniform
+  if (!early && heavy) node_lane_load<K, REPLAY, NT>(p, tp, grp, tl, g, bc, node, nl, lane, in);
+  const uint32_t nearfin = heavy ? polled & k1[2] & k1[1] & k1[0] & in.k0[3] : 0u;  // count >= 120
+  const bool exact = __syncthreads_or(nearfin != 0u) != 0;  // workgroup-uniform
+
+  if (exact) {  // some polled record may reach 128: the exact pass (k_round_capped) takes this node
+    if (b == 0) p.node_flags[nl] = 1u;
+    return;
+  }
+  const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
+  const uint32_t prow = node * p.BL + b;
+  const uint32_t pub_byz = is_byz(p.byz, node) ? 1u : 0u;
+  if (!heavy) {  // nothing polled in this wave: records unchanged, A republished
+    if (active) p.pref_out[prow] = pub_byz ? byz_pattern(p.round + 1u) : A;
+    count_stats(p, wave_id, lane, 0u, active, 16u + 4u + 4u, 0u, 0u, 0u);
+    return;
+  }
 
   // ---- votes of this round: ys/ns hold y/n of [V_6..V_0, w_0..w_{K-1}]
   uint32_t ys[7 + K], ns[7 + K], cwv[K];
-  if constexpr (REPLAY) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const uint32_t cw = p.replay[(size_t)(2 * j + 1) * p.Lpad + g];
-      const uint32_t yw = p.replay[(size_t)(2 * j) * p.Lpad + g] & cw;  // err == 0 implies considered
-      ys[7 + j] = yw;
-      ns[7 + j] = ~yw & cw;
-      cwv[j] = cw;
-    }
-  } else {
-    uint32_t peers[K];
-    draw_peers<K>(p, p.round, node, nl, nl, 1u, lane, peers);  // every lane of the workgroup is the same node
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const uint32_t w = p.pref_in[peers[j] * p.BL + bc];  // < N * BL < 2^31 (engine check)
-      ys[7 + j] = w;
-      ns[7 + j] = ~w;
-      cwv[j] = ~0u;
-    }
+  for (int j = 0; j < K; ++j) {
+    const uint32_t cw = REPLAY ? in.cw[REPLAY ? j : 0] : ~0u;
+    const uint32_t yw = in.w[j] & cw;  // err == 0 implies considered
+    ys[7 + j] = yw;
+    ns[7 + j] = ~yw & cw;
+    cwv[j] = cw;
   }
+  const u32x4 v0 = in.v0, v1 = in.v1, k0 = in.k0;
+  const uint32_t* const C = in.C;
 #pragma unroll
   for (int i = 0; i < 7; ++i) {  // old planes V_6..V_0
     const uint32_t vi = (6 - i) < 4 ? v0[6 - i] : v1[2 - i];
     ys[i] = vi & C[6 - i];
     ns[i] = ~vi & C[6 - i];
   }
-
-  const uint32_t live0 = ~k1[3];
-  const uint32_t P0 = live0 & vmask;  // live and IsValid (processor.go:95-103)
-  uint32_t polled = cap_select(P0, lane, wave, wsum, 0u);
   uint32_t Kp[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     Kp[i] = k0[i];
     Kp[4 + i] = k1[i];
   }
-  const uint32_t nearfin = polled & Kp[6] & Kp[5] & Kp[4] & Kp[3];  // count >= 120
-  const bool exact = __syncthreads_or(nearfin != 0u) != 0;          // workgroup-uniform
-
-  if (exact) {  // some polled record may reach 128: the exact pass (k_round_capped) takes this node
-    if (b == 0) p.node_flags[nl] = 1u;
-    return;
-  }
   uint32_t E[K], applied = 0u;
   const uint32_t died = 0u;
   // the poll set is fixed for the round: every polled record shifts by K
   // votes; its V/C planes are final now (stored before the slot loop so
-  // their registers are free during it)
-  if (active) {
+  // their registers are free during it). A lane with no polled record keeps
+  // its planes: no stores.
+  const bool any = polled != 0u;
+  if (active && any) {
     u32x4 o0, o1;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -157,22 +199,25 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
   }
 
   if (active) {
-    u32x4 o2, o3;
+    if (any) {
+      u32x4 o2, o3;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      o2[i] = Kp[i];
-      o3[i] = Kp[4 + i];
+      for (int i = 0; i < 4; ++i) {
+        o2[i] = Kp[i];
+        o3[i] = Kp[4 + i];
+      }
+      pst4<NT>(grp + 128, o2);
+      pst4<NT>(grp + 192, o3);
+      pst<NT>(tp + 1536u + tl, A);
     }
-    pst4<NT>(grp + 128, o2);
-    pst4<NT>(grp + 192, o3);
-    pst<NT>(tp + 1536u + tl, A);
-    p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
+    p.pref_out[prow] = pub_byz ? byz_pattern(p.round + 1u) : A;
   }
-  const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
   uint32_t upd = 0;
   const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, died, upd);
-  count_stats(p, wave_id, lane, applied, active, 2u * kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u, emitted, upd,
-              died);
+  // bytes: a lane of a polling wave reads all 25 planes and its k vote words,
+  // writes its published word, and writes its planes back if it polled a record
+  const uint32_t lane_bytes = kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u + (any ? kPlanes * 4u : 0u);
+  count_stats(p, wave_id, lane, applied, active, lane_bytes, emitted, upd, died);
 }
 
 template <int K, int MAXT>

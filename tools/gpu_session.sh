@@ -41,6 +41,7 @@ for s in "$@"; do
             --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --rehearse-one-gpu --no-secondary --shard peers ;;
     rehearse4p) step rehearse4p 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
             --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --rehearse-one-gpu --no-secondary --shard peers ;;
+    capped) step capped 600 python -u -m pytest tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "capped or c2 or replay or fuzz or poll_sets" ;;
     peertests) step peertests 600 python -u -m pytest tests/test_gpu_peer_push.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     nsprobe) step nsprobe 600 python tools/node_shard_probe.py --json $OUT/node_shard_probe.json ;;
     ab) step ab 900 python tools/ab_tune.py --json $OUT/ab.json ;;
