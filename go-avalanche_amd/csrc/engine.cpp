@@ -113,6 +113,9 @@ struct av_engine {
   // live record was polled (all targets valid, uncapped); cleared by anything that can write a 0
   // consider bit (init, add, write_records, drop-in votes, replay)
   bool warm_all = false;
+  // every record is a NewVoteRecord from av_init_records (votes = consider =
+  // count = 0): the next sweep round reads only the A plane (kernels.h fresh)
+  bool fresh = false;
   uint32_t bl_magic = 1, bl_sh1 = 0, bl_sh2 = 0;
   uint32_t store_policy = 0;  // option "store_policy": 2 = sc1 (write-through) plane stores, 3 = nt sc1
   // upper bound on any live record's count (confidence >> 1) at the start of the next round: a
@@ -241,6 +244,9 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.bl_sh2 = e->bl_sh2;
   p.kpend = e->kpend;
   p.klazy = 0u;
+  p.kconsume = 0u;
+  p.fresh = 0u;
+  p.tn = (uint32_t)(e->t1 - e->t0);
   return p;
 }
 
@@ -348,25 +354,32 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
            "node-sharded engine needs av_comm_init before running rounds");
   avk::RoundParams p = round_params(e, replay);
   const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped;
-  // vote planes may be left unstored: the sweep's warm sim modes at k = 8 (launch_sweep_k)
-  const bool vv = e->virtual_votes && sweep && e->k == 8 && !replay && e->c_monotone && e->warm_all &&
-                  !e->ablate_gather && e->BL >= e->vv_min_bl;
+  // the round after av_init_records: planes known to be zero are not read
+  const bool fresh = e->fresh && sweep && !replay && !e->ablate_gather;
+  // the sweep's warm sim modes (launch_sweep_k): every consider plane all-ones
+  const bool warm = sweep && !replay && e->c_monotone && e->warm_all && !e->ablate_gather && !fresh;
+  // vote planes may be left unstored: warm (or fresh) k = 8 sim rounds
+  const bool vv = e->virtual_votes && e->k == 8 && e->BL >= e->vv_min_bl && (warm || fresh);
   if (!vv) {
     int rc = materialize_votes_only(e);
     if (rc != AV_OK) return rc;
   }
   p.vv = vv ? 1u : 0u;
   if (vv) e->v_stale = true;
-  // count planes may be deferred: the sweep's warm k = 8 sim modes, while no
-  // record can finalize (every true count < 120 at round start)
-  const bool klazy = e->count_lazy && sweep && e->k == 8 && !replay && e->c_monotone && e->warm_all &&
-                     !e->ablate_gather && e->count_bound < 120;
-  if (!klazy) {
+  p.fresh = fresh ? 1u : 0u;
+  // count planes may be deferred: warm k = 8 sim rounds while no record can
+  // finalize (every true count < 120 at round start); the first warm round
+  // that can finalize applies the pending steps itself (kconsume)
+  const bool klazy = e->count_lazy && warm && e->k == 8 && e->count_bound < 120;
+  const bool kconsume = !klazy && e->k_pend && warm && e->k == 8;
+  if (!klazy && !kconsume) {
     int rc = materialize_counts(e);
     if (rc != AV_OK) return rc;
   }
   p.klazy = klazy ? 1u : 0u;
+  p.kconsume = kconsume ? 1u : 0u;
   if (klazy) e->k_pend = true;
+  if (kconsume) e->k_pend = false;
   bool all_valid = true;
   for (uint32_t b = 0; b < e->BL; ++b) {
     const int64_t tb = e->t0 + 32ll * b;
@@ -397,6 +410,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   else
     AV_HIP(avk::launch_round(p, e->k, replay != nullptr, e->capped, e->stream));
   e->count_bound = std::min(127, e->count_bound + e->k);
+  e->fresh = false;
   if (replay)
     e->warm_all = false;
   else if (e->c_monotone && e->k >= 8 && !e->capped && all_valid)
@@ -657,6 +671,7 @@ int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
   p.mode = init_mode;
   p.param = init_param;
   AV_HIP(avk::launch_init(p, e->stream));
+  e->fresh = init_mode != AV_INIT_NONE;
   // lanes of the padded tail of the last tile hold no records
   if (e->Lpad > e->L) {
     // padded lanes are never loaded (active = g < L), nothing to do
@@ -693,6 +708,7 @@ int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uin
     if (rc != AV_OK) return rc;
   }
   e->warm_all = false;
+  e->fresh = false;
   std::vector<uint32_t> tl;
   std::vector<uint8_t> acc;
   std::vector<int64_t> pos;
@@ -747,6 +763,7 @@ int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const 
     if (rc != AV_OK) return rc;
   }
   for (int64_t i = 0; i < n; ++i) status_out[i] = -1;
+  e->fresh = false;
   e->count_bound = std::min<int64_t>(127, e->count_bound + n);  // at most one step per vote
   // group votes by block, keeping Response order inside each block
   std::vector<uint32_t> cnt(e->BL + 1, 0);
@@ -851,6 +868,7 @@ int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t
   const size_t n = (size_t)(n1 - n0) * (size_t)(t1 - t0);
   if (!n) return AV_OK;
   e->c_monotone = false;
+  e->fresh = false;
   e->count_bound = 127;  // arbitrary counts written
   Scratch s;
   AV_HIP(s.ensure(n * 4));
@@ -1358,6 +1376,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   } else if (n == "vv_min_bl") {
     AV_CHECK(value >= 1 && value < (1ll << 31), AV_ERR_INVALID_ARG, "bad vv_min_bl");
     e->vv_min_bl = (uint32_t)value;
+  } else if (n == "fresh") {  // 0: a round after init reads every plane (A/B only)
+    if (!value) e->fresh = false;
   } else if (n == "peer_fine") {  // before av_peer_handles: fine-grained snapshot buffers (default 1)
     AV_CHECK(!e->arrive, AV_ERR_INVALID_ARG, "peer_fine must be set before av_peer_handles");
     e->peer_fine = value != 0;

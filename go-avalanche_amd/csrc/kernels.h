@@ -96,6 +96,16 @@ struct RoundParams {
   // be read to find the polled set).
   uint32_t klazy;            // this round may defer count planes
   uint32_t* kpend;           // [tiles]
+  // kconsume: a warm k = 8 sim round that may finalize records (no deferral)
+  // applies the tiles' pending steps itself before it tests for count 120
+  // (instead of a separate write-back pass) and clears kpend.
+  uint32_t kconsume;
+  // fresh: the round right after av_init_records: every record is a
+  // NewVoteRecord (votes = consider = 0, count 0, vote.go:33-35), so the
+  // kernel reads only the A plane; the live mask of a block is its existing
+  // targets (tn = targets in this engine's range).
+  uint32_t fresh;
+  uint32_t tn;
 };
 constexpr uint32_t kPendAllLive = 0x80000000u;
 

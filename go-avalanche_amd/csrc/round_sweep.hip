@@ -44,7 +44,7 @@ struct SweepAcc {
   uint32_t emitted_bytes = 0, updates = 0;  // wave-uniform: StatusUpdate log bytes written, updates emitted
 };
 
-enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3, kModeWarmPipe = 4 };
+enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3, kModeWarmPipe = 4, kModeFresh = 5 };
 
 // Everything one 64-lane tile loads before its round step: the state planes
 // (vote.go:25-29; V0-7 and K0-7 as dwordx4 groups, A, C0-7 unless warm), the
@@ -78,7 +78,7 @@ __device__ __forceinline__ LaneIdx lane_idx(const RoundParams& p, uint32_t tile,
   return x;
 }
 
-template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE, bool VVM = false>
+template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE, bool VVM = false, bool FRESH = false>
 __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
                                           TileIn<K, REPLAY, WARM>& in) {
   const LaneIdx x = lane_idx(p, tile, lane);
@@ -86,26 +86,37 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
   const u32x4* const grp = reinterpret_cast<const u32x4*>(tp) + lane;
   constexpr bool VV = VVM && WARM && !REPLAY && K == 8;  // VVM: the warm sim modes only
   in.stale = VV && p.vv ? uni(p.vstale[tile]) : 0u;
-  if (!in.stale) {
-    in.v0 = ld4<POL>(grp);
-    in.v1 = ld4<POL>(grp + 64);
-  }
   in.kw = 0u;
-  if constexpr (VV) {
-    if (p.klazy) in.kw = uni(p.kpend[tile]);
-  }
-  if (!(in.kw & kPendAllLive)) {
-    in.k0 = ld4<POL>(grp + 128);
-    in.k1 = ld4<POL>(grp + 192);
+  if constexpr (FRESH) {
+    // NewVoteRecords (vote.go:33-35): votes, consider and count all zero; K7
+    // marks the slots past the engine's last target (never added)
+    const uint32_t rem = p.tn - x.b * 32u;
+    const uint32_t real = rem >= 32u ? ~0u : ((1u << rem) - 1u);
+    in.v0 = in.v1 = in.k0 = u32x4{0u, 0u, 0u, 0u};
+    in.k1 = u32x4{0u, 0u, 0u, ~real};
+#pragma unroll
+    for (int i = 0; i < (WARM ? 1 : 8); ++i) in.C[i] = 0u;
   } else {
-    in.k0 = u32x4{0u, 0u, 0u, 0u};
-    in.k1 = u32x4{0u, 0u, 0u, 0u};
+    if (!in.stale) {
+      in.v0 = ld4<POL>(grp);
+      in.v1 = ld4<POL>(grp + 64);
+    }
+    if constexpr (VV) {
+      if (p.klazy || p.kconsume) in.kw = uni(p.kpend[tile]);
+    }
+    if (!(in.kw & kPendAllLive) || !p.klazy) {
+      in.k0 = ld4<POL>(grp + 128);
+      in.k1 = ld4<POL>(grp + 192);
+    } else {
+      in.k0 = u32x4{0u, 0u, 0u, 0u};
+      in.k1 = u32x4{0u, 0u, 0u, 0u};
+    }
+    if constexpr (!WARM) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) in.C[i] = ld1<POL>(tp + 1024u + (uint32_t)i * 64u + lane);
+    }
   }
   in.A = ld1<POL>(tp + 1536u + lane);
-  if constexpr (!WARM) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) in.C[i] = ld1<POL>(tp + 1024u + (uint32_t)i * 64u + lane);
-  }
   in.vmask = x.active ? p.valid[x.b] : 0u;
   in.byzw = p.byz[x.node >> 5];
   if constexpr (REPLAY) {
@@ -185,7 +196,8 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
 
   constexpr bool KL = VVM && WARM && !REPLAY && K == 8;  // deferred count planes possible (kernels.h klazy)
   const bool klazy = KL && p.klazy;                      // wave-uniform: no record can finalize this round
-  const bool kunread = KL && (in.kw & kPendAllLive);     // K planes not loaded: live == valid
+  const bool kcons = KL && p.kconsume;                   // wave-uniform: apply pending steps, defer nothing
+  const bool kunread = klazy && (in.kw & kPendAllLive);  // K planes not loaded: live == valid
   const uint32_t live0 = kunread ? in.vmask : ~k1[3];    // K7 = no live record
   const uint32_t P0 = live0 & vmask;                     // polled: live and IsValid (processor.go:95-103)
   const uint32_t keep = active ? (live0 & ~vmask) : 0u;  // live but !IsValid: untouched (processor.go:101-103)
@@ -196,9 +208,8 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   // a warm sim wave with no live-but-invalid record leaves its V planes
   // unstored: next round (or av materialize) regathers them (kernels.h vv)
   bool virt = false;
-  if constexpr (VVM && WARM && !REPLAY && K == 8) virt = p.vv && __ballot(keep != 0u) == 0ull;
+  if constexpr (VVM && !REPLAY && K == 8) virt = p.vv && __ballot(keep != 0u) == 0ull;
   if (active && !virt) {
-    const uint32_t dead0 = ~(P0 | keep);
     u32x4 o0, o1;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -212,13 +223,14 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     }
     st4<POL>(tr, grp, lane * 16u, o0);
     st4<POL>(tr, grp + 64, 1024u + lane * 16u, o1);
-    if (!WARM) {
+  }
+  if (!WARM && active) {  // consider planes (a fresh tile stores them even when its vote planes stay virtual)
+    const uint32_t dead0 = ~(P0 | keep);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t cs = i < K ? cwv[K - 1 - i] : C[i - K];
-        st1<POL>(tr, tp + 1024u + (uint32_t)i * 64u + lane, (1024u + (uint32_t)i * 64u + lane) * 4u,
-                 (cs & P0) | (C[i] & keep) | dead0);
-      }
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t cs = i < K ? cwv[K - 1 - i] : C[i - K];
+      st1<POL>(tr, tp + 1024u + (uint32_t)i * 64u + lane, (1024u + (uint32_t)i * 64u + lane) * 4u,
+               (cs & P0) | (C[i] & keep) | dead0);
     }
   }
 
@@ -227,6 +239,18 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   for (int i = 0; i < 4; ++i) {
     Kp[i] = k0[i];
     Kp[4 + i] = k1[i];
+  }
+  if (kcons && (in.kw & 0xFFu)) {  // pending +8 steps on the polled records: pend added to count bits 3..6
+    const uint32_t pend = in.kw & 0xFFu;
+    uint32_t cy = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t bi = ((pend >> i) & 1u) ? P0 : 0u;
+      const uint32_t t = Kp[3 + i] ^ bi;
+      const uint32_t si = t ^ cy;
+      cy = (t & cy) | (Kp[3 + i] & bi);
+      Kp[3 + i] = si;
+    }
   }
   uint32_t E[K], alive = P0, applied = 0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u;
   const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
@@ -337,7 +361,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
   }
-  if constexpr (VVM && WARM && !REPLAY && K == 8) {
+  if constexpr (VVM && !REPLAY && K == 8) {
     if (p.vv && lane == 0 && virt != (in.stale != 0u)) p.vstale[tile] = virt ? 1u : 0u;
   }
   if constexpr (KL) {
@@ -348,12 +372,16 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
       const uint32_t kw = (kdefer ? pend + 1u : 0u) | (all_live ? kPendAllLive : 0u);
       if (lane == 0 && kw != in.kw) p.kpend[tile] = kw;
       if (lane == 0) acc.lane_bytes += kw != in.kw ? 8u : 4u;  // kpend word read (+ written)
+    } else if (kcons) {
+      if (lane == 0 && in.kw) p.kpend[tile] = 0u;
+      if (lane == 0) acc.lane_bytes += in.kw ? 8u : 4u;
     }
   }
   const uint32_t emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates);
 
+  // fresh (p.fresh, cold template): no plane is read but A (96 B fewer)
   constexpr uint32_t plane_bytes = WARM ? 2u * 17u * 4u : 2u * kPlanes * 4u;
-  constexpr uint32_t lane_bytes = plane_bytes + (REPLAY ? 8u : 4u) * K + 4u;
+  const uint32_t lane_bytes = plane_bytes + (REPLAY ? 8u : 4u) * K + 4u - (!WARM && p.fresh ? 96u : 0u);
   acc.applied += applied;
   acc.died += (uint32_t)__popc(died);
   // stale: 7 regathered words instead of the 8 V planes read; virt: V planes not written
@@ -373,7 +401,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
 // (kModeWarm for a resident grid: the next tile's loads are issued before the
 // current tile is computed; 93 VGPRs, 5 waves per SIMD).
 template <int K, int MODE, int POL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeReplay || MODE == kModeWarm ? 6 : 7))) void k_round_sweep(const RoundParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeReplay || MODE == kModeWarm || MODE == kModeFresh ? 6 : 7))) void k_round_sweep(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave0 = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * 4u;
@@ -398,6 +426,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         TileIn<K, false, true> in;
         load_tile<K, false, true, POL, false, true>(p, tile, lane, in);
         process_tile<K, false, true, POL, true>(p, tile, lane, in, 0u, acc);
+      } else if constexpr (MODE == kModeFresh) {
+        TileIn<K, false, false> in;
+        load_tile<K, false, false, POL, false, true, true>(p, tile, lane, in);
+        process_tile<K, false, false, POL, true>(p, tile, lane, in, 0u, acc);
       } else if constexpr (MODE == kModeReplay) {
         TileIn<K, true, false> in;
         load_tile<K, true, false, POL, false>(p, tile, lane, in);
@@ -461,6 +493,7 @@ hipError_t launch_sweep_k(const RoundParams& p, bool replay, uint32_t blocks, hi
   const uint32_t grid = std::max(1u, blocks ? std::min(blocks, need) : need);
   if (replay) return launch_mode<K, kModeReplay>(p, grid, s);
   if (p.ablate_gather) return launch_mode<K, kModeAblate>(p, grid, s);
+  if (p.fresh) return launch_mode<K, kModeFresh>(p, grid, s);
   if (p.warm_skip && p.warm_all)  // a resident grid walks several tiles per wave: pipeline them
     return blocks && grid < need ? launch_mode<K, kModeWarmPipe>(p, grid, s) : launch_mode<K, kModeWarm>(p, grid, s);
   return launch_mode<K, kModeCheck>(p, grid, s);

@@ -107,20 +107,22 @@ def test_count_lazy_on_off_identical():
 
 def test_count_lazy_bytes():
     """Per-lane bytes of warm k=8 sim rounds of an all-accepted network (every
-    tile uniform, vote planes recomputed): round 1 reads K (the tile is not yet
-    known all-live) but stores neither K nor A nor V: 172 - 68 = 104 B; from
-    round 2 K is not read either: 136 - 68 = 68 B (7 regathered + 8 gathered
-    words, the A read and the published word). Plus the tile's kpend word:
-    read, and written when it changes (every deferred round)."""
+    tile uniform, vote planes recomputed): round 0 (fresh after init) leaves
+    the vote planes virtual, so round 1 regathers them (7 words for the 8-word
+    V read) and reads K (the tile is not yet known all-live) but stores
+    neither K nor A nor V: 172 - 4 - 68 = 100 B; from round 2 K is not read
+    either: 68 B (7 regathered + 8 gathered words, the A read and the
+    published word). Plus the tile's kpend word: read, and written when it
+    changes (every deferred round)."""
     n, m = 4000, 1000
     e = avhip.Engine(n, m, k=8, seed=1, log_capacity=1 << 22)
     e.init_records(avhip.INIT_ACCEPTED, 0)
     lanes = e.layout_info()["lanes"]
     tiles = (lanes + 63) // 64
-    e.run_rounds(1)  # round 0 cold
+    e.run_rounds(1)  # round 0 fresh: A read, C/K/A/pref written, V virtual
     b = e.alg_bytes()
     e.run_rounds(1)
-    assert e.alg_bytes() - b == lanes * 104 + tiles * 8
+    assert e.alg_bytes() - b == lanes * 100 + tiles * 8
     b = e.alg_bytes()
     e.run_rounds(1)
     assert e.alg_bytes() - b == lanes * 68 + tiles * 8

@@ -1,0 +1,62 @@
+"""The round after av_init_records ("fresh": every record a NewVoteRecord,
+vote.go:33-35, so only the A plane is read) and the warm round that applies
+pending count steps itself instead of a separate write-back pass
+("kconsume", the first round in which a record can reach 128). Both are
+compared with the engine running every plane through memory (option
+"fresh" 0, "count_lazy" 0) and with the oracle."""
+import numpy as np
+import pytest
+
+import avhip
+
+pytestmark = pytest.mark.gpu
+
+BYZ20 = int(0.2 * 2**32)
+P80 = int(0.8 * 2**32)
+
+CASES = [
+    # n, m, k, byz, init_mode, invalid targets before round 0
+    (300, 1000, 8, 0, avhip.INIT_BERNOULLI, ()),        # BL 32: fresh + virtual votes
+    (500, 517, 8, BYZ20, avhip.INIT_PAIRS, (3, 516)),    # ragged last block, invalid targets: keep records
+    (700, 200, 8, 0, avhip.INIT_ACCEPTED, ()),           # BL 7: fresh, no virtual votes
+    (90, 333, 5, BYZ20, avhip.INIT_REJECTED, (0,)),      # k = 5
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"n{c[0]}m{c[1]}k{c[2]}")
+def test_fresh_round_vs_oracle(oracle, case):
+    n, m, k, byz, init_mode, invalid = case
+    eng = avhip.Engine(n, m, k=k, seed=17, byz_threshold=byz, log_capacity=1 << 22)
+    eng.init_records(init_mode, P80)
+    sim = oracle.Sim(n, m, k, seed=17, byz_threshold=byz, init_mode=init_mode, init_param=P80)
+    for t in invalid:
+        eng.set_valid(t, False)
+        sim.set_valid(t, False)
+    for r in range(20):
+        eng.run_rounds(1)
+        exp, _ = sim.run_round()
+        assert np.array_equal(eng.fetch_updates(), exp), r
+        if r in (0, 1, 15, 16, 19):
+            assert np.array_equal(eng.read_records(), sim.dump()), r
+
+
+def test_fresh_and_kconsume_identical_to_stored_planes():
+    """C4 shape at 1/50 scale through finalization: the fresh round 0 and the
+    consuming round 15 change nothing but the bytes moved; a re-initialised
+    engine is fresh again."""
+    n, m = 20_000, 1000
+    out = []
+    for opt in (0, 1):
+        e = avhip.Engine(n, m, k=8, seed=0xA7A1A9C4, log_capacity=1 << 27)
+        e.set_option("count_lazy", opt)
+        for epoch in range(2):
+            e.init_records(avhip.INIT_BERNOULLI, P80)
+            if not opt:
+                e.set_option("fresh", 0)
+            e.run_rounds(20)
+        out.append((e.read_records(), e.fetch_updates(), e.applied_votes(), e.finalized_count(), e.alg_bytes()))
+        e.close()
+    off, on = out
+    for a, b in zip(off[:4], on[:4]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    assert on[4] < off[4]

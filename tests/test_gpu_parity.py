@@ -338,22 +338,25 @@ def test_c4_shape_properties():
     results; the published preference equals the records' accepted bit."""
     n, m, k = 100_000, 1000, 8
     digests = []
-    # warm bytes per lane over rounds 1-15: kernel 1 176 each; the sweep 172 - 32
-    # (round 1: vote planes left unstored) then 172 - 36 (regathered, not read)
-    for kernel, warm_bytes in ((1, 15 * 176), (2, 140 + 14 * 136)):
+    # round 0: kernel 1 reads and writes all 25 planes (236 B per 32-record
+    # lane); the sweep's fresh round reads only A and leaves the vote planes
+    # virtual (236 - 96 - 32 = 108 B). Warm bytes per lane over rounds 1-15:
+    # kernel 1 176 each; the sweep 172 - 36 (vote planes regathered, not read
+    # or written)
+    for kernel, cold_bytes, warm_bytes in ((1, 236, 15 * 176), (2, 108, 15 * 136)):
         e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4)
         e.set_option("kernel", kernel)
         e.set_option("count_lazy", 0)  # per-lane bytes with stored count planes (test_gpu_count_lazy.py)
         e.init_records(avhip.INIT_BERNOULLI, P80)
         lanes = e.layout_info()["lanes"]
-        e.run_rounds(1)  # round 0: consider planes fill up (236 B per 32-record lane)
+        e.run_rounds(1)  # round 0: consider planes fill up
         b1 = e.alg_bytes()
         e.run_rounds(15)  # warm: the all-ones consider planes are skipped
         b16 = e.alg_bytes()
         assert e.applied_votes() == n * m * k * 16
         u = e.fetch_updates()
         r0 = u[:, 0] == 0
-        assert b1 == lanes * 236 + emitted_bytes(u[r0])
+        assert b1 == lanes * cold_bytes + emitted_bytes(u[r0])
         assert b16 - b1 == lanes * warm_bytes + emitted_bytes(u[~r0])
         assert not np.isin(u[:, 4], [avhip.STATUS_FINALIZED, avhip.STATUS_INVALID]).any()
         recs = e.read_records(0, n, 0, m)

@@ -99,7 +99,7 @@ def test_virtual_votes_bytes():
     e.set_option("count_lazy", 0)  # count planes stored every round (test_gpu_count_lazy.py)
     e.init_records(avhip.INIT_ACCEPTED, 0)
     lanes = e.layout_info()["lanes"]
-    e.run_rounds(2)  # round 0 cold; round 1 warm, vv on, nothing stale yet
+    e.run_rounds(2)  # round 0 fresh (V left virtual); round 1 warm and stale
     b = e.alg_bytes()
     e.run_rounds(1)
     assert e.alg_bytes() - b == lanes * 136 + 0  # no updates: all accepted from the start, no flips

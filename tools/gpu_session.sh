@@ -42,6 +42,13 @@ for s in "$@"; do
     rehearse4p) step rehearse4p 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
             --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --rehearse-one-gpu --no-secondary --shard peers ;;
     capped) step capped 600 python -u -m pytest tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "capped or c2 or replay or fuzz or poll_sets" ;;
+    fresh) step fresh 600 python -u -m pytest tests/test_gpu_fresh.py tests/test_gpu_count_lazy.py tests/test_gpu_virtual_votes.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    probe_c4) step probe_c4 300 python tools/round_probe.py --workload c4 --json $OUT/probe_c4.json ;;
+    probe_c3) step probe_c3 300 python tools/round_probe.py --workload c3 --json $OUT/probe_c3.json ;;
+    sq_c4a) step sq_c4a 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/sq_c4a -o probe -- \
+            python3 tools/round_probe.py --workload c4 --warm-epochs 0 ;;
+    sq_c4b) step sq_c4b 300 timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq_c4b -o probe -- \
+            python3 tools/round_probe.py --workload c4 --warm-epochs 0 ;;
     peertests) step peertests 600 python -u -m pytest tests/test_gpu_peer_push.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     nsprobe) step nsprobe 600 python tools/node_shard_probe.py --json $OUT/node_shard_probe.json ;;
     ab) step ab 900 python tools/ab_tune.py --json $OUT/ab.json ;;
