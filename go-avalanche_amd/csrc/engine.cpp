@@ -109,6 +109,10 @@ struct av_engine {
   // 1 = k_round_fast / k_round_capped (the first versions; any k, A/B baseline)
   int kernel = 2;
   uint32_t sweep_blocks = 0;  // resident workgroups of the sweep grid (option "sweep_blocks"; 0 = one wave per tile)
+  // option "sweep_nopipe": a walking grid runs without next-tile prefetch
+  // (kModeWarm; default); 0 = the prefetching kModeWarmPipe (A/B)
+  bool sweep_nopipe = true;
+  uint32_t tiles_per_wave = 4;  // option "tiles_per_wave" (default grid, default_sweep_blocks)
   // every consider plane of every lane is all-ones: set after a sim round with k >= 8 in which every
   // live record was polled (all targets valid, uncapped); cleared by anything that can write a 0
   // consider bit (init, add, write_records, drop-in votes, replay)
@@ -247,6 +251,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.kconsume = 0u;
   p.fresh = 0u;
   p.tn = (uint32_t)(e->t1 - e->t0);
+  p.nopipe = e->sweep_nopipe ? 1u : 0u;
   return p;
 }
 
@@ -441,19 +446,24 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   return AV_OK;
 }
 
-// Sweep grid (0 = one wave per tile). Measured on MI355X (tools/ab_tune.py):
-// one wave per tile is fastest for large tile counts (C4 on 1-4 GPUs: the
-// dispatcher keeps the active tiles in a narrow, DRAM-friendly window); a
-// resident grid that walks the tiles wins slightly once there are only a few
-// tiles per resident wave (C4 8-way target shard: 62.5k tiles, ~12 per wave),
-// where the warm sweep also pipelines each wave's next tile. force: always the
-// resident grid (A/B).
+// Sweep grid (0 = one wave per tile). Each wave walks `tiles_per_wave`
+// tiles (grid stride, no next-tile prefetch): the wave's prologue — kernel
+// parameters, the loop-invariant Philox key schedule and the SGPR spills the
+// compiler parks in VGPR lanes, ~150 SALU and ~100 VALU instructions — is then
+// paid once per 4 tiles instead of per tile. Measured on MI355X
+// (tools/round_probe.py, C4 epoch): one wave per tile 9.37 ms, 4 tiles per
+// wave 8.37 ms, 17 per wave 8.39 ms; the prefetching resident grid
+// (kModeWarmPipe, 5 waves per SIMD) 9.5-10.2 ms. force: the resident grid (A/B).
 uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
   if (e->k > 8 || e->capped) return 0;
-  int bpc = 0, cus = 0;
-  if (avk::round_sweep_occupancy(e->k, false, &bpc, &cus) != hipSuccess || bpc <= 0 || cus <= 0) return 0;
-  const uint64_t resident_waves = (uint64_t)bpc * cus * 4;
-  return force || (uint64_t)(e->Lpad / 64) <= 16 * resident_waves ? (uint32_t)(bpc * cus) : 0u;
+  const uint64_t tiles = e->Lpad / 64;
+  if (force) {
+    int bpc = 0, cus = 0;
+    if (avk::round_sweep_occupancy(e->k, false, &bpc, &cus) != hipSuccess || bpc <= 0 || cus <= 0) return 0;
+    return (uint32_t)(bpc * cus);
+  }
+  const uint64_t waves = (tiles + e->tiles_per_wave - 1) / e->tiles_per_wave;
+  return (uint32_t)std::max<uint64_t>(1, (waves + 3) / 4);
 }
 
 int refresh_pref(av_engine* e) {
@@ -1362,6 +1372,12 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     } else {
       e->sweep_blocks = (uint32_t)value;
     }
+  } else if (n == "sweep_nopipe") {
+    e->sweep_nopipe = value != 0;
+  } else if (n == "tiles_per_wave") {
+    AV_CHECK(value >= 1 && value <= 4096, AV_ERR_INVALID_ARG, "bad tiles_per_wave");
+    e->tiles_per_wave = (uint32_t)value;
+    e->sweep_blocks = default_sweep_blocks(e);
   } else if (n == "unsynced_shard") {
     e->unsynced_shard = value != 0;
   } else if (n == "round_marker") {

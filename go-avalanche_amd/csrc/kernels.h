@@ -75,7 +75,11 @@ struct RoundParams {
   // gathered words, so a tile may skip storing its V planes and the next
   // round regathers them from the previous snapshot instead of reading them.
   uint32_t vv;               // this round may leave V planes unstored (vstale)
-  uint32_t* vstale;          // [tiles] 1: the tile's V planes are stale; V = votes of round - 1
+  // [tiles] kVStale: the tile's V planes are stale, V = votes of round - 1
+  // (regathered with round - 1's peers); kVUniform: the tile was settled (all
+  // 8 votes of round - 1 equal the accepted bit of every polled record), so V
+  // = A on the polled records and nothing needs gathering; 0: V stored
+  uint32_t* vstale;
   const uint32_t* pref_prev; // [N_pad][BL] snapshot of round - 1 (read by stale tiles)
   // Peer-push exchange (node-sharded engines, k_round_sweep only):
   // every replica of a snapshot buffer is identical between rounds, so the
@@ -106,8 +110,10 @@ struct RoundParams {
   // targets (tn = targets in this engine's range).
   uint32_t fresh;
   uint32_t tn;
+  uint32_t nopipe;  // tuning: a grid smaller than the tile count runs kModeWarm (no next-tile prefetch)
 };
 constexpr uint32_t kPendAllLive = 0x80000000u;
+constexpr uint32_t kVStale = 1u, kVUniform = 2u;
 
 // Division by the (runtime) block count BL without a hardware divide:
 // Granlund-Montgomery round-up magic, exact for every 32-bit n.

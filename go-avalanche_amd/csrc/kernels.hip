@@ -438,11 +438,15 @@ __global__ __launch_bounds__(256) void k_read_records_v(const RoundParams p, uin
   const uint32_t g = nl * p.BL + b, tile = g >> 6;
   St s;
   load_state(p.planes, g, s);
-  if (p.vv && p.vstale[tile]) {  // V_i = the vote of round - 1's slot 7 - i (k = 8)
+  const uint32_t st = p.vv ? p.vstale[tile] : 0u;
+  if (st == kVStale) {  // V_i = the vote of round - 1's slot 7 - i (k = 8)
     uint32_t pp[8];
     sample_peers<8>(p.seed, p.n0 + nl, p.round - 1u, p.n_nodes, p.peer_mode, pp);
 #pragma unroll
     for (int q = 0; q < 8; ++q) s.V[q] = p.pref_prev[pp[7 - q] * p.BL + b];
+  } else if (st == kVUniform) {  // every polled record's vote register = its accepted bit
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s.V[q] = s.A;
   }
   if (p.klazy) {
     const uint32_t pend = p.kpend[tile] & 0xFFu;

@@ -117,6 +117,10 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
     }
   }
   in.A = ld1<POL>(tp + 1536u + lane);
+  if (in.stale == kVUniform) {  // the vote register of every polled record = its accepted bit (kernels.h)
+    in.v0 = u32x4{in.A, in.A, in.A, in.A};
+    in.v1 = u32x4{in.A, in.A, in.A, in.A};
+  }
   in.vmask = x.active ? p.valid[x.b] : 0u;
   in.byzw = p.byz[x.node >> 5];
   if constexpr (REPLAY) {
@@ -130,7 +134,7 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
     uint32_t peers[K];
     bool drawn = false;
     if constexpr (VV) {
-      if (in.stale) {
+      if (in.stale == kVStale) {
         // the vote register after last round's 8 sim votes is those votes:
         // V_i = (previous round's slot 7 - i vote); V_7 is never read at k = 8
         const PairDraw pd = pair_draw(p, p.round, nlA, nn, lane);
@@ -362,7 +366,10 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     // k_add_targets resets all planes) and the next round's store zeroes them
   }
   if constexpr (VVM && !REPLAY && K == 8) {
-    if (p.vv && lane == 0 && virt != (in.stale != 0u)) p.vstale[tile] = virt ? 1u : 0u;
+    // a settled tile's 8 new votes all equal its accepted plane on the polled
+    // records: its vote register is A next round (no regather)
+    const uint32_t nv = virt ? (settled ? kVUniform : kVStale) : 0u;
+    if (p.vv && lane == 0 && nv != in.stale) p.vstale[tile] = nv;
   }
   if constexpr (KL) {
     if (klazy) {
@@ -388,7 +395,9 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   // push: + the 4-B read of the word being overwritten
   // kl: K planes neither read (kunread and deferred) nor written (deferred); A not rewritten
   const uint32_t kbytes = (kunread && kdefer ? 32u : 0u) + (kdefer ? 32u : 0u);
-  acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale ? 4u : 0u) - (virt ? 32u : 0u) + (p.push_n ? 4u : 0u) -
+  // V read: 32 B stored, 28 B regathered (stale), 0 B uniform
+  acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale == kVStale ? 4u : in.stale == kVUniform ? 32u : 0u) -
+                                 (virt ? 32u : 0u) + (p.push_n ? 4u : 0u) -
                                  kbytes - (astore ? 0u : 4u)
                            : 0u;
   acc.emitted_bytes += emitted;
@@ -495,7 +504,8 @@ hipError_t launch_sweep_k(const RoundParams& p, bool replay, uint32_t blocks, hi
   if (p.ablate_gather) return launch_mode<K, kModeAblate>(p, grid, s);
   if (p.fresh) return launch_mode<K, kModeFresh>(p, grid, s);
   if (p.warm_skip && p.warm_all)  // a resident grid walks several tiles per wave: pipeline them
-    return blocks && grid < need ? launch_mode<K, kModeWarmPipe>(p, grid, s) : launch_mode<K, kModeWarm>(p, grid, s);
+    return blocks && grid < need && !p.nopipe ? launch_mode<K, kModeWarmPipe>(p, grid, s)
+                                              : launch_mode<K, kModeWarm>(p, grid, s);
   return launch_mode<K, kModeCheck>(p, grid, s);
 }
 
@@ -505,16 +515,22 @@ hipError_t launch_sweep_k(const RoundParams& p, bool replay, uint32_t blocks, hi
 __global__ __launch_bounds__(256) void k_vv_materialize(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t tile = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
-  if (tile >= (p.Lpad >> 6) || uni(p.vstale[tile]) == 0u) return;
+  const uint32_t st = tile < (p.Lpad >> 6) ? uni(p.vstale[tile]) : 0u;
+  if (st == 0u) return;
   const LaneIdx x = lane_idx(p, tile, lane);
-  const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
-  uint32_t pp[8];
-  draw_peers<8>(p, p.round - 1u, x.node, x.nl, nlA, nn, lane, pp);
   u32x4 o0, o1;
+  if (st == kVUniform) {  // V_i = A on every polled record
+    const uint32_t A = p.planes[(size_t)tile * (kPlanes * 64u) + 1536u + lane];
+    o0 = o1 = u32x4{A, A, A, A};
+  } else {
+    const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
+    uint32_t pp[8];
+    draw_peers<8>(p, p.round - 1u, x.node, x.nl, nlA, nn, lane, pp);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    o0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
-    o1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
+    for (int i = 0; i < 4; ++i) {
+      o0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
+      o1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
+    }
   }
   if (x.active) {
     u32x4* const grp = reinterpret_cast<u32x4*>(p.planes + (size_t)tile * (kPlanes * 64u)) + lane;

@@ -341,9 +341,9 @@ def test_c4_shape_properties():
     # round 0: kernel 1 reads and writes all 25 planes (236 B per 32-record
     # lane); the sweep's fresh round reads only A and leaves the vote planes
     # virtual (236 - 96 - 32 = 108 B). Warm bytes per lane over rounds 1-15:
-    # kernel 1 176 each; the sweep 172 - 36 (vote planes regathered, not read
-    # or written)
-    for kernel, cold_bytes, warm_bytes in ((1, 236, 15 * 176), (2, 108, 15 * 136)):
+    # kernel 1 176 each; the sweep's depend on which tiles settled
+    # (test_gpu_virtual_votes.py, test_gpu_count_lazy.py check them exactly)
+    for kernel, cold_bytes, warm_bytes in ((1, 236, 15 * 176), (2, 108, None)):
         e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4)
         e.set_option("kernel", kernel)
         e.set_option("count_lazy", 0)  # per-lane bytes with stored count planes (test_gpu_count_lazy.py)
@@ -357,7 +357,10 @@ def test_c4_shape_properties():
         u = e.fetch_updates()
         r0 = u[:, 0] == 0
         assert b1 == lanes * cold_bytes + emitted_bytes(u[r0])
-        assert b16 - b1 == lanes * warm_bytes + emitted_bytes(u[~r0])
+        if warm_bytes is not None:
+            assert b16 - b1 == lanes * warm_bytes + emitted_bytes(u[~r0])
+        else:
+            assert lanes * 108 <= b16 - b1 - emitted_bytes(u[~r0]) <= lanes * 15 * 136
         assert not np.isin(u[:, 4], [avhip.STATUS_FINALIZED, avhip.STATUS_INVALID]).any()
         recs = e.read_records(0, n, 0, m)
         assert ((recs >> 17) < 128).all()

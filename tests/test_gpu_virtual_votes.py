@@ -93,7 +93,8 @@ def test_virtual_votes_on_off_identical():
 def test_virtual_votes_bytes():
     """Per-lane bytes of a warm k=8 sim round: 172 B with stored vote planes;
     140 B in the first round that leaves them unstored (no V write); 136 B
-    once the tile is stale (7 regathered words instead of the 8 V planes)."""
+    once the tile is stale (7 regathered words instead of the 8 V planes);
+    108 B once the tile was settled (the vote register is the A plane)."""
     n, m = 4000, 1000
     e = avhip.Engine(n, m, k=8, seed=1, log_capacity=1 << 22)
     e.set_option("count_lazy", 0)  # count planes stored every round (test_gpu_count_lazy.py)
@@ -102,5 +103,5 @@ def test_virtual_votes_bytes():
     e.run_rounds(2)  # round 0 fresh (V left virtual); round 1 warm and stale
     b = e.alg_bytes()
     e.run_rounds(1)
-    assert e.alg_bytes() - b == lanes * 136 + 0  # no updates: all accepted from the start, no flips
+    assert e.alg_bytes() - b == lanes * 108 + 0  # round 1 settled: uniform; no updates, no flips
     e.close()

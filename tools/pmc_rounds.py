@@ -11,6 +11,7 @@ import csv
 import glob
 import json
 import os
+import re
 
 
 def load(d):
@@ -21,7 +22,8 @@ def load(d):
             name = r["Kernel_Name"]
             if "k_round_sweep" not in name and "k_round_node" not in name and "materialize" not in name:
                 continue
-            key = (int(r["Dispatch_Id"]), name.split("(")[0].split("::")[-1])
+            mk = re.search(r"(k_\w+)(<[^>]*>)?", name)
+            key = (int(r["Dispatch_Id"]), mk.group(0) if mk else name)
             per.setdefault(key, {})[r["Counter_Name"]] = float(r["Counter_Value"])
     return per
 
