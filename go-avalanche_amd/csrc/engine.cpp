@@ -158,6 +158,14 @@ struct av_engine {
   avk::PeerPtrs peer_arrive{};
   uint32_t** push_tbl = nullptr;                     // device [3][kMaxPeers]: peers' replicas of each buffer
 
+  // responder variant (option "responder", kernels.h pub_mode) and the nodes
+  // that no longer poll (av_set_polling); both run the first-generation kernel
+  int32_t pub_mode = 0;
+  uint32_t* readd = nullptr;     // [L] pub_mode 2: re-add marks
+  uint32_t* died_out = nullptr;  // [L] pub_mode 2: records deleted this round
+  std::vector<uint32_t> nopoll_host;
+  uint32_t* nopoll = nullptr;    // [ceil(NL/32)]
+  bool any_nopoll = false;
   // per-local-node Processor.round (processor.go:15,40-42): a field only the
   // caller changes (avalanche_test.go:302); allocated on the first set
   std::vector<int64_t> proc_round;
@@ -252,6 +260,10 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.fresh = 0u;
   p.tn = (uint32_t)(e->t1 - e->t0);
   p.nopipe = e->sweep_nopipe ? 1u : 0u;
+  p.pub_mode = (uint32_t)e->pub_mode;
+  p.readd = e->pub_mode == 2 ? e->readd : nullptr;
+  p.died_out = e->pub_mode == 2 ? e->died_out : nullptr;
+  p.nopoll = e->any_nopoll ? e->nopoll : nullptr;
   return p;
 }
 
@@ -358,7 +370,11 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
            AV_ERR_UNSUPPORTED,
            "node-sharded engine needs av_comm_init before running rounds");
   avk::RoundParams p = round_params(e, replay);
-  const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped;
+  // responder variants and non-polling nodes run the first-generation kernels
+  const bool compat = e->pub_mode != 0 || e->any_nopoll;
+  AV_CHECK(!(compat && e->capped && (e->pub_mode == 2 || e->any_nopoll)), AV_ERR_UNSUPPORTED,
+           "the example responder and av_set_polling need M <= 4096 (uncapped)");
+  const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped && !compat;
   // the round after av_init_records: planes known to be zero are not read
   const bool fresh = e->fresh && sweep && !replay && !e->ablate_gather;
   // the sweep's warm sim modes (launch_sweep_k): every consider plane all-ones
@@ -408,12 +424,17 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   }
   if (sweep)
     AV_HIP(avk::launch_round_sweep(p, e->k, replay != nullptr, e->sweep_blocks, e->stream));
-  else if (e->kernel == 2 && e->k <= 8 && e->capped) {
+  else if (e->kernel == 2 && e->k <= 8 && e->capped && !compat) {
     p.node_flags = e->node_flags;
     AV_HIP(avk::launch_round_node(p, e->k, replay != nullptr, /*exact_pass=*/e->count_bound >= 120, e->stream));
   }
   else
     AV_HIP(avk::launch_round(p, e->k, replay != nullptr, e->capped, e->stream));
+  if (e->pub_mode == 2) {  // the responders' re-adds (main.go:175-177)
+    AV_HIP(avk::launch_readd(p, e->stream));
+    e->warm_all = false;
+    e->count_bound = 127;
+  }
   e->count_bound = std::min(127, e->count_bound + e->k);
   e->fresh = false;
   if (replay)
@@ -467,8 +488,8 @@ uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
 }
 
 int refresh_pref(av_engine* e) {
-  AV_HIP(avk::launch_refresh_pref(e->planes, e->pref[e->cur], e->byz, (uint32_t)e->n0, e->NL, e->BL,
-                                  (uint32_t)e->round, e->stream));
+  AV_HIP(avk::launch_refresh_pref((uint32_t)e->pub_mode, e->planes, e->pref[e->cur], e->byz, (uint32_t)e->n0, e->NL,
+                                  e->BL, (uint32_t)e->round, e->stream));
   return AV_OK;
 }
 
@@ -519,6 +540,7 @@ int av_destroy(av_engine* e) {
   if (e->push_tbl) (void)hipFree(e->push_tbl);
   if (e->marker) (void)hipEventDestroy(e->marker);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->kpend, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
+                  e->readd, e->died_out, e->nopoll,
                   e->dlog, e->dlog_count, e->upd_count,
                   e->applied, e->bytes, e->finalized, e->scratch_count, e->replay};
   for (void* b : bufs)
@@ -679,6 +701,7 @@ int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
   p.n_targets = (uint32_t)e->t1;  // targets >= t1 belong to another shard (or do not exist)
   p.round = (uint32_t)e->round;
   p.mode = init_mode;
+  p.pub_mode = (uint32_t)e->pub_mode;
   p.param = init_param;
   AV_HIP(avk::launch_init(p, e->stream));
   e->fresh = init_mode != AV_INIT_NONE;
@@ -751,6 +774,7 @@ int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uin
   p.node = (uint32_t)node;
   p.BL = e->BL;
   p.round = (uint32_t)e->round;
+  p.pub_mode = (uint32_t)e->pub_mode;
   AV_HIP(avk::launch_add_targets(p, e->stream));
   std::vector<uint8_t> res(m);
   AV_HIP(hipMemcpyAsync(res.data(), dadd, m, hipMemcpyDeviceToHost, e->stream));
@@ -834,6 +858,7 @@ int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const 
   p.node = (uint32_t)node;
   p.BL = e->BL;
   p.round = (uint32_t)e->round;
+  p.pub_mode = (uint32_t)e->pub_mode;
   AV_HIP(avk::launch_register_votes(p, e->stream));
   AV_HIP(hipMemcpyAsync(status_out, dstat, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
@@ -1073,6 +1098,27 @@ int av_set_round(av_engine* e, int64_t node, int64_t round) {
   AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
   if (e->proc_round.empty()) e->proc_round.assign(e->NL, 0);
   e->proc_round[(size_t)(node - e->n0)] = round;
+  return AV_OK;
+}
+
+int av_set_polling(av_engine* e, int64_t node, int32_t polls) {
+  AV_ENTER(e);
+  AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
+  AV_CHECK(e->peer_world <= 1, AV_ERR_UNSUPPORTED, "av_set_polling on a peer-push engine");
+  if (e->nopoll_host.empty()) {
+    e->nopoll_host.assign((e->NL + 31) / 32, 0u);
+    AV_HIP(dev_alloc(&e->nopoll, e->nopoll_host.size()));
+  }
+  const uint32_t nl = (uint32_t)(node - e->n0);
+  uint32_t& w = e->nopoll_host[nl >> 5];
+  w = polls ? (w & ~(1u << (nl & 31))) : (w | (1u << (nl & 31)));
+  int rc = materialize_votes(e);  // rounds of non-polling networks run the first-generation kernel
+  if (rc != AV_OK) return rc;
+  AV_HIP(hipMemcpyAsync(e->nopoll, e->nopoll_host.data(), e->nopoll_host.size() * 4, hipMemcpyHostToDevice,
+                        e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  e->any_nopoll = false;
+  for (uint32_t v : e->nopoll_host) e->any_nopoll |= v != 0;
   return AV_OK;
 }
 
@@ -1392,6 +1438,24 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   } else if (n == "vv_min_bl") {
     AV_CHECK(value >= 1 && value < (1ll << 31), AV_ERR_INVALID_ARG, "bad vv_min_bl");
     e->vv_min_bl = (uint32_t)value;
+  } else if (n == "responder") {  // 0 = R2 decision, 1 = IsAccepted literally, 2 = the example's responder
+    AV_ENTER(e);
+    AV_CHECK(value >= 0 && value <= 2, AV_ERR_INVALID_ARG, "responder must be 0, 1 or 2");
+    AV_CHECK(value != 2 || (e->NL == (uint32_t)e->N && e->t0 == 0 && e->t1 == e->M && e->peer_world <= 1 && !e->comm),
+             AV_ERR_UNSUPPORTED, "the example responder (re-adds) needs an unsharded engine");
+    AV_CHECK(value == 0 || e->peer_world <= 1, AV_ERR_UNSUPPORTED, "responder variants on a peer-push engine");
+    if (value == 2 && !e->readd) {
+      AV_HIP(dev_alloc(&e->readd, e->L));
+      AV_HIP(dev_alloc(&e->died_out, e->L));
+      AV_HIP(hipMemsetAsync(e->readd, 0, (size_t)e->L * 4, e->stream));
+      AV_HIP(hipMemsetAsync(e->died_out, 0, (size_t)e->L * 4, e->stream));
+    }
+    int rc = materialize_votes(e);
+    if (rc != AV_OK) return rc;
+    e->pub_mode = (int32_t)value;
+    rc = refresh_pref(e);  // republish the current snapshot under the new rule
+    if (rc != AV_OK) return rc;
+    AV_HIP(hipStreamSynchronize(e->stream));
   } else if (n == "fresh") {  // 0: a round after init reads every plane (A/B only)
     if (!value) e->fresh = false;
   } else if (n == "peer_fine") {  // before av_peer_handles: fine-grained snapshot buffers (default 1)

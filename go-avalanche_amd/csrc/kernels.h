@@ -111,6 +111,16 @@ struct RoundParams {
   uint32_t fresh;
   uint32_t tn;
   uint32_t nopipe;  // tuning: a grid smaller than the tile count runs kModeWarm (no next-tile prefetch)
+  // Responder variants (engine option "responder", first-generation kernel
+  // only; see publish_word): pub_mode 0 = R2 decision, 1 = IsAccepted
+  // literally, 2 = the example's responder, whose re-adds of queried targets
+  // are marked in readd[g] (OR of the polled masks per peer lane) and applied
+  // by k_readd after the round (died_out[g]: records deleted this round).
+  // nopoll: [ceil(NL/32)] local nodes that do not poll (their loop returned).
+  uint32_t pub_mode;
+  uint32_t* readd;
+  uint32_t* died_out;
+  const uint32_t* nopoll;
 };
 constexpr uint32_t kPendAllLive = 0x80000000u;
 constexpr uint32_t kVStale = 1u, kVUniform = 2u;
@@ -182,6 +192,7 @@ struct InitParams {
   uint32_t n_nodes, n0, NL, BL, L, Lpad, t0, n_targets, round;
   int32_t mode;
   uint32_t param;
+  uint32_t pub_mode;    // RoundParams::pub_mode
 };
 hipError_t launch_init(const InitParams& p, hipStream_t s);
 hipError_t launch_byz(uint32_t* byz, uint32_t n_nodes, uint64_t seed, uint32_t threshold, hipStream_t s);
@@ -196,6 +207,7 @@ struct DropInParams {
   const uint32_t* entries; // pairs (pos, meta = bit | yes<<5 | considered<<6)
   int32_t* status_out;     // per vote position, -1 = no update
   uint32_t n_blocks, node_local, node, BL, round;
+  uint32_t pub_mode;
 };
 hipError_t launch_register_votes(const DropInParams& p, hipStream_t s);
 
@@ -208,6 +220,7 @@ struct AddParams {
   const uint8_t* accepted;
   uint8_t* added;
   uint32_t n, node_local, node, BL, round;
+  uint32_t pub_mode;
 };
 hipError_t launch_add_targets(const AddParams& p, hipStream_t s);
 
@@ -236,8 +249,11 @@ hipError_t launch_sort_updates(void* temp, size_t* temp_bytes, const uint64_t* i
 
 hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0,
                                 uint32_t tl1, const uint32_t* in, hipStream_t s);
-hipError_t launch_refresh_pref(const uint32_t* planes, uint32_t* pref, const uint32_t* byz, uint32_t n0,
-                               uint32_t NL, uint32_t BL, uint32_t round, hipStream_t s);
+// After a round with the example's responder (pub_mode 2): re-create the
+// records queried this round that their responder did not hold.
+hipError_t launch_readd(const RoundParams& p, hipStream_t s);
+hipError_t launch_refresh_pref(uint32_t pub_mode, const uint32_t* planes, uint32_t* pref, const uint32_t* byz,
+                               uint32_t n0, uint32_t NL, uint32_t BL, uint32_t round, hipStream_t s);
 hipError_t launch_sample_peers(uint64_t seed, uint32_t n_nodes, uint32_t a, uint32_t b, uint32_t round,
                                int k, int mode, uint32_t* out, hipStream_t s);
 hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t BL, uint32_t L, uint32_t Lpad,

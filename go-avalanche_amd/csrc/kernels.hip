@@ -50,7 +50,7 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
     s.A = pld<NT>(tile + plane_off(kPA, lane));
   }
 
-  uint32_t w[K], cw[K];
+  uint32_t w[K], cw[K], peer_of[K];
   if (REPLAY) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -67,22 +67,29 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
       const uint32_t src = p.ablate_gather ? (node ^ (uint32_t)j) % p.n_nodes : peers[j];
       w[j] = active ? p.pref_in[(size_t)src * p.BL + b] : 0u;
       cw[j] = ~0u;  // honest/Byzantine votes are 0 or 1
+      peer_of[j] = src - p.n0;  // local row of the peer (responder re-adds: single-engine networks only)
     }
   }
   const uint32_t vmask = active ? p.valid[b] : 0u;
   const uint32_t live0 = ~s.K[7];
-  const uint32_t P0 = live0 & vmask;
+  // a node whose run loop has returned (main.go:160-162) polls nothing
+  const uint32_t nl = g / p.BL;
+  const bool polls = !p.nopoll || !((p.nopoll[nl >> 5] >> (nl & 31u)) & 1u);
+  const uint32_t P0 = polls ? live0 & vmask : 0u;
 
   uint32_t alive = P0, applied = 0, E[K];
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     applied += __popc(alive);
+    // the example's responder re-adds what it is queried for (main.go:175-177)
+    if (!REPLAY && p.readd && alive) atomicOr(&p.readd[peer_of[j] * p.BL + b], alive);
     uint32_t fin;
     vote_step<false>(s, w[j], cw[j], alive, E[j], fin);
     alive &= ~fin;
   }
   const uint32_t died = P0 & ~alive;
-  const uint32_t keep = live0 & ~vmask;  // live but !IsValid(): skipped (processor.go:101-103)
+  const uint32_t keep = live0 & ~P0;  // live but !IsValid() (processor.go:101-103) or not polling: untouched
+  if (p.died_out && active) p.died_out[g] = died;
 
   if (active) {
     uint32_t Vo[8], Co[8];
@@ -113,7 +120,8 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
       for (int i = 0; i < 8; ++i) pst<NT>(tile + plane_off(kPC + i, lane), (s.C[i] & alive) | (Co[i] & keep) | dead);
     }
     pst<NT>(tile + plane_off(kPA, lane), s.A);
-    p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
+    p.pref_out[(size_t)node * p.BL + b] =
+        is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : publish_word(s.A, s.K[7], p.pub_mode);
   }
   const uint32_t wave_id = g >> 6;
   uint32_t upd = 0;
@@ -249,7 +257,8 @@ __device__ __forceinline__ void capped_node(const RoundParams& p, uint32_t nl, u
       s.C[i] |= died;
     }
     store_state(p.planes, g, s);
-    p.pref_out[(size_t)node * p.BL + b] = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : s.A;
+    p.pref_out[(size_t)node * p.BL + b] =
+        is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : publish_word(s.A, s.K[7], p.pub_mode);
   }
   const uint32_t wave_id = nl * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
   uint32_t upd = 0;
@@ -290,7 +299,8 @@ __global__ void k_register_votes(const DropInParams p) {
     s.C[q] |= died;
   }
   store_state(p.planes, g, s);
-  p.pref[(size_t)p.node * p.BL + b] = is_byz(p.byz, p.node) ? byz_pattern(p.round) : s.A;
+  p.pref[(size_t)p.node * p.BL + b] =
+      is_byz(p.byz, p.node) ? byz_pattern(p.round) : publish_word(s.A, s.K[7], p.pub_mode);
 }
 
 // AddTargetToReconcile (processor.go:45-58) for a list of targets of one
@@ -315,7 +325,8 @@ __global__ void k_add_targets(const AddParams p) {
     uint32_t* a = pw(p.planes, g, kPA);
     *a = p.accepted[i] ? (*a | m) : (*a & ~m);
     p.added[i] = 1;
-    p.pref[(size_t)p.node * p.BL + b] = is_byz(p.byz, p.node) ? byz_pattern(p.round) : *a;
+    p.pref[(size_t)p.node * p.BL + b] = is_byz(p.byz, p.node) ? byz_pattern(p.round)
+                                                               : publish_word(*a, *pw(p.planes, g, kPK + 7), p.pub_mode);
   }
 }
 
@@ -381,7 +392,8 @@ __global__ void k_init_pref(const InitParams p) {
   if (is_byz(p.byz, node))
     v = byz_pattern(p.round);
   else
-    v = p.mode == 0 ? 0u : (init_accept_block(p.seed, p.mode, p.param, node, tb) & target_mask(tb, p.n_targets));
+    v = p.mode == 0 ? (p.pub_mode == 2u ? target_mask(tb, p.n_targets) : 0u)  // no records (K7 set)
+                    : (init_accept_block(p.seed, p.mode, p.param, node, tb) & target_mask(tb, p.n_targets));
   p.pref[i] = v;
 }
 
@@ -515,12 +527,36 @@ __global__ void k_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uin
   store_state(planes, g, s);
 }
 
-__global__ void k_refresh_pref(const uint32_t* planes, uint32_t* pref, const uint32_t* byz, uint32_t n0, uint32_t NL,
-                               uint32_t BL, uint32_t round) {
+__global__ void k_refresh_pref(uint32_t pub_mode, const uint32_t* planes, uint32_t* pref, const uint32_t* byz,
+                               uint32_t n0, uint32_t NL, uint32_t BL, uint32_t round) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= NL * BL) return;
   const uint32_t nl = g / BL, b = g - nl * BL, node = n0 + nl;
-  pref[(size_t)node * BL + b] = is_byz(byz, node) ? byz_pattern(round) : *pw(planes, g, kPA);
+  pref[(size_t)node * BL + b] =
+      is_byz(byz, node) ? byz_pattern(round) : publish_word(*pw(planes, g, kPA), *pw(planes, g, kPK + 7), pub_mode);
+}
+
+// The example's responder (main.go:175-177), after a round: every record a
+// node was queried for (readd, OR of the querying lanes' polled masks) and
+// did not hold at the round start (no record now, not deleted this round) is
+// re-created as AddTargetToReconcile(&tx{isAccepted: true}) (processor.go:
+// 45-58, valid targets only): votes, consider and count zero, accepted.
+__global__ __launch_bounds__(256) void k_readd(const RoundParams p) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= p.L) return;
+  const uint32_t q = p.readd[g];
+  if (!q) return;
+  p.readd[g] = 0u;
+  const uint32_t b = g % p.BL;
+  const uint32_t m = q & *pw(p.planes, g, kPK + 7) & ~p.died_out[g] & p.valid[b];
+  if (!m) return;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    *pw(p.planes, g, kPV + i) &= ~m;
+    *pw(p.planes, g, kPC + i) &= ~m;
+    *pw(p.planes, g, kPK + i) &= ~m;
+  }
+  *pw(p.planes, g, kPA) |= m;
 }
 
 template <int K>
@@ -787,11 +823,18 @@ hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uin
   return hipGetLastError();
 }
 
-hipError_t launch_refresh_pref(const uint32_t* planes, uint32_t* pref, const uint32_t* byz, uint32_t n0, uint32_t NL,
-                               uint32_t BL, uint32_t round, hipStream_t s) {
+hipError_t launch_refresh_pref(uint32_t pub_mode, const uint32_t* planes, uint32_t* pref, const uint32_t* byz,
+                               uint32_t n0, uint32_t NL, uint32_t BL, uint32_t round, hipStream_t s) {
   const uint32_t n = NL * BL;
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_refresh_pref, dim3((n + 255) / 256), dim3(256), 0, s, planes, pref, byz, n0, NL, BL, round);
+  hipLaunchKernelGGL(k_refresh_pref, dim3((n + 255) / 256), dim3(256), 0, s, pub_mode, planes, pref, byz, n0, NL, BL,
+                     round);
+  return hipGetLastError();
+}
+
+hipError_t launch_readd(const RoundParams& p, hipStream_t s) {
+  if (!p.readd || !p.died_out || !p.L) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_readd, dim3((p.L + 255) / 256), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

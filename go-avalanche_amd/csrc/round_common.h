@@ -80,6 +80,15 @@ __device__ __forceinline__ uint32_t byz_pattern(uint32_t round) { return (round 
 
 __device__ __forceinline__ bool is_byz(const uint32_t* byz, uint32_t node) { return (byz[node >> 5] >> (node & 31u)) & 1u; }
 
+// The word a node publishes for 32 targets (what its responder answers,
+// main.go:168-192): live records their accepted bit; records it does not hold
+// (K7): mode 0 the finalized decision kept in A (harness rule R2), mode 1
+// false (IsAccepted literally, processor.go:125-130), mode 2 true (the
+// example's responder re-adds &tx{isAccepted: true} first, main.go:175-182).
+__device__ __forceinline__ uint32_t publish_word(uint32_t A, uint32_t K7, uint32_t mode) {
+  return mode == 0u ? A : mode == 1u ? (A & ~K7) : (A | K7);
+}
+
 struct St {
   uint32_t V[8], C[8], A, K[8];
 };

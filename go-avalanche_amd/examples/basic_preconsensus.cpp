@@ -4,9 +4,13 @@
 //
 // Each node polls one peer per round (k = 1, AV_PEERS_ROUND_ROBIN reproduces
 // the example's `i % N, skip self` peer sequence); the round is synchronous
-//  instead of goroutine-interleaved, and a finalized record
-// publishes its decision (R2) instead of being re-created by the responder
-// (main.go:177). Prints the example's log lines and final count.
+//  instead of goroutine-interleaved. By default a finalized
+// record publishes its decision (R2); -literal runs the example's own
+// semantics: the responder re-adds a queried target it does not hold as
+// accepted (main.go:175-177, engine option "responder" 2), and a node stops
+// polling once it counted txCount Finalized updates (main.go:143-162,
+// av_set_polling) while still answering. Prints the example's log lines and
+// final count.
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -33,9 +37,11 @@ struct Tx : Target {  // main.go:196-209
 
 int main(int argc, char** argv) {
   bool logging = false;  // main.go:24 -logging
+  bool literal = false;
   int64_t node_count = 100, tx_count = 100;  // main.go:13-16
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "-logging")) logging = true;
+    if (!std::strcmp(argv[i], "-literal")) literal = true;
     if (!std::strcmp(argv[i], "-nodes") && i + 1 < argc) node_count = std::atoll(argv[++i]);
     if (!std::strcmp(argv[i], "-txs") && i + 1 < argc) tx_count = std::atoll(argv[++i]);
   }
@@ -54,6 +60,10 @@ int main(int argc, char** argv) {
     for (auto& tx : txs) p.AddTargetToReconcile(*tx);
   }
 
+  if (literal && av_set_option(engine->handle(), "responder", 2) != AV_OK) {
+    std::fprintf(stderr, "responder option: %s\n", av_last_error());
+    return 2;
+  }
   std::vector<int64_t> finalized(node_count, 0);
   int64_t nodes_fully_finalized = 0, round = 0;
   while (nodes_fully_finalized < node_count && round < 100000) {
@@ -68,7 +78,10 @@ int main(int argc, char** argv) {
       if (logging)
         std::printf("%s tx %lld on node %lld after %lld queries\n", what, (long long)av_update_target(u),
                     (long long)node, (long long)round);
-      if (st == AV_STATUS_FINALIZED && ++finalized[node] == tx_count) ++nodes_fully_finalized;
+      if (st == AV_STATUS_FINALIZED && ++finalized[node] == tx_count) {
+        ++nodes_fully_finalized;  // main.go:159-162: the node's run loop returns
+        if (literal) av_set_polling(engine->handle(), node, 0);
+      }
     }
   }
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

@@ -81,7 +81,7 @@ EXPORTED = [
     "av_update_log_overflowed", "av_applied_votes", "av_alg_bytes", "av_finalized_count", "av_live_records", "av_discard_updates", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
     "av_peer_handles", "av_peer_init", "av_get_round", "av_set_round", "av_log_base_round", "av_updates_digest",
-    "av_updates_digest_range", "av_read_pref_words",
+    "av_updates_digest_range", "av_read_pref_words", "av_set_polling",
 ]
 
 _lib = None
@@ -144,6 +144,7 @@ def lib():
         "av_updates_digest": (i32, [_vp, _vp]),
         "av_updates_digest_range": (i32, [_vp, i64, i64, _vp]),
         "av_read_pref_words": (i32, [_vp, i64, i64, _vp]),
+        "av_set_polling": (i32, [_vp, i64, i32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -305,6 +306,10 @@ class Engine:
 
     def set_round(self, node, rnd):
         _check(lib().av_set_round(self._h, node, rnd))
+
+    def set_polling(self, node, polls):
+        """Whether `node` polls in the rounds (the example's loop returns, main.go:160-162)."""
+        _check(lib().av_set_polling(self._h, node, int(bool(polls))))
 
     @property
     def round(self):

@@ -162,6 +162,11 @@ int av_round_index(av_engine* e, int64_t* out);
  * that only its owner changes (the reference test sets it, avalanche_test.go:
  * 302); 0 until av_set_round. Not advanced by rounds. */
 int av_get_round(av_engine* e, int64_t node, int64_t* out);
+/* Whether `node` polls in the batched rounds (default 1). The example's run
+ * loop returns once the node counted every tx finalized (main.go:143-162);
+ * such a node still answers queries. Rounds with non-polling nodes run the
+ * first-generation kernel; not on peer-push engines. */
+int av_set_polling(av_engine* e, int64_t node, int32_t polls);
 int av_set_round(av_engine* e, int64_t node, int64_t round);
 
 /* ---- outputs ---- */
@@ -217,7 +222,16 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  * "store_policy"   : 2 = write-through (sc1) plane stores, 3 = nt sc1 (A/B).
  * "peer_fine" (0/1): snapshot buffers fine-grained once exported (default 1;
  *                    set before av_peer_handles).
- * "barrier_timeout_ms": peer barrier timeout (default 30000). */
+ * "barrier_timeout_ms": peer barrier timeout (default 30000).
+ * "responder" (0/1/2): what a node publishes for a target it no longer holds
+ *                    (what its responder answers, main.go:168-192): 0 = the
+ *                    finalized decision (harness rule R2, default); 1 =
+ *                    IsAccepted literally, false after deletion
+ *                    (processor.go:125-130); 2 = the example's responder,
+ *                    which re-adds a queried target it does not hold as
+ *                    accepted and answers yes (main.go:175-182; unsharded
+ *                    engines, M <= 4096). 1 and 2 run the first-generation
+ *                    kernel. */
 int av_set_option(av_engine* e, const char* name, int64_t value);
 
 /* ---- measurement ---- */

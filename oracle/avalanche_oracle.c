@@ -231,8 +231,17 @@ uint32_t avo_processor_dump_word(const avo_processor* p, int64_t t) {
   return AVO_ABSENT_WORD | ((uint32_t)p->decision[t] << 16);
 }
 
-static int published_pref(const avo_processor* p, int64_t t) {
+/* What a node answers for target t (the responder of main.go:168-192):
+ *   AVO_RESP_DECISION (harness rule R2): its record's accepted bit, or the
+ *     decision of a record it finalized and deleted;
+ *   AVO_RESP_IS_ACCEPTED: processor.go:125-130 literally: false once deleted;
+ *   AVO_RESP_EXAMPLE: the example's responder (main.go:175-182): it first
+ *     AddTargetToReconcile(&tx{isAccepted: true}), so an absent record comes
+ *     back accepted and the answer is yes. */
+static int published_pref_mode(const avo_processor* p, int64_t t, int32_t mode) {
   if (p->present[t]) return avo_is_accepted_rec(&p->rec[t]);
+  if (mode == AVO_RESP_IS_ACCEPTED) return 0;
+  if (mode == AVO_RESP_EXAMPLE) return 1;
   return p->decision[t];
 }
 
@@ -336,6 +345,8 @@ struct avo_sim {
   uint8_t* pref;  /* [N][M] round-start published preference snapshot */
   uint8_t* byz;   /* [N] */
   int literal;    /* 1: always the literal per-vote path (cross-checks the branch-free one) */
+  int32_t responder; /* AVO_RESP_* */
+  uint8_t* polls;    /* [N] the node polls in the rounds (the example's run loop stops, main.go:160-162) */
 };
 
 avo_sim* avo_sim_new(const avo_sim_config* cfg) { return avo_sim_new_threads(cfg, 1); }
@@ -349,6 +360,8 @@ avo_sim* avo_sim_new_threads(const avo_sim_config* cfg, int32_t threads) {
   memset(s->valid, 1, (size_t)m);
   s->pref = (uint8_t*)calloc((size_t)(n * m), 1);
   s->byz = (uint8_t*)calloc((size_t)n, 1);
+  s->polls = (uint8_t*)malloc((size_t)n);
+  memset(s->polls, 1, (size_t)n);
   int nt = threads > 0 ? threads : 1;
   (void)nt;
 #ifdef _OPENMP
@@ -375,6 +388,7 @@ void avo_sim_free(avo_sim* s) {
   free(s->valid);
   free(s->pref);
   free(s->byz);
+  free(s->polls);
   free(s);
 }
 
@@ -387,7 +401,7 @@ int avo_sim_is_byzantine(const avo_sim* s, int64_t node) { return s->byz[node]; 
 
 int avo_sim_add(avo_sim* s, int64_t node, int64_t t, int accepted) {
   int r = avo_processor_add(s->procs[node], t, accepted, s->valid[t]);
-  s->pref[node * s->cfg.n_targets + t] = (uint8_t)published_pref(s->procs[node], t);
+  s->pref[node * s->cfg.n_targets + t] = (uint8_t)published_pref_mode(s->procs[node], t, s->responder);
   return r;
 }
 
@@ -396,7 +410,7 @@ int avo_sim_register_votes(avo_sim* s, int64_t node, const int64_t* targets, con
   int r = avo_processor_register_votes(s->procs[node], targets, errs, n, s->valid, out_targets,
                                        out_status, n_out);
   for (int64_t t = 0; t < s->cfg.n_targets; ++t)
-    s->pref[node * s->cfg.n_targets + t] = (uint8_t)published_pref(s->procs[node], t);
+    s->pref[node * s->cfg.n_targets + t] = (uint8_t)published_pref_mode(s->procs[node], t, s->responder);
   return r;
 }
 
@@ -547,6 +561,15 @@ void avo_transition_batch_branchfree(const uint32_t* words_in, const uint32_t* e
 
 void avo_sim_set_literal(avo_sim* s, int literal) { s->literal = literal != 0; }
 
+void avo_sim_set_responder(avo_sim* s, int32_t mode) {
+  s->responder = mode;
+  const int64_t n = s->cfg.n_nodes, m = s->cfg.n_targets;
+  for (int64_t j = 0; j < n; ++j)
+    for (int64_t t = 0; t < m; ++t) s->pref[j * m + t] = (uint8_t)published_pref_mode(s->procs[j], t, mode);
+}
+
+void avo_sim_set_polling(avo_sim* s, int64_t node, int polls) { s->polls[node] = (uint8_t)(polls != 0); }
+
 /* One synchronous round (R1): every node draws k peers; for slot s it builds
  * the capped poll set (GetInvsForNextPoll, ascending index) and registers one
  * Response whose votes are the peer's round-start published preference
@@ -574,6 +597,16 @@ int avo_sim_round_ex(avo_sim* s, int64_t n0, int64_t n1, const uint32_t* replay_
   /* rows are kept per node (reference append order) only when the caller asks for them */
   upd_buf* bufs = updates ? (upd_buf*)calloc((size_t)(n1 - n0), sizeof(upd_buf)) : NULL;
   int64_t applied = 0, total = 0;
+  /* the example's responder re-creates every record it is queried for and
+   * does not hold (main.go:175-177): marked during the round against the
+   * round-start presence, applied after it */
+  uint8_t* pres0 = NULL;
+  uint8_t* readd = NULL;
+  if (s->responder == AVO_RESP_EXAMPLE) {
+    pres0 = (uint8_t*)malloc((size_t)(n_nodes * m));
+    readd = (uint8_t*)calloc((size_t)(n_nodes * m), 1);
+    for (int64_t j = 0; j < n_nodes; ++j) memcpy(pres0 + j * m, s->procs[j]->present, (size_t)m);
+  }
   uint64_t dsum = 0, dxor = 0;
   int nt = threads > 0 ? threads : 1;
   (void)nt;
@@ -595,8 +628,9 @@ int avo_sim_round_ex(avo_sim* s, int64_t n0, int64_t n1, const uint32_t* replay_
 #endif
     for (int64_t node = n0; node < n1; ++node) {
       avo_processor* p = s->procs[node];
+      if (!s->polls[node]) continue;  /* a node whose run loop has ended still answers queries */
       avo_sample_peers(s->cfg.seed, node, r, n_nodes, k, s->cfg.peer_mode, peers);
-      if (!s->literal && node_live_valid(p, s->valid) <= AVO_MAX_ELEMENT_POLL) {
+      if (!s->literal && !readd && node_live_valid(p, s->valid) <= AVO_MAX_ELEMENT_POLL) {
         /* cap cannot bind this round (live valid records only decrease within it) */
         for (int32_t slot = 0; slot < k; ++slot) {
           const int64_t peer = peers[slot];
@@ -625,6 +659,7 @@ int avo_sim_round_ex(avo_sim* s, int64_t n0, int64_t n1, const uint32_t* replay_
         for (int64_t i = 0; i < ni; ++i) {
           int64_t t = invs[i];
           uint32_t err;
+          if (readd && !pres0[peer * m + t] && s->valid[t]) __atomic_store_n(&readd[peer * m + t], 1, __ATOMIC_RELAXED);
           if (replay_errs) {
             err = replay_errs[(node * k + slot) * m + t];
           } else if (s->byz[peer]) {
@@ -668,11 +703,21 @@ int avo_sim_round_ex(avo_sim* s, int64_t n0, int64_t n1, const uint32_t* replay_
     for (int64_t node = n0; node < n1; ++node) free(bufs[node - n0].rows);
     free(bufs);
   }
+  int64_t p0 = n0, p1 = n1;
+  if (readd) {
+    for (int64_t j = 0; j < n_nodes; ++j)
+      for (int64_t t = 0; t < m; ++t)
+        if (readd[j * m + t]) avo_processor_add(s->procs[j], t, 1, s->valid[t]); /* &tx{isAccepted: true} */
+    free(pres0);
+    free(readd);
+    p0 = 0;  /* re-adds touch any node's rows */
+    p1 = n_nodes;
+  }
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static) num_threads(nt)
 #endif
-  for (int64_t j = n0; j < n1; ++j)
-    for (int64_t t = 0; t < m; ++t) s->pref[j * m + t] = (uint8_t)published_pref(s->procs[j], t);
+  for (int64_t j = p0; j < p1; ++j)
+    for (int64_t t = 0; t < m; ++t) s->pref[j * m + t] = (uint8_t)published_pref_mode(s->procs[j], t, s->responder);
   if (applied_votes) *applied_votes = applied;
   s->round++;
   return rc;

@@ -45,6 +45,12 @@ extern "C" {
 #define AVO_DOM_PAIRS 4u
 #define AVO_DOM_REPLAY 5u
 
+/* What a node publishes for a target it no longer holds (see
+ * published_pref_mode in avalanche_oracle.c) */
+#define AVO_RESP_DECISION 0    /* R2 (default): the finalized decision */
+#define AVO_RESP_IS_ACCEPTED 1 /* processor.go:125-130: false after deletion */
+#define AVO_RESP_EXAMPLE 2     /* main.go:175-182: re-added as accepted when queried, answers yes */
+
 #define AVO_PEERS_RANDOM 0
 #define AVO_PEERS_ROUND_ROBIN 1
 
@@ -141,6 +147,8 @@ int avo_sim_round_ex(avo_sim* s, int64_t n0, int64_t n1, const uint32_t* replay_
  * RegisterVotes per slot); 0 (default): the branch-free per-node form when the
  * poll cap cannot bind. Both are the same restatement; tests compare them. */
 void avo_sim_set_literal(avo_sim* s, int literal);
+void avo_sim_set_responder(avo_sim* s, int32_t mode); /* AVO_RESP_* */
+void avo_sim_set_polling(avo_sim* s, int64_t node, int polls);
 /* One node's literal round against an external snapshot (pref_words
  * [n_nodes][ceil(m/32)] bitsets, byz_words [ceil(n/32)]): words[m] canonical
  * record words in/out; digest accumulates its StatusUpdates; returns the

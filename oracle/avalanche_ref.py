@@ -148,10 +148,18 @@ class Processor:
             invs.append(h)
         return invs[:MAX_ELEMENT_POLL]
 
-    def published(self, h: int) -> bool:
+    def published(self, h: int, responder: int = 0) -> bool:
+        """What this node answers for h: its record's IsAccepted; without a
+        record: 0 = the finalized decision (R2), 1 = IsAccepted literally
+        (false, processor.go:125-130), 2 = the example's responder (it re-adds
+        &tx{isAccepted: true} first and answers yes, main.go:175-182)."""
         vr = self.vote_records.get(h)
         if vr is not None:
             return vr.is_accepted()
+        if responder == 1:
+            return False
+        if responder == 2:
+            return True
         return bool(self.decision.get(h, False))
 
     def dump_word(self, h: int) -> int:
@@ -255,23 +263,35 @@ class Sim:
                 for t in range(n_targets):
                     p.add_target_to_reconcile(Target(t, accepted=initial_accept(seed, init_mode, init_param, j, t)))
                     p.targets[t] = self.targets[t]  # validity is a property of the shared target
+        self.responder = 0
+        self.polls = [True] * n_nodes
         self.pref = self._snapshot()
 
     def set_valid(self, t, valid):
         self.targets[t].valid = bool(valid)
 
+    def set_responder(self, mode):
+        self.responder = mode
+        self.pref = self._snapshot()
+
     def _snapshot(self):
-        return [[p.published(t) for t in range(self.m)] for p in self.procs]
+        return [[p.published(t, self.responder) for t in range(self.m)] for p in self.procs]
 
     def run_round(self, replay_errs=None):
         r, updates = self.round, []
+        held = [set(p.vote_records) for p in self.procs]  # round-start records (responder 2)
+        readd = set()
         for node, p in enumerate(self.procs):
+            if not self.polls[node]:  # the example's run loop has returned (main.go:160-162)
+                continue
             peers = sample_peers(self.seed, node, r, self.n, self.k, self.peer_mode)
             for slot in range(self.k):
                 invs = p.get_invs_for_next_poll()
                 peer = peers[slot]
                 votes = []
                 for t in invs:
+                    if self.responder == 2 and t not in held[peer] and self.targets[t].valid:
+                        readd.add((peer, t))  # AddTargetToReconcile(&tx{isAccepted: true}) (main.go:175-177)
                     if replay_errs is not None:
                         err = int(replay_errs[node, slot, t])
                     elif self.byz[peer]:
@@ -282,6 +302,9 @@ class Sim:
                 ups = []
                 p.register_votes(peer, votes, ups)
                 updates.extend((r, node, slot, h, st) for h, st in ups)
+        for peer, t in sorted(readd):
+            self.procs[peer].add_target_to_reconcile(Target(t, accepted=True))
+            self.procs[peer].targets[t] = self.targets[t]
         self.pref = self._snapshot()
         self.round += 1
         return updates

@@ -67,6 +67,8 @@ def lib():
         L.avo_sim_get_round.restype = C.c_int64
         L.avo_sim_get_round.argtypes = [C.c_void_p, C.c_int64]
         L.avo_sim_set_round.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
+        L.avo_sim_set_responder.argtypes = [C.c_void_p, C.c_int32]
+        L.avo_sim_set_polling.argtypes = [C.c_void_p, C.c_int64, C.c_int]
         L.avo_sim_set_literal.argtypes = [C.c_void_p, C.c_int]
         L.avo_mix64.restype = C.c_uint64
         L.avo_mix64.argtypes = [C.c_uint64]
@@ -187,6 +189,14 @@ class Sim:
 
     def set_round(self, node, rnd):
         lib().avo_sim_set_round(self._h, node, rnd)
+
+    def set_responder(self, mode):
+        """0: publish the decision (R2); 1: IsAccepted literally (processor.go:125-130);
+        2: the example's responder, re-adding queried targets (main.go:175-182)."""
+        lib().avo_sim_set_responder(self._h, mode)
+
+    def set_polling(self, node, polls):
+        lib().avo_sim_set_polling(self._h, node, int(polls))
 
     def set_literal(self, literal=True):
         """Force the literal per-vote path (cross-check of the branch-free one)."""

@@ -360,7 +360,7 @@ def test_c4_shape_properties():
         if warm_bytes is not None:
             assert b16 - b1 == lanes * warm_bytes + emitted_bytes(u[~r0])
         else:
-            assert lanes * 108 <= b16 - b1 - emitted_bytes(u[~r0]) <= lanes * 15 * 136
+            assert lanes * 15 * 108 <= b16 - b1 - emitted_bytes(u[~r0]) <= lanes * 15 * 136
         assert not np.isin(u[:, 4], [avhip.STATUS_FINALIZED, avhip.STATUS_INVALID]).any()
         recs = e.read_records(0, n, 0, m)
         assert ((recs >> 17) < 128).all()

@@ -333,3 +333,60 @@ def test_digest_mode_matches_rows(oracle):
         assert na == nb and d == oracle.update_digest(words), r
         assert int(words[0]) == oracle.pack_update(3, int(u[0, 1]), int(u[0, 2]), int(u[0, 3]), int(u[0, 4]))
     assert np.array_equal(a.dump(), b.dump())
+
+
+@pytest.mark.parametrize("responder", [1, 2])
+def test_sim_responder_modes_c_vs_python(oracle, responder):
+    """Responder variants: 1 = IsAccepted literally (a deleted
+    record answers no, processor.go:125-130); 2 = the example's responder
+    (main.go:175-182: a queried target it does not hold is re-added as
+    accepted and answered yes). Some nodes stop polling (the example's run
+    loop returns, main.go:160-162) but keep answering."""
+    n, m, k = 24, 70, 3
+    kw = dict(seed=6, byz_threshold=int(0.2 * 2**32), init_mode=2)
+    c = oracle.Sim(n, m, k, **kw)
+    p = ref.Sim(n, m, k, 6, byz_threshold=int(0.2 * 2**32), init_mode=2)
+    c.set_responder(responder)
+    p.set_responder(responder)
+    for r in range(60):
+        if r == 30:
+            for j in (2, 5, 11):
+                c.set_polling(j, False)
+                p.polls[j] = False
+        if r == 20:
+            c.set_valid(4, False)
+            p.set_valid(4, False)
+        u1, _ = c.run_round()
+        u2 = p.run_round()
+        assert [tuple(x) for x in u1.tolist()] == [tuple(x) for x in u2], r
+        assert np.array_equal(c.dump(), p.dump()), r
+        assert np.array_equal(c.pref(), np.array(p.pref, np.uint8)), r
+
+
+def run_example_oracle(oracle, n=100, m=100, max_rounds=2000):
+    """examples/basic-preconcensus (main.go:91-192) as synchronous rounds:
+    every node adds every tx as accepted (main.go:49-54), polls one peer per
+    round in round-robin order skipping itself (main.go:110-116, k = 1), the
+    responder re-adds what it does not hold (main.go:175-177), and a node's
+    loop returns once it counted txCount Finalized updates (main.go:143-162)."""
+    sim = oracle.Sim(n, m, 1, peer_mode=1, init_mode=2)
+    sim.set_responder(2)
+    finalized = np.zeros(n, np.int64)
+    rounds, all_updates = 0, []
+    while (finalized < m).any() and rounds < max_rounds:
+        u, _ = sim.run_round()
+        all_updates.append(u)
+        fin = u[u[:, 4] == 3]
+        np.add.at(finalized, fin[:, 1], 1)
+        for j in np.flatnonzero(finalized >= m):
+            sim.set_polling(int(j), False)
+        rounds += 1
+    return sim, rounds, finalized, all_updates
+
+
+def test_example_c1_oracle():
+    from oracle import cabi
+
+    sim, rounds, finalized, _ = run_example_oracle(cabi)
+    assert (finalized >= 100).all()  # "Nodes fully finalized: 100"
+    assert rounds == 134  # every record finalizes at its 134th vote (vote.go:66-69), one vote per round
