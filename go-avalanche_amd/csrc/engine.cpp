@@ -785,62 +785,88 @@ int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uin
 
 int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const uint32_t* errs, int64_t n,
                       int32_t* status_out) {
+  const int64_t offs[2] = {0, n};
+  return av_register_votes_batch(e, 1, &node, offs, targets, errs, status_out);
+}
+
+int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, const int64_t* offsets,
+                            const int64_t* targets, const uint32_t* errs, int32_t* status_out) {
   AV_ENTER(e);
   {
     int rc = peer_local_write_check(e);
     if (rc != AV_OK) return rc;
   }
-  AV_CHECK(n >= 0 && (n == 0 || (targets && errs && status_out)), AV_ERR_INVALID_ARG, "null argument");
-  AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
+  AV_CHECK(n_resp >= 0 && (n_resp == 0 || (nodes && offsets)), AV_ERR_INVALID_ARG, "null argument");
+  if (n_resp == 0) return AV_OK;
+  AV_CHECK(offsets[0] == 0, AV_ERR_INVALID_ARG, "offsets[0] must be 0");
+  for (int64_t i = 0; i < n_resp; ++i) {
+    AV_CHECK(offsets[i + 1] >= offsets[i], AV_ERR_INVALID_ARG, "offsets must not decrease");
+    AV_CHECK(local_node(e, nodes[i]), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)nodes[i]);
+  }
+  const int64_t n = offsets[n_resp];
+  AV_CHECK(n == 0 || (targets && errs && status_out), AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(n < (1ll << 31), AV_ERR_INVALID_ARG, "too many votes in one call");
   {
     int rc = materialize_votes(e);
     if (rc != AV_OK) return rc;
   }
   for (int64_t i = 0; i < n; ++i) status_out[i] = -1;
   e->fresh = false;
-  e->count_bound = std::min<int64_t>(127, e->count_bound + n);  // at most one step per vote
-  // group votes by block, keeping Response order inside each block
-  std::vector<uint32_t> cnt(e->BL + 1, 0);
-  int64_t nv = 0;
-  for (int64_t i = 0; i < n; ++i)
-    if (local_target(e, targets[i])) {
-      cnt[(uint32_t)((targets[i] - e->t0) >> 5)]++;
-      nv++;
+  // every vote of every Response applies to its (node, 32-target block) lane
+  // in Response order, then vote order: group the votes by lane, keeping that
+  // order (the global vote index grows with it)
+  std::vector<std::pair<uint32_t, uint32_t>> lv;  // (lane, vote index)
+  lv.reserve((size_t)n);
+  std::vector<int32_t> per_node_votes;
+  int64_t max_node_votes = 0;
+  {
+    std::vector<int64_t> cnt;
+    for (int64_t i = 0; i < n_resp; ++i) {
+      const uint32_t nl = (uint32_t)(nodes[i] - e->n0);
+      for (int64_t v = offsets[i]; v < offsets[i + 1]; ++v) {
+        if (!local_target(e, targets[v])) continue;  // unknown hash (processor.go:95-99)
+        lv.emplace_back(nl * e->BL + (uint32_t)((targets[v] - e->t0) >> 5), (uint32_t)v);
+        if ((int32_t)errs[v] < 0) e->c_monotone = false;  // neutral vote shifts in consider = 0
+      }
     }
-  if (nv == 0) return AV_OK;
-  std::vector<uint32_t> blocks, offs;
-  std::vector<uint32_t> start(e->BL, 0);
-  uint32_t acc = 0;
-  for (uint32_t b = 0; b < e->BL; ++b) {
-    if (cnt[b]) {
-      blocks.push_back(b);
-      offs.push_back(acc);
-      start[b] = acc;
-      acc += cnt[b];
+    // at most one confidence step per vote: bound by the most votes one node gets
+    std::vector<std::pair<uint32_t, int64_t>> nn;
+    for (int64_t i = 0; i < n_resp; ++i) nn.emplace_back((uint32_t)(nodes[i] - e->n0), offsets[i + 1] - offsets[i]);
+    std::sort(nn.begin(), nn.end());
+    for (size_t i = 0; i < nn.size();) {
+      int64_t c = 0;
+      size_t j = i;
+      for (; j < nn.size() && nn[j].first == nn[i].first; ++j) c += nn[j].second;
+      max_node_votes = std::max(max_node_votes, c);
+      i = j;
     }
   }
-  offs.push_back(acc);
-  std::vector<uint32_t> entries(2 * (size_t)nv);
-  for (int64_t i = 0; i < n; ++i) {
-    if (!local_target(e, targets[i])) continue;
-    const int64_t tl = targets[i] - e->t0;
-    const uint32_t b = (uint32_t)(tl >> 5);
-    const uint32_t err = errs[i];
-    if ((int32_t)err < 0) e->c_monotone = false;  // neutral vote shifts in consider = 0
-    const uint32_t meta = (uint32_t)(tl & 31) | ((err == 0u ? 1u : 0u) << 5) | (((int32_t)err >= 0 ? 1u : 0u) << 6);
-    const uint32_t slot = start[b]++;
-    entries[2 * (size_t)slot] = (uint32_t)i;
-    entries[2 * (size_t)slot + 1] = meta;
+  e->count_bound = (int)std::min<int64_t>(127, e->count_bound + max_node_votes);
+  if (lv.empty()) return AV_OK;
+  std::sort(lv.begin(), lv.end());
+  std::vector<uint32_t> lanes, offs, entries(2 * lv.size());
+  for (size_t i = 0; i < lv.size(); ++i) {
+    if (i == 0 || lv[i].first != lv[i - 1].first) {
+      lanes.push_back(lv[i].first);
+      offs.push_back((uint32_t)i);
+    }
+    const uint32_t v = lv[i].second;
+    const int64_t tl = targets[v] - e->t0;
+    const uint32_t err = errs[v];
+    entries[2 * i] = v;
+    entries[2 * i + 1] = (uint32_t)(tl & 31) | ((err == 0u ? 1u : 0u) << 5) | (((int32_t)err >= 0 ? 1u : 0u) << 6);
   }
-  const size_t nb = blocks.size();
-  Scratch s;
+  offs.push_back((uint32_t)lv.size());
+  const size_t nb = lanes.size();
   const size_t words = nb + (nb + 1) + entries.size() + (size_t)n;
-  AV_HIP(s.ensure(words * 4 + 64));
-  auto* dblocks = static_cast<uint32_t*>(s.p);
-  auto* doffs = dblocks + nb;
+  void* buf = nullptr;
+  int rc = engine_scratch(e, words * 4 + 64, &buf);
+  if (rc != AV_OK) return rc;
+  auto* dlanes = static_cast<uint32_t*>(buf);
+  auto* doffs = dlanes + nb;
   auto* dent = doffs + nb + 1;
   auto* dstat = reinterpret_cast<int32_t*>(dent + entries.size());
-  AV_HIP(hipMemcpyAsync(dblocks, blocks.data(), nb * 4, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(hipMemcpyAsync(dlanes, lanes.data(), nb * 4, hipMemcpyHostToDevice, e->stream));
   AV_HIP(hipMemcpyAsync(doffs, offs.data(), (nb + 1) * 4, hipMemcpyHostToDevice, e->stream));
   AV_HIP(hipMemcpyAsync(dent, entries.data(), entries.size() * 4, hipMemcpyHostToDevice, e->stream));
   AV_HIP(hipMemsetAsync(dstat, 0xFF, (size_t)n * 4, e->stream));
@@ -849,13 +875,12 @@ int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const 
   p.pref = e->pref[e->cur];
   p.valid = e->valid;
   p.byz = e->byz;
-  p.blocks = dblocks;
+  p.blocks = dlanes;
   p.offs = doffs;
   p.entries = dent;
   p.status_out = dstat;
   p.n_blocks = (uint32_t)nb;
-  p.node_local = (uint32_t)(node - e->n0);
-  p.node = (uint32_t)node;
+  p.n0 = (uint32_t)e->n0;
   p.BL = e->BL;
   p.round = (uint32_t)e->round;
   p.pub_mode = (uint32_t)e->pub_mode;

@@ -202,11 +202,11 @@ struct DropInParams {
   uint32_t* pref;          // current published snapshot row for the node
   const uint32_t* valid;
   const uint32_t* byz;
-  const uint32_t* blocks;  // touched local blocks
+  const uint32_t* blocks;  // touched lanes (local node * BL + block), each once
   const uint32_t* offs;    // [n_blocks + 1] into entries
   const uint32_t* entries; // pairs (pos, meta = bit | yes<<5 | considered<<6)
   int32_t* status_out;     // per vote position, -1 = no update
-  uint32_t n_blocks, node_local, node, BL, round;
+  uint32_t n_blocks, n0, BL, round;
   uint32_t pub_mode;
 };
 hipError_t launch_register_votes(const DropInParams& p, hipStream_t s);

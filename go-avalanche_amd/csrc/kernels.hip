@@ -270,13 +270,16 @@ __device__ __forceinline__ void capped_node(const RoundParams& p, uint32_t nl, u
 // ---------------------------------------------------------------------------
 // Drop-in RegisterVotes for one node (processor.go:61-122): one thread per
 // touched block applies that block's votes in Response order, so duplicate
-// hashes in one Response apply sequentially. Status per vote position.
+// hashes in one Response apply sequentially. Status per vote position. One
+// thread per touched lane (node, 32-target block) of any number of nodes
+// (av_register_votes_batch): a node's Responses apply one after the other.
 // ---------------------------------------------------------------------------
 __global__ void k_register_votes(const DropInParams p) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n_blocks) return;
-  const uint32_t b = p.blocks[i];
-  const uint32_t g = p.node_local * p.BL + b;
+  const uint32_t g = p.blocks[i];  // lane: local node * BL + block
+  const uint32_t nl = g / p.BL, b = g - nl * p.BL;
+  const uint32_t node = p.n0 + nl;
   St s;
   load_state(p.planes, g, s);
   const uint32_t vmask = p.valid[b];
@@ -299,8 +302,8 @@ __global__ void k_register_votes(const DropInParams p) {
     s.C[q] |= died;
   }
   store_state(p.planes, g, s);
-  p.pref[(size_t)p.node * p.BL + b] =
-      is_byz(p.byz, p.node) ? byz_pattern(p.round) : publish_word(s.A, s.K[7], p.pub_mode);
+  p.pref[(size_t)node * p.BL + b] =
+      is_byz(p.byz, node) ? byz_pattern(p.round) : publish_word(s.A, s.K[7], p.pub_mode);
 }
 
 // AddTargetToReconcile (processor.go:45-58) for a list of targets of one

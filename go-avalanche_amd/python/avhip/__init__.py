@@ -82,6 +82,7 @@ EXPORTED = [
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
     "av_peer_handles", "av_peer_init", "av_get_round", "av_set_round", "av_log_base_round", "av_updates_digest",
     "av_updates_digest_range", "av_read_pref_words", "av_set_polling",
+    "av_register_votes_batch",
 ]
 
 _lib = None
@@ -145,6 +146,7 @@ def lib():
         "av_updates_digest_range": (i32, [_vp, i64, i64, _vp]),
         "av_read_pref_words": (i32, [_vp, i64, i64, _vp]),
         "av_set_polling": (i32, [_vp, i64, i32]),
+        "av_register_votes_batch": (i32, [_vp, i64, _vp, _vp, _vp, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -247,6 +249,18 @@ class Engine:
         e = np.ascontiguousarray(errs, np.uint32)
         st = np.zeros(max(1, t.size), np.int32)
         _check(lib().av_register_votes(self._h, node, _ptr(t), _ptr(e), t.size, _ptr(st)))
+        return st[: t.size]
+
+    def register_votes_batch(self, nodes, offsets, targets, errs):
+        """Many Responses in one call: Response i = node nodes[i], votes
+        offsets[i]..offsets[i+1]-1. Returns the per-vote status (-1 = none)."""
+        nd = np.ascontiguousarray(nodes, np.int64)
+        of = np.ascontiguousarray(offsets, np.int64)
+        t = np.ascontiguousarray(targets, np.int64)
+        e = np.ascontiguousarray(errs, np.uint32)
+        assert of.size == nd.size + 1 and t.size == e.size == (of[-1] if of.size else 0)
+        st = np.zeros(max(1, t.size), np.int32)
+        _check(lib().av_register_votes_batch(self._h, nd.size, _ptr(nd), _ptr(of), _ptr(t), _ptr(e), _ptr(st)))
         return st[: t.size]
 
     def is_accepted(self, node, target):

@@ -12,6 +12,8 @@
  * Reference interfaces replaced (itsdevbear/go-avalanche):
  *   av_add_targets      <- (*Processor).AddTargetToReconcile   processor.go:45-58
  *   av_register_votes   <- (*Processor).RegisterVotes           processor.go:61-122
+ *   av_register_votes_batch <- RegisterVotes of many Responses /  processor.go:61-122, main.go:136
+ *                          Processors in one call
  *   av_is_accepted      <- (*Processor).IsAccepted              processor.go:125-130
  *   av_get_confidence   <- (*Processor).GetConfidence           processor.go:133-140
  *   av_get_invs         <- (*Processor).GetInvsForNextPoll      processor.go:144-170
@@ -130,6 +132,13 @@ int av_set_valid(av_engine* e, int64_t target, int32_t valid);
  * (RegisterVotes returns true: processor.go:121). */
 int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const uint32_t* errs, int64_t n,
                       int32_t* status_out);
+/* RegisterVotes for many Responses in one call (processor.go:61-122 once per
+ * Response, as main.go:136 calls it): Response i is registered by node
+ * nodes[i] with the votes offsets[i] .. offsets[i+1]-1 of targets/errs, in
+ * order; a node may appear several times (its Responses apply one after the
+ * other). status_out[v] as for av_register_votes. */
+int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, const int64_t* offsets,
+                            const int64_t* targets, const uint32_t* errs, int32_t* status_out);
 int av_is_accepted(av_engine* e, int64_t node, int64_t target, int32_t* out);
 /* AV_ERR_NOT_FOUND where the reference panics "VoteRecord not found". */
 int av_get_confidence(av_engine* e, int64_t node, int64_t target, uint16_t* out);

@@ -86,3 +86,38 @@ def test_node_sharded_rccl_world1(oracle):
     comm.run_rounds(R)
     assert np.array_equal(plain.read_records(), comm.read_records())
     assert np.array_equal(plain.fetch_updates(), comm.fetch_updates())
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13])
+def test_register_votes_batch_vs_oracle(oracle, seed):
+    """av_register_votes_batch: many Responses of many nodes in one call (a
+    node may appear several times; its Responses apply in order), with
+    duplicates, unknown hashes, invalid targets, neutral votes and records
+    finalizing inside the batch == the oracle's RegisterVotes per Response."""
+    rng = np.random.default_rng(seed)
+    n, m = 40, 300
+    eng = avhip.Engine(n, m, k=8, seed=seed)
+    eng.init_records(avhip.INIT_BERNOULLI, int(0.6 * 2**32))
+    sim = oracle.Sim(n, m, 8, seed=seed, init_mode=3, init_param=int(0.6 * 2**32))
+    for t in (7, 100):
+        eng.set_valid(t, False)
+        sim.set_valid(t, False)
+    # push records close to 128 so that batches finalize some of them
+    for _ in range(16):
+        eng.run_rounds(1)
+        sim.run_round()
+    eng.discard_updates()
+    for batch in range(12):
+        n_resp = int(rng.integers(1, 60))
+        nodes = rng.integers(0, n, size=n_resp)
+        sizes = rng.integers(0, 200, size=n_resp)
+        offsets = np.concatenate([[0], np.cumsum(sizes)])
+        targets = rng.integers(-3, m + 3, size=int(offsets[-1]))
+        errs = rng.choice(ERRS, size=targets.size)
+        got = eng.register_votes_batch(nodes, offsets, targets, errs)
+        for i in range(n_resp):
+            a, b = int(offsets[i]), int(offsets[i + 1])
+            exp = sim.register_votes(int(nodes[i]), targets[a:b], errs[a:b])
+            have = [(int(targets[v]), int(got[v])) for v in range(a, b) if got[v] >= 0]
+            assert have == exp, (batch, i)
+        check(eng, sim, f"batch {batch}")
