@@ -112,6 +112,9 @@ struct av_engine {
   // option "sweep_nopipe": a walking grid runs without next-tile prefetch
   // (kModeWarm; default); 0 = the prefetching kModeWarmPipe (A/B)
   bool sweep_nopipe = true;
+  // option "wave_runs": a walking grid gives each wave a run of consecutive
+  // tiles whose peers one Philox pass draws (round_sweep.hip WaveDraw)
+  bool wave_runs = true;
   uint32_t tiles_per_wave = 4;  // option "tiles_per_wave" (default grid, default_sweep_blocks)
   // every consider plane of every lane is all-ones: set after a sim round with k >= 8 in which every
   // live record was polled (all targets valid, uncapped); cleared by anything that can write a 0
@@ -160,6 +163,7 @@ struct av_engine {
 
   // responder variant (option "responder", kernels.h pub_mode) and the nodes
   // that no longer poll (av_set_polling); both run the first-generation kernel
+  uint32_t dense_min = 0;  // option "dense_min" (kernels.h dense records; default dense_min(k))
   int32_t pub_mode = 0;
   uint32_t* readd = nullptr;     // [L] pub_mode 2: re-add marks
   uint32_t* died_out = nullptr;  // [L] pub_mode 2: records deleted this round
@@ -260,10 +264,12 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.fresh = 0u;
   p.tn = (uint32_t)(e->t1 - e->t0);
   p.nopipe = e->sweep_nopipe ? 1u : 0u;
+  p.tpw = e->wave_runs && e->sweep_blocks ? 1u : 0u;
   p.pub_mode = (uint32_t)e->pub_mode;
   p.readd = e->pub_mode == 2 ? e->readd : nullptr;
   p.died_out = e->pub_mode == 2 ? e->died_out : nullptr;
   p.nopoll = e->any_nopoll ? e->nopoll : nullptr;
+  p.dense_min = e->dense_min;
   return p;
 }
 
@@ -628,7 +634,8 @@ int av_create(const av_config* cfg, av_engine** out) {
   // a dense record holds >= dense_min(k) updates: log_cap / dense_min records
   // take any log_cap updates that go dense (8 B of capacity per update)
   const uint32_t dw = avk::dense_words((uint32_t)e->k);
-  e->dlog_cap = std::max<uint32_t>(e->log_cap / avk::dense_min((uint32_t)e->k), 16);
+  e->dense_min = avk::dense_min((uint32_t)e->k);
+  e->dlog_cap = std::max<uint32_t>(e->log_cap / e->dense_min, 16);
   if ((he = dev_alloc(&e->dlog, (size_t)e->dlog_cap * e->log_shards * dw)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->dlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->upd_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
@@ -1443,6 +1450,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     } else {
       e->sweep_blocks = (uint32_t)value;
     }
+  } else if (n == "wave_runs") {
+    e->wave_runs = value != 0;
   } else if (n == "sweep_nopipe") {
     e->sweep_nopipe = value != 0;
   } else if (n == "tiles_per_wave") {
@@ -1481,6 +1490,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     rc = refresh_pref(e);  // republish the current snapshot under the new rule
     if (rc != AV_OK) return rc;
     AV_HIP(hipStreamSynchronize(e->stream));
+  } else if (n == "dense_min") {  // tuning (A/B): fewer updates per dense record; the dense log may fill sooner
+    AV_CHECK(value >= 1 && value <= 32 * (int64_t)e->k + 1, AV_ERR_INVALID_ARG, "bad dense_min");
+    e->dense_min = (uint32_t)value;
   } else if (n == "fresh") {  // 0: a round after init reads every plane (A/B only)
     if (!value) e->fresh = false;
   } else if (n == "peer_fine") {  // before av_peer_handles: fine-grained snapshot buffers (default 1)

@@ -110,6 +110,7 @@ struct RoundParams {
   // targets (tn = targets in this engine's range).
   uint32_t fresh;
   uint32_t tn;
+  uint32_t tpw;     // kModeWarm, k = 8: run length of consecutive tiles per wave with one shared peer draw (0 = grid stride)
   uint32_t nopipe;  // tuning: a grid smaller than the tile count runs kModeWarm (no next-tile prefetch)
   // Responder variants (engine option "responder", first-generation kernel
   // only; see publish_word): pub_mode 0 = R2 decision, 1 = IsAccepted
@@ -121,6 +122,7 @@ struct RoundParams {
   uint32_t* readd;
   uint32_t* died_out;
   const uint32_t* nopoll;
+  uint32_t dense_min;  // a lane with >= dense_min updates logs one dense record (default dense_min(k))
 };
 constexpr uint32_t kPendAllLive = 0x80000000u;
 constexpr uint32_t kVStale = 1u, kVUniform = 2u;

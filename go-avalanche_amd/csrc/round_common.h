@@ -326,7 +326,7 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
 #pragma unroll
   for (int j = 0; j < K; ++j) cnt += (uint32_t)__popc(E[j]);
   constexpr uint32_t DW = dense_words(K);
-  const bool dense = cnt >= dense_min(K);
+  const bool dense = cnt >= p.dense_min;
   const uint64_t dl = __ballot(dense);
   const uint32_t tot_u = wave_sum(cnt), tot_s = wave_sum(dense ? 0u : cnt);
   const uint32_t tot_d = (uint32_t)__popcll(dl);

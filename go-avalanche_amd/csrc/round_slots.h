@@ -269,6 +269,66 @@ __device__ __forceinline__ PairDraw pair_draw(const RoundParams& p, uint32_t rou
   return d;
 }
 
+// One draw of `round` for the nn nodes starting at local node nlA (nn * 2
+// <= 64 producer lanes at k = 8): producer lane q holds Philox block q % 2 of
+// node nlA + q / 2; distinctness of a node's 8 candidates is decided on its
+// two producer lanes. The layout of pair_draw's second half, for all 64 lanes.
+__device__ __forceinline__ PairDraw single_draw(const RoundParams& p, uint32_t round, uint32_t nlA, uint32_t nn,
+                                                uint32_t lane) {
+  PairDraw d;
+  const uint32_t others = p.n_nodes - 1u;
+  d.fallback = p.peer_mode == 1 || 8u >= others || nn * 2u > 64u;
+  d.bad = 0ull;
+  if (d.fallback) return d;
+  uint32_t q = lane;
+  asm volatile("" : "+v"(q));  // opaque: keep the lane-derived counters where they are used
+  const uint32_t pnode = p.n0 + nlA + min(q >> 1, nn - 1u);
+  uint32_t x[4];
+  philox(x, p.seed, pnode, round, q & 1u, kDomPeers);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t u = __umulhi(x[i], others);
+    d.prod[i] = u + (u >= pnode ? 1u : 0u);
+  }
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t part = (uint32_t)__shfl((int)d.prod[i], (int)(lane ^ 1u), 64);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ok &= d.prod[j] != part;
+#pragma unroll
+    for (int j = 0; j < i; ++j) ok &= d.prod[i] != d.prod[j];
+  }
+  d.bad = __ballot(!ok);
+  return d;
+}
+
+// A draw parked in LDS (sd[q * 4 + i] = producer lane q's prod[i]): the node
+// whose producers are lanes base, base + 1 reads its 8 candidates as two
+// 16-byte broadcasts. `bad` = the draw's ballot.
+__device__ __forceinline__ void park_draw(const PairDraw& d, uint32_t* sd, uint32_t lane) {
+  *reinterpret_cast<u32x4*>(sd + lane * 4u) = u32x4{d.prod[0], d.prod[1], d.prod[2], d.prod[3]};
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void pick_parked(const RoundParams& p, const uint32_t* sd, unsigned long long bad,
+                                            uint32_t base, uint32_t node, uint32_t round, uint32_t (&peers)[8]) {
+  const u32x4 lo = *reinterpret_cast<const u32x4*>(sd + base * 4u);
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(sd + base * 4u + 4u);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    peers[c] = lo[c];
+    peers[c + 4] = hi[c];
+  }
+  if ((bad >> base) & 3ull) {
+    const PeerList<8> g = sample_peers_general<8>(p.seed, node, round, p.n_nodes, p.peer_mode);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) peers[j] = g.v[j];
+  }
+}
+
 // which = 0: round - 1's peers, 1: round's (pair_draw's round)
 __device__ __forceinline__ void pick_peers(const RoundParams& p, const PairDraw& d, uint32_t which, uint32_t round,
                                            uint32_t node, uint32_t nl, uint32_t nlA, uint32_t nn, uint32_t lane,

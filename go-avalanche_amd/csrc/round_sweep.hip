@@ -62,6 +62,17 @@ struct TileIn {
   uint32_t cw[REPLAY ? K : 1];   // consider bits: int32(err) >= 0 (vote.go:56); sim votes: all-ones
 };
 
+// The peer draws of a wave's run of consecutive tiles, made once for the
+// whole run (kModeWarm with p.tpw, k = 8): `pair` = round - 1's and round's
+// draws (some tile of the run is kVStale), else round's only; `ok` = the
+// run's nodes fit the producer lanes (otherwise every tile draws its own).
+struct WaveDraw {
+  const uint32_t* sd;  // the draw, parked in LDS (round_slots.h park_draw)
+  unsigned long long bad;
+  uint32_t nlA;
+  bool pair, ok;
+};
+
 struct LaneIdx {
   uint32_t g, gc, nl, b, node;
   bool active;
@@ -80,7 +91,7 @@ __device__ __forceinline__ LaneIdx lane_idx(const RoundParams& p, uint32_t tile,
 
 template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE, bool VVM = false, bool FRESH = false>
 __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
-                                          TileIn<K, REPLAY, WARM>& in) {
+                                          TileIn<K, REPLAY, WARM>& in, const WaveDraw* wd = nullptr) {
   const LaneIdx x = lane_idx(p, tile, lane);
   const uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
   const u32x4* const grp = reinterpret_cast<const u32x4*>(tp) + lane;
@@ -134,7 +145,20 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
     uint32_t peers[K];
     bool drawn = false;
     if constexpr (VV) {
-      if (in.stale == kVStale) {
+      if (wd && wd->ok) {  // the wave's draws, made once for its run of tiles
+        const uint32_t base = (x.nl - wd->nlA) * 2u;
+        if (in.stale == kVStale) {
+          uint32_t pp[K];
+          pick_parked(p, wd->sd, wd->bad, base, x.node, p.round - 1u, pp);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) in.v0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) in.v1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
+          in.v1[3] = 0u;
+        }
+        pick_parked(p, wd->sd, wd->bad, base + (wd->pair ? 32u : 0u), x.node, p.round, peers);
+        drawn = true;
+      } else if (in.stale == kVStale) {
         // the vote register after last round's 8 sim votes is those votes:
         // V_i = (previous round's slot 7 - i vote); V_7 is never read at k = 8
         const PairDraw pd = pair_draw(p, p.round, nlA, nn, lane);
@@ -429,11 +453,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
       cur = nxt;
     }
   } else {
-    for (uint32_t tile = wave0; tile < tiles; tile += nwaves) {
+    uint32_t tile = wave0, tile_end = tiles, stride = nwaves;
+    WaveDraw wd;
+    wd.ok = false;
+    wd.pair = false;
+    wd.nlA = 0u;
+    wd.bad = 0ull;
+    wd.sd = nullptr;
+    if constexpr (MODE == kModeWarm && K == 8) {
+      if (p.tpw) {
+        // a run of p.tpw consecutive tiles per wave; one Philox pass draws the
+        // peers of all its nodes (round - 1's too if a tile is kVStale)
+        tile = wave0 * p.tpw;
+        tile_end = min(tile + p.tpw, tiles);
+        stride = 1u;
+        if (tile < tiles) {
+          const uint32_t nlA = uni(div_bl(p, tile * 64u));
+          const uint32_t nlB = uni(div_bl(p, min(tile_end * 64u, p.L) - 1u));
+          const uint32_t nn = nlB - nlA + 1u;
+          bool any_stale = false;
+          if (p.vv)
+            for (uint32_t t = tile; t < tile_end; ++t) any_stale |= uni(p.vstale[t]) == kVStale;
+          __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][256];
+          const PairDraw d = any_stale ? pair_draw(p, p.round, nlA, nn, lane) : single_draw(p, p.round, nlA, nn, lane);
+          wd.nlA = nlA;
+          wd.pair = any_stale;
+          wd.ok = !d.fallback;
+          wd.bad = d.bad;
+          wd.sd = s_draw[threadIdx.x >> 6];
+          if (wd.ok) park_draw(d, s_draw[threadIdx.x >> 6], lane);
+        }
+      }
+    }
+    for (; tile < tile_end; tile += stride) {
       constexpr bool AB = MODE == kModeAblate;
       if constexpr (MODE == kModeWarm) {
         TileIn<K, false, true> in;
-        load_tile<K, false, true, POL, false, true>(p, tile, lane, in);
+        load_tile<K, false, true, POL, false, true>(p, tile, lane, in, &wd);
         process_tile<K, false, true, POL, true>(p, tile, lane, in, 0u, acc);
       } else if constexpr (MODE == kModeFresh) {
         TileIn<K, false, false> in;
@@ -497,9 +553,18 @@ hipError_t launch_mode(const RoundParams& p, uint32_t grid, hipStream_t s) {
 }
 
 template <int K>
-hipError_t launch_sweep_k(const RoundParams& p, bool replay, uint32_t blocks, hipStream_t s) {
-  const uint32_t need = (p.Lpad / 64u + 3u) / 4u;
+hipError_t launch_sweep_k(const RoundParams& p_in, bool replay, uint32_t blocks, hipStream_t s) {
+  const uint32_t need = (p_in.Lpad / 64u + 3u) / 4u;
   const uint32_t grid = std::max(1u, blocks ? std::min(blocks, need) : need);
+  RoundParams p = p_in;
+  p.tpw = 0u;
+  if (p_in.tpw && K == 8 && !replay && !p.ablate_gather && !p.fresh && p.warm_skip && p.warm_all) {
+    // p_in.tpw = enabled: each wave takes a run of consecutive tiles
+    const uint32_t tiles = p.Lpad / 64u, waves = grid * 4u;
+    p.tpw = (tiles + waves - 1u) / waves;
+    if (p.tpw > 16u) p.tpw = 0u;  // long runs: grid stride (their nodes overflow the shared draw anyway)
+    if (p.tpw) return launch_mode<K, kModeWarm>(p, grid, s);
+  }
   if (replay) return launch_mode<K, kModeReplay>(p, grid, s);
   if (p.ablate_gather) return launch_mode<K, kModeAblate>(p, grid, s);
   if (p.fresh) return launch_mode<K, kModeFresh>(p, grid, s);
