@@ -115,6 +115,8 @@ struct av_engine {
   // option "wave_runs": a walking grid gives each wave a run of consecutive
   // tiles whose peers one Philox pass draws (round_sweep.hip WaveDraw)
   bool wave_runs = true;
+  // option "settled_fast": settled warm tiles skip the round step's bookkeeping
+  bool settled_fast = true;
   uint32_t tiles_per_wave = 4;  // option "tiles_per_wave" (default grid, default_sweep_blocks)
   // every consider plane of every lane is all-ones: set after a sim round with k >= 8 in which every
   // live record was polled (all targets valid, uncapped); cleared by anything that can write a 0
@@ -265,6 +267,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.tn = (uint32_t)(e->t1 - e->t0);
   p.nopipe = e->sweep_nopipe ? 1u : 0u;
   p.tpw = e->wave_runs && e->sweep_blocks ? 1u : 0u;
+  p.settled_fast = e->settled_fast ? 1u : 0u;
   p.pub_mode = (uint32_t)e->pub_mode;
   p.readd = e->pub_mode == 2 ? e->readd : nullptr;
   p.died_out = e->pub_mode == 2 ? e->died_out : nullptr;
@@ -380,7 +383,8 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   const bool compat = e->pub_mode != 0 || e->any_nopoll;
   AV_CHECK(!(compat && e->capped && (e->pub_mode == 2 || e->any_nopoll)), AV_ERR_UNSUPPORTED,
            "the example responder and av_set_polling need M <= 4096 (uncapped)");
-  const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped && !compat;
+  // the sweep addresses the preference table by 32-bit byte offsets
+  const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped && !compat && (uint64_t)e->N * e->BL < (1ull << 30);
   // the round after av_init_records: planes known to be zero are not read
   const bool fresh = e->fresh && sweep && !replay && !e->ablate_gather;
   // the sweep's warm sim modes (launch_sweep_k): every consider plane all-ones
@@ -1450,6 +1454,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     } else {
       e->sweep_blocks = (uint32_t)value;
     }
+  } else if (n == "settled_fast") {
+    e->settled_fast = value != 0;
   } else if (n == "wave_runs") {
     e->wave_runs = value != 0;
   } else if (n == "sweep_nopipe") {

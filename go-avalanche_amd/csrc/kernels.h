@@ -111,6 +111,7 @@ struct RoundParams {
   uint32_t fresh;
   uint32_t tn;
   uint32_t tpw;     // kModeWarm, k = 8: run length of consecutive tiles per wave with one shared peer draw (0 = grid stride)
+  uint32_t settled_fast;  // kModeWarm, k = 8: settled tiles skip process_tile (round_sweep.hip settled_fast)
   uint32_t nopipe;  // tuning: a grid smaller than the tile count runs kModeWarm (no next-tile prefetch)
   // Responder variants (engine option "responder", first-generation kernel
   // only; see publish_word): pub_mode 0 = R2 decision, 1 = IsAccepted

@@ -25,6 +25,9 @@ __device__ __forceinline__ void philox(uint32_t x[4], uint64_t seed, uint32_t a,
                                        uint32_t dom) {
   uint32_t c0 = a, c1 = b, c2 = c, c3 = dom;
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  // opaque key: the 20-word key schedule is recomputed (SALU) per call instead
+  // of being hoisted out of the tile loop into 20 live SGPRs (spills)
+  asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     if (r) {

@@ -303,29 +303,33 @@ __device__ __forceinline__ PairDraw single_draw(const RoundParams& p, uint32_t r
   return d;
 }
 
-// A draw parked in LDS (sd[q * 4 + i] = producer lane q's prod[i]): the node
-// whose producers are lanes base, base + 1 reads its 8 candidates as two
-// 16-byte broadcasts. `bad` = the draw's ballot.
-__device__ __forceinline__ void park_draw(const PairDraw& d, uint32_t* sd, uint32_t lane) {
-  *reinterpret_cast<u32x4*>(sd + lane * 4u) = u32x4{d.prod[0], d.prod[1], d.prod[2], d.prod[3]};
+// A draw parked in LDS as preference-row byte offsets (sd[q * 4 + i] =
+// producer lane q's prod[i] * row_bytes): the node whose producers are lanes
+// base, base + 1 reads its 8 candidates' rows as two 16-byte broadcasts.
+// `bad` = the draw's ballot.
+__device__ __forceinline__ void park_draw(const PairDraw& d, uint32_t* sd, uint32_t lane, uint32_t row_bytes) {
+  *reinterpret_cast<u32x4*>(sd + lane * 4u) =
+      u32x4{d.prod[0] * row_bytes, d.prod[1] * row_bytes, d.prod[2] * row_bytes, d.prod[3] * row_bytes};
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// rows[j] = byte offset of peer j's preference row (peer * row_bytes)
 __device__ __forceinline__ void pick_parked(const RoundParams& p, const uint32_t* sd, unsigned long long bad,
-                                            uint32_t base, uint32_t node, uint32_t round, uint32_t (&peers)[8]) {
+                                            uint32_t base, uint32_t node, uint32_t round, uint32_t row_bytes,
+                                            uint32_t (&rows)[8]) {
   const u32x4 lo = *reinterpret_cast<const u32x4*>(sd + base * 4u);
   const u32x4 hi = *reinterpret_cast<const u32x4*>(sd + base * 4u + 4u);
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    peers[c] = lo[c];
-    peers[c + 4] = hi[c];
+    rows[c] = lo[c];
+    rows[c + 4] = hi[c];
   }
   if ((bad >> base) & 3ull) {
     const PeerList<8> g = sample_peers_general<8>(p.seed, node, round, p.n_nodes, p.peer_mode);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) peers[j] = g.v[j];
+    for (int j = 0; j < 8; ++j) rows[j] = g.v[j] * row_bytes;
   }
 }
 

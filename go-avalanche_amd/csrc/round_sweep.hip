@@ -69,9 +69,20 @@ struct TileIn {
 struct WaveDraw {
   const uint32_t* sd;  // the draw, parked in LDS (round_slots.h park_draw)
   unsigned long long bad;
-  uint32_t nlA;
+  uint32_t nlA, t0;
+  uint32_t meta;  // lane i: tile t0 + i's vstale << 8 | kpend & (kPendAllLive | 0xFF)
   bool pair, ok;
 };
+
+__device__ __forceinline__ uint32_t meta_of(const WaveDraw& wd, uint32_t tile) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wd.meta, (int)(tile - wd.t0));
+}
+
+// word at a 32-bit byte offset from a wave-uniform base (SGPR base + VGPR
+// offset addressing: one VALU add per gather instead of a 64-bit multiply-add)
+__device__ __forceinline__ uint32_t at_byte(const uint32_t* base, uint32_t off) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(base) + off);
+}
 
 struct LaneIdx {
   uint32_t g, gc, nl, b, node;
@@ -96,7 +107,8 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
   const uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
   const u32x4* const grp = reinterpret_cast<const u32x4*>(tp) + lane;
   constexpr bool VV = VVM && WARM && !REPLAY && K == 8;  // VVM: the warm sim modes only
-  in.stale = VV && p.vv ? uni(p.vstale[tile]) : 0u;
+  const bool meta = VV && wd && wd->t0 <= tile && tile - wd->t0 < 64u && p.tpw;
+  in.stale = VV && p.vv ? (meta ? (meta_of(*wd, tile) >> 8) & 0xFFu : uni(p.vstale[tile])) : 0u;
   in.kw = 0u;
   if constexpr (FRESH) {
     // NewVoteRecords (vote.go:33-35): votes, consider and count all zero; K7
@@ -113,7 +125,7 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
       in.v1 = ld4<POL>(grp + 64);
     }
     if constexpr (VV) {
-      if (p.klazy || p.kconsume) in.kw = uni(p.kpend[tile]);
+      if (p.klazy || p.kconsume) in.kw = meta ? meta_of(*wd, tile) & (kPendAllLive | 0xFFu) : uni(p.kpend[tile]);
     }
     if (!(in.kw & kPendAllLive) || !p.klazy) {
       in.k0 = ld4<POL>(grp + 128);
@@ -143,21 +155,26 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
   } else {
     const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
     uint32_t peers[K];
-    bool drawn = false;
+    // the gathers address the preference table by 32-bit byte offsets (SGPR
+    // base + VGPR offset: one add per gather): the engine runs the sweep only
+    // for tables below 4 GiB (N * BL < 2^30)
+    const uint32_t rb = p.BL * 4u, bo = x.b * 4u;
+    uint32_t rows[K];  // byte offsets of the peers' rows
+    bool drawn = false, have_rows = false;
     if constexpr (VV) {
-      if (wd && wd->ok) {  // the wave's draws, made once for its run of tiles
+      if (wd && wd->ok) {  // the wave's draws, made once for its run of tiles (implies off32)
         const uint32_t base = (x.nl - wd->nlA) * 2u;
         if (in.stale == kVStale) {
           uint32_t pp[K];
-          pick_parked(p, wd->sd, wd->bad, base, x.node, p.round - 1u, pp);
+          pick_parked(p, wd->sd, wd->bad, base, x.node, p.round - 1u, rb, pp);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) in.v0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
+          for (int i = 0; i < 4; ++i) in.v0[i] = at_byte(p.pref_prev, pp[7 - i] + bo);
 #pragma unroll
-          for (int i = 0; i < 3; ++i) in.v1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
+          for (int i = 0; i < 3; ++i) in.v1[i] = at_byte(p.pref_prev, pp[3 - i] + bo);
           in.v1[3] = 0u;
         }
-        pick_parked(p, wd->sd, wd->bad, base + (wd->pair ? 32u : 0u), x.node, p.round, peers);
-        drawn = true;
+        pick_parked(p, wd->sd, wd->bad, base + (wd->pair ? 32u : 0u), x.node, p.round, rb, rows);
+        drawn = have_rows = true;
       } else if (in.stale == kVStale) {
         // the vote register after last round's 8 sim votes is those votes:
         // V_i = (previous round's slot 7 - i vote); V_7 is never read at k = 8
@@ -176,12 +193,13 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
       }
     }
     if (!drawn) draw_peers<K>(p, p.round, x.node, x.nl, nlA, nn, lane, peers);
+    if (!have_rows) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      // ABLATE (timing diagnostics only, results invalid): the node's own row, coalesced
-      const uint32_t src = ABLATE ? x.node : peers[j];
-      in.w[j] = p.pref_in[src * p.BL + x.b];  // < N * BL < 2^31 (engine check); never neutral
+      for (int j = 0; j < K; ++j) rows[j] = (ABLATE ? x.node : peers[j]) * rb;
     }
+    // ABLATE (timing diagnostics only, results invalid): the node's own row, coalesced
+#pragma unroll
+    for (int j = 0; j < K; ++j) in.w[j] = at_byte(p.pref_in, rows[j] + bo);
   }
 }
 
@@ -427,6 +445,63 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   acc.emitted_bytes += emitted;
 }
 
+// Settled-tile fast path (kModeWarm, k = 8, klazy round, the wave's parked
+// draw): a tile whose vote register is uniform (kVUniform: V = A on every
+// polled record) and whose count planes are deferred with every live record
+// valid (kPendAllLive) is settled this round iff every polled record's 8
+// gathered votes equal its accepted bit. process_tile would then store only
+// the published words and the tile's pending count (+8 steps deferred once
+// more): no flip, no StatusUpdate, no deletion, V stays uniform, A and K
+// unchanged. This reads A, the validity word and the 8 votes and does exactly
+// that; any other tile returns false and takes the general load + step.
+template <int POL>
+__device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile, uint32_t lane, uint32_t kw,
+                                             const WaveDraw& wd, SweepAcc& acc) {
+  const uint32_t g = tile * 64u + lane;
+  const bool active = g < p.L;
+  const uint32_t gc = active ? g : p.L - 1u;
+  const uint32_t nl = div_bl(p, gc);
+  const uint32_t b = gc - nl * p.BL;
+  // A plane: SGPR tile base + the lane's constant byte offset
+  const char* const ta = reinterpret_cast<const char*>(p.planes + (size_t)tile * (kPlanes * 64u));
+  const uint32_t ao = (1536u + lane) * 4u;
+  const uint32_t A = POL > 0 ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(ta + ao))
+                             : *reinterpret_cast<const uint32_t*>(ta + ao);
+  const uint32_t P0 = active ? at_byte(p.valid, b * 4u) : 0u;  // polled = live (kPendAllLive) and valid
+  uint32_t rows[8];
+  pick_parked(p, wd.sd, wd.bad, (nl - wd.nlA) * 2u + (wd.pair ? 32u : 0u), p.n0 + nl, p.round, p.BL * 4u, rows);
+  const uint32_t bo = b * 4u;
+  uint32_t dis = 0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dis |= at_byte(p.pref_in, rows[j] + bo);
+  uint32_t all = ~0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) all &= at_byte(p.pref_in, rows[j] + bo);
+  // every vote equals A  <=>  (OR of votes) == A == (AND of votes) on P0
+  if (__ballot(((dis ^ A) | (all ^ A)) & P0) != 0ull) return false;
+  if (active) {
+    const uint32_t node = p.n0 + nl;
+    const uint32_t prow = node * p.BL + b;  // < N * BL < 2^30 (sweep gate)
+    const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
+    if (p.push_n) {  // peer-push exchange: as process_tile
+      const uint32_t old = p.pref_out[prow];
+      if (pub != old) {
+        for (uint32_t r = 0; r < p.push_n; ++r)
+          __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, 0x7FFFFFFF, kRsrcWord3);
+    st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
+  }
+  if (lane == 0) p.kpend[tile] = ((kw & 0xFFu) + 1u) | kPendAllLive;
+  acc.applied += 8u * (uint32_t)__popc(P0);
+  // process_tile's accounting for this case: 17 plane words + 8 vote words +
+  // valid read, minus V (uniform), V store (virtual), K read + store (deferred),
+  // A store (unchanged) = 40 B per lane (+ 4 B push read); kpend read + write
+  acc.lane_bytes += (active ? 40u + (p.push_n ? 4u : 0u) : 0u) + (lane == 0 ? 8u : 0u);
+  return true;
+}
+
 // MODE: kModeWarm (sim, every consider plane all-ones), kModeCheck (sim, per
 // tile: the oldest consider plane decides), kModeReplay (replayed votes),
 // kModeAblate (kModeCheck with the peer gather replaced by a coalesced read of
@@ -458,6 +533,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     wd.ok = false;
     wd.pair = false;
     wd.nlA = 0u;
+    wd.t0 = 0u;
+    wd.meta = 0u;
     wd.bad = 0ull;
     wd.sd = nullptr;
     if constexpr (MODE == kModeWarm && K == 8) {
@@ -471,9 +548,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           const uint32_t nlA = uni(div_bl(p, tile * 64u));
           const uint32_t nlB = uni(div_bl(p, min(tile_end * 64u, p.L) - 1u));
           const uint32_t nn = nlB - nlA + 1u;
-          bool any_stale = false;
-          if (p.vv)
-            for (uint32_t t = tile; t < tile_end; ++t) any_stale |= uni(p.vstale[t]) == kVStale;
+          // the run's per-tile words, one lane per tile (tpw <= 16)
+          const uint32_t ti = tile + lane;
+          const uint32_t st = p.vv && ti < tile_end ? p.vstale[ti] : 0u;
+          const uint32_t kw = (p.klazy || p.kconsume) && ti < tile_end ? p.kpend[ti] : 0u;
+          wd.meta = (st << 8) | (kw & (kPendAllLive | 0xFFu));
+          wd.t0 = tile;
+          const bool any_stale = __ballot(st == kVStale) != 0ull;
           __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][256];
           const PairDraw d = any_stale ? pair_draw(p, p.round, nlA, nn, lane) : single_draw(p, p.round, nlA, nn, lane);
           wd.nlA = nlA;
@@ -481,13 +562,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           wd.ok = !d.fallback;
           wd.bad = d.bad;
           wd.sd = s_draw[threadIdx.x >> 6];
-          if (wd.ok) park_draw(d, s_draw[threadIdx.x >> 6], lane);
+          if (wd.ok) park_draw(d, s_draw[threadIdx.x >> 6], lane, p.BL * 4u);
         }
       }
     }
     for (; tile < tile_end; tile += stride) {
       constexpr bool AB = MODE == kModeAblate;
       if constexpr (MODE == kModeWarm) {
+        if constexpr (K == 8) {
+          if (wd.ok && p.settled_fast && p.klazy && p.vv) {
+            const uint32_t m = meta_of(wd, tile);
+            if (((m >> 8) & 0xFFu) == kVUniform && (m & kPendAllLive) && settled_tile<POL>(p, tile, lane, m & 0x800000FFu, wd, acc))
+              continue;
+          }
+        }
         TileIn<K, false, true> in;
         load_tile<K, false, true, POL, false, true>(p, tile, lane, in, &wd);
         process_tile<K, false, true, POL, true>(p, tile, lane, in, 0u, acc);

@@ -52,6 +52,7 @@ for s in "$@"; do
     probe_grid) step probe_grid 600 bash -c 'for o in "sweep_blocks=0" "sweep_blocks=-2" "sweep_blocks=62500" "sweep_blocks=31250" "sweep_blocks=62500 --option sweep_nopipe=1" "sweep_blocks=31250 --option sweep_nopipe=1" "sweep_blocks=7168 --option sweep_nopipe=1"; do echo "== $o"; python tools/round_probe.py --workload c4 --option $o | tail -1; done' ;;
     probe_c3grid) step probe_c3grid 600 bash -c 'for o in "tiles_per_wave=1" "tiles_per_wave=2" "tiles_per_wave=4" "tiles_per_wave=8" "sweep_blocks=0"; do echo "== $o"; python tools/round_probe.py --workload c3 --option $o | tail -1; done' ;;
     probe_runs) step probe_runs 600 bash -c 'for w in c4 c3 c5; do for o in "wave_runs=0" "wave_runs=1"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
+    probe_fast) step probe_fast 600 bash -c 'for w in c4 c3 c5; do for o in "settled_fast=0" "settled_fast=1"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     newtests) step newtests 900 python -u -m pytest tests/test_gpu_example.py tests/test_gpu_dropin_fuzz.py tests/test_gpu_parity.py tests/test_gpu_delivery.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     dropin) step dropin 300 python tools/dropin_latency.py --json $OUT/dropin_latency.json ;;
     cpptests) step cpptests 300 go-avalanche_amd/bin/avalanche_gpu_tests ;;
