@@ -78,7 +78,10 @@ struct RoundParams {
   // [tiles] kVStale: the tile's V planes are stale, V = votes of round - 1
   // (regathered with round - 1's peers); kVUniform: the tile was settled (all
   // 8 votes of round - 1 equal the accepted bit of every polled record), so V
-  // = A on the polled records and nothing needs gathering; 0: V stored
+  // = A on the polled records and nothing needs gathering; 0: V stored.
+  // | kCAll: the tile's consider planes were left unstored by the fresh round
+  // (after 8 sim votes every consider bit of the tile is 1; no record of the
+  // tile is live-but-invalid) and read as all-ones until written back.
   uint32_t* vstale;
   const uint32_t* pref_prev; // [N_pad][BL] snapshot of round - 1 (read by stale tiles)
   // Peer-push exchange (node-sharded engines, k_round_sweep only):
@@ -126,7 +129,7 @@ struct RoundParams {
   uint32_t dense_min;  // a lane with >= dense_min updates logs one dense record (default dense_min(k))
 };
 constexpr uint32_t kPendAllLive = 0x80000000u;
-constexpr uint32_t kVStale = 1u, kVUniform = 2u;
+constexpr uint32_t kVStale = 1u, kVUniform = 2u, kVMask = 3u, kCAll = 4u;
 
 // Division by the (runtime) block count BL without a hardware divide:
 // Granlund-Montgomery round-up magic, exact for every 32-bit n.

@@ -453,7 +453,11 @@ __global__ __launch_bounds__(256) void k_read_records_v(const RoundParams p, uin
   const uint32_t g = nl * p.BL + b, tile = g >> 6;
   St s;
   load_state(p.planes, g, s);
-  const uint32_t st = p.vv ? p.vstale[tile] : 0u;
+  const uint32_t raw = p.vv ? p.vstale[tile] : 0u, st = raw & kVMask;
+  if (raw & kCAll) {  // consider planes left unstored by the fresh round: all-ones
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s.C[q] = ~0u;
+  }
   if (st == kVStale) {  // V_i = the vote of round - 1's slot 7 - i (k = 8)
     uint32_t pp[8];
     sample_peers<8>(p.seed, p.n0 + nl, p.round - 1u, p.n_nodes, p.peer_mode, pp);

@@ -55,7 +55,8 @@ template <int K, bool REPLAY, bool WARM>
 struct TileIn {
   u32x4 v0, v1, k0, k1;
   uint32_t A, vmask, byzw;
-  uint32_t stale;                // wave-uniform: V planes stale, v0/v1 regathered (kernels.h vstale)
+  uint32_t stale;                // wave-uniform: V planes stale, v0/v1 regathered (kernels.h vstale & kVMask)
+  uint32_t cflag;                // wave-uniform: vstale & kCAll (consider planes virtual, all-ones)
   uint32_t kw;                   // wave-uniform: kpend[tile] (kernels.h klazy); K planes not loaded if all-live
   uint32_t C[WARM ? 1 : 8];
   uint32_t w[K];                 // yes bits: err == 0 (vote.go:55)
@@ -108,7 +109,9 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
   const u32x4* const grp = reinterpret_cast<const u32x4*>(tp) + lane;
   constexpr bool VV = VVM && WARM && !REPLAY && K == 8;  // VVM: the warm sim modes only
   const bool meta = VV && wd && wd->t0 <= tile && tile - wd->t0 < 64u && p.tpw;
-  in.stale = VV && p.vv ? (meta ? (meta_of(*wd, tile) >> 8) & 0xFFu : uni(p.vstale[tile])) : 0u;
+  const uint32_t raw = VV && p.vv ? (meta ? (meta_of(*wd, tile) >> 8) & 0xFFu : uni(p.vstale[tile])) : 0u;
+  in.stale = raw & kVMask;
+  in.cflag = raw & kCAll;
   in.kw = 0u;
   if constexpr (FRESH) {
     // NewVoteRecords (vote.go:33-35): votes, consider and count all zero; K7
@@ -270,7 +273,10 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     st4<POL>(tr, grp, lane * 16u, o0);
     st4<POL>(tr, grp + 64, 1024u + lane * 16u, o1);
   }
-  if (!WARM && active) {  // consider planes (a fresh tile stores them even when its vote planes stay virtual)
+  // fresh round with virtual vote planes: every consider bit of the tile is 1
+  // after the 8 sim votes (C_i = P0 | dead0 with keep = 0): leave them unstored
+  const bool cvirt = virt && !WARM && !REPLAY && p.fresh;
+  if (!WARM && active && !cvirt) {  // consider planes
     const uint32_t dead0 = ~(P0 | keep);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -410,8 +416,8 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   if constexpr (VVM && !REPLAY && K == 8) {
     // a settled tile's 8 new votes all equal its accepted plane on the polled
     // records: its vote register is A next round (no regather)
-    const uint32_t nv = virt ? (settled ? kVUniform : kVStale) : 0u;
-    if (p.vv && lane == 0 && nv != in.stale) p.vstale[tile] = nv;
+    const uint32_t nv = (virt ? (settled ? kVUniform : kVStale) : 0u) | in.cflag | (cvirt ? kCAll : 0u);
+    if (p.vv && lane == 0 && nv != (in.stale | in.cflag)) p.vstale[tile] = nv;
   }
   if constexpr (KL) {
     if (klazy) {
@@ -439,7 +445,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   const uint32_t kbytes = (kunread && kdefer ? 32u : 0u) + (kdefer ? 32u : 0u);
   // V read: 32 B stored, 28 B regathered (stale), 0 B uniform
   acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale == kVStale ? 4u : in.stale == kVUniform ? 32u : 0u) -
-                                 (virt ? 32u : 0u) + (p.push_n ? 4u : 0u) -
+                                 (virt ? 32u : 0u) - (cvirt ? 32u : 0u) + (p.push_n ? 4u : 0u) -
                                  kbytes - (astore ? 0u : 4u)
                            : 0u;
   acc.emitted_bytes += emitted;
@@ -554,7 +560,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           const uint32_t kw = (p.klazy || p.kconsume) && ti < tile_end ? p.kpend[ti] : 0u;
           wd.meta = (st << 8) | (kw & (kPendAllLive | 0xFFu));
           wd.t0 = tile;
-          const bool any_stale = __ballot(st == kVStale) != 0ull;
+          const bool any_stale = __ballot((st & kVMask) == kVStale) != 0ull;
           __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][256];
           const PairDraw d = any_stale ? pair_draw(p, p.round, nlA, nn, lane) : single_draw(p, p.round, nlA, nn, lane);
           wd.nlA = nlA;
@@ -572,7 +578,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         if constexpr (K == 8) {
           if (wd.ok && p.settled_fast && p.klazy && p.vv) {
             const uint32_t m = meta_of(wd, tile);
-            if (((m >> 8) & 0xFFu) == kVUniform && (m & kPendAllLive) && settled_tile<POL>(p, tile, lane, m & 0x800000FFu, wd, acc))
+            if (((m >> 8) & kVMask) == kVUniform && (m & kPendAllLive) && settled_tile<POL>(p, tile, lane, m & 0x800000FFu, wd, acc))
               continue;
           }
         }
@@ -668,9 +674,21 @@ hipError_t launch_sweep_k(const RoundParams& p_in, bool replay, uint32_t blocks,
 __global__ __launch_bounds__(256) void k_vv_materialize(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t tile = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
-  const uint32_t st = tile < (p.Lpad >> 6) ? uni(p.vstale[tile]) : 0u;
-  if (st == 0u) return;
+  const uint32_t raw = tile < (p.Lpad >> 6) ? uni(p.vstale[tile]) : 0u;
+  if (raw == 0u) return;
+  const uint32_t st = raw & kVMask;
   const LaneIdx x = lane_idx(p, tile, lane);
+  if (raw & kCAll) {  // consider planes: all-ones
+    if (x.active) {
+      uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) tp[1024u + (uint32_t)i * 64u + lane] = ~0u;
+    }
+    if (st == 0u) {
+      if (lane == 0) p.vstale[tile] = 0u;
+      return;
+    }
+  }
   u32x4 o0, o1;
   if (st == kVUniform) {  // V_i = A on every polled record
     const uint32_t A = p.planes[(size_t)tile * (kPlanes * 64u) + 1536u + lane];

@@ -60,3 +60,48 @@ def test_fresh_and_kconsume_identical_to_stored_planes():
     for a, b in zip(off[:4], on[:4]):
         assert np.array_equal(np.asarray(a), np.asarray(b))
     assert on[4] < off[4]
+
+
+@pytest.mark.parametrize("path", ["set_valid", "register_votes", "replay", "write_records", "add_targets", "none"])
+def test_fresh_virtual_consider_writeback(oracle, path):
+    """The fresh round leaves the consider planes of its tiles unstored
+    (kernels.h kCAll: all-ones after 8 sim votes). Every operation that reads
+    or writes the planes right after it must see them as all-ones (write-back
+    in k_vv_materialize; k_read_records_v reads them virtually); the rounds
+    after it must match the oracle bit for bit."""
+    n, m, k, seed = 300, 1000, 8, 29
+    eng = avhip.Engine(n, m, k=k, seed=seed, log_capacity=1 << 22)
+    eng.init_records(avhip.INIT_BERNOULLI, P80)
+    sim = oracle.Sim(n, m, k, seed=seed, init_mode=avhip.INIT_BERNOULLI, init_param=P80)
+    rng = np.random.default_rng(seed)
+    eng.run_rounds(1)  # fresh
+    exp, _ = sim.run_round()
+    assert np.array_equal(eng.fetch_updates(), exp)
+    assert np.array_equal(eng.read_records(), sim.dump())  # virtual read of kCAll tiles
+    if path == "set_valid":
+        eng.set_valid(40, False)
+        sim.set_valid(40, False)
+    elif path == "register_votes":
+        node = 17
+        ts = rng.integers(0, m, size=64)
+        errs = rng.choice(np.array([0, 1, 0x80000000, 0x7FFFFFFF], np.uint32), 64)
+        st = eng.register_votes(node, ts, errs)
+        got = sim.register_votes(node, ts, errs)
+        assert [(int(t), int(s)) for t, s in zip(ts, st) if s >= 0] == got
+    elif path == "replay":
+        errs = rng.choice(np.array([0, 1, 0x80000000], np.uint32), size=(n, k, m)).astype(np.uint32)
+        eng.replay_round_errs(errs)
+        exp, _ = sim.run_round(replay_errs=errs)
+        assert np.array_equal(eng.fetch_updates(), exp)
+    elif path == "write_records":
+        eng.write_records(eng.read_records()[:50], n0=0, t0=0)
+    elif path == "add_targets":
+        assert not eng.add_targets(5, [7, 8], [True, False]).any()  # live records: no-op
+        assert not sim.add(5, 7, True) and not sim.add(5, 8, False)
+    assert np.array_equal(eng.read_records(), sim.dump()), path
+    for r in range(8):
+        eng.run_rounds(1)
+        exp, _ = sim.run_round()
+        assert np.array_equal(eng.fetch_updates(), exp), (path, r)
+    assert np.array_equal(eng.read_records(), sim.dump()), path
+    eng.close()

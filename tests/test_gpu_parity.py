@@ -340,10 +340,10 @@ def test_c4_shape_properties():
     digests = []
     # round 0: kernel 1 reads and writes all 25 planes (236 B per 32-record
     # lane); the sweep's fresh round reads only A and leaves the vote planes
-    # virtual (236 - 96 - 32 = 108 B). Warm bytes per lane over rounds 1-15:
+    # and consider planes virtual (236 - 96 - 32 - 32 = 76 B). Warm bytes per lane over rounds 1-15:
     # kernel 1 176 each; the sweep's depend on which tiles settled
     # (test_gpu_virtual_votes.py, test_gpu_count_lazy.py check them exactly)
-    for kernel, cold_bytes, warm_bytes in ((1, 236, 15 * 176), (2, 108, None)):
+    for kernel, cold_bytes, warm_bytes in ((1, 236, 15 * 176), (2, 76, None)):
         e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4)
         e.set_option("kernel", kernel)
         e.set_option("count_lazy", 0)  # per-lane bytes with stored count planes (test_gpu_count_lazy.py)
