@@ -424,6 +424,8 @@ def roofline(r, window=None, world=1):
                      "valu_issue": iss.get("frac_valu", 0.0), "salu_issue": iss.get("frac_salu", 0.0)}
             out["binding"] = max(cands, key=cands.get)
             out["binding_fracs"] = cands
+            # the resource closest to its peak in this window (PMC): HBM traffic or instruction issue
+            out["bound"] = "hbm" if out["binding"] == "hbm" else "issue"
         out["pmc_source"] = pmc.get("source")
     return out
 

@@ -102,6 +102,7 @@ struct av_engine {
   bool c_monotone = true;
   bool plane_nt = true;  // tuning option "plane_nt" (A/B on MI355X: -8 % kernel time warm, -16 % cold)
   bool ablate_gather = false;  // diagnostics option "ablate_gather" (invalid results)
+  bool ablate_emit = false;    // diagnostics option "ablate_emit" (StatusUpdates counted, not stored)
   // diagnostics option "unsynced_shard": a node-sharded engine runs rounds with no exchange (other
   // shards' preference rows keep their initial values; per-rank kernel timing only, invalid results)
   bool unsynced_shard = false;
@@ -241,6 +242,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.warm_skip = e->c_monotone ? 1u : 0u;
   p.plane_nt = e->plane_nt ? 1u : 0u;
   p.ablate_gather = e->ablate_gather ? 1u : 0u;
+  p.ablate_emit = e->ablate_emit ? 1u : 0u;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
   p.log_shards = e->log_shards;
@@ -794,6 +796,68 @@ int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uin
   return AV_OK;
 }
 
+namespace {
+// Batches of at least this many votes are grouped by lane on the device
+// (radix sort + run-length encode, log_ops.hip launch_group_votes) instead of
+// a host sort: the host sort of 32M (lane, vote) pairs took ~1 s.
+constexpr size_t kDeviceGroupVotes = 1u << 16;
+
+int register_votes_device(av_engine* e, const std::vector<std::pair<uint32_t, uint32_t>>& lv, const int64_t* targets,
+                          const uint32_t* errs, int64_t n, int32_t* status_out) {
+  const uint32_t m = (uint32_t)lv.size();
+  std::vector<uint32_t> host(3 * (size_t)m);  // keys | vote index | packed vote
+  for (uint32_t i = 0; i < m; ++i) {
+    const uint32_t v = lv[i].second;
+    const int64_t tl = targets[v] - e->t0;
+    const uint32_t err = errs[v];
+    host[i] = lv[i].first;
+    host[m + i] = v;
+    host[2 * (size_t)m + i] = (uint32_t)(tl & 31) | ((err == 0u ? 1u : 0u) << 5) | (((int32_t)err >= 0 ? 1u : 0u) << 6);
+  }
+  const uint64_t lanes_total = (uint64_t)e->NL * e->BL;
+  int key_bits = 1;
+  while (key_bits < 32 && (1ull << key_bits) < lanes_total) ++key_bits;
+  size_t tb = 0;
+  AV_HIP(avk::launch_group_votes(nullptr, &tb, nullptr, nullptr, nullptr, m, key_bits, nullptr, nullptr, nullptr, nullptr,
+                                 nullptr, nullptr, nullptr, nullptr, e->stream));
+  // keys vidx info keys_s perm perm_s lanes counts(m+1) offs(m+1) nruns entries(2m) status(n) temp
+  const size_t words = 7 * (size_t)m + 2 * ((size_t)m + 1) + 1 + 2 * (size_t)m + (size_t)n;
+  void* buf = nullptr;
+  int rc = engine_scratch(e, words * 4 + tb + 256, &buf);
+  if (rc != AV_OK) return rc;
+  auto* w = static_cast<uint32_t*>(buf);
+  uint32_t *keys = w, *vidx = keys + m, *info = vidx + m, *keys_s = info + m, *perm = keys_s + m, *perm_s = perm + m,
+           *lanes = perm_s + m, *counts = lanes + m, *offs = counts + m + 1, *nruns = offs + m + 1, *ent = nruns + 1;
+  auto* dstat = reinterpret_cast<int32_t*>(ent + 2 * (size_t)m);
+  void* temp = reinterpret_cast<void*>(((uintptr_t)(dstat + n) + 255) & ~(uintptr_t)255);
+  AV_HIP(hipMemcpyAsync(keys, host.data(), host.size() * 4, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(avk::launch_group_votes(temp, &tb, keys, vidx, info, m, key_bits, keys_s, perm, perm_s, lanes, counts, offs,
+                                 nruns, ent, e->stream));
+  AV_HIP(hipMemsetAsync(dstat, 0xFF, (size_t)n * 4, e->stream));
+  uint32_t nb = 0;
+  AV_HIP(hipMemcpyAsync(&nb, nruns, 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  avk::DropInParams p{};
+  p.planes = e->planes;
+  p.pref = e->pref[e->cur];
+  p.valid = e->valid;
+  p.byz = e->byz;
+  p.blocks = lanes;
+  p.offs = offs;
+  p.entries = ent;
+  p.status_out = dstat;
+  p.n_blocks = nb;
+  p.n0 = (uint32_t)e->n0;
+  p.BL = e->BL;
+  p.round = (uint32_t)e->round;
+  p.pub_mode = (uint32_t)e->pub_mode;
+  AV_HIP(avk::launch_register_votes(p, e->stream));
+  AV_HIP(hipMemcpyAsync(status_out, dstat, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return AV_OK;
+}
+}  // namespace
+
 int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const uint32_t* errs, int64_t n,
                       int32_t* status_out) {
   const int64_t offs[2] = {0, n};
@@ -854,6 +918,7 @@ int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, 
   }
   e->count_bound = (int)std::min<int64_t>(127, e->count_bound + max_node_votes);
   if (lv.empty()) return AV_OK;
+  if (lv.size() >= kDeviceGroupVotes) return register_votes_device(e, lv, targets, errs, n, status_out);
   std::sort(lv.begin(), lv.end());
   std::vector<uint32_t> lanes, offs, entries(2 * lv.size());
   for (size_t i = 0; i < lv.size(); ++i) {
@@ -1438,6 +1503,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   const std::string n(name);
   if (n == "plane_nt") {
     e->plane_nt = value != 0;
+  } else if (n == "ablate_emit") {
+    e->ablate_emit = value != 0;
   } else if (n == "ablate_gather") {
     e->ablate_gather = value != 0;
   } else if (n == "kernel") {  // 2 = k_round_sweep (default where it applies), 1 = k_round_fast

@@ -66,6 +66,7 @@ struct RoundParams {
   uint32_t warm_skip;        // consider planes are monotone (sim votes only): skip all-ones planes
   uint32_t plane_nt;         // stream state planes with non-temporal loads/stores
   uint32_t ablate_gather;    // diagnostics only: gather the node's own row (wrong results)
+  uint32_t ablate_emit;      // diagnostics only: count StatusUpdates, store none (log left empty)
   // k_round_sweep only
   uint32_t warm_all;         // every consider plane of every lane is all-ones (no per-tile check)
   uint32_t store_policy;     // 0/1: per plane_nt; 2: sc1 plane/pref stores; 3: nt sc1 (k = 8)
@@ -252,6 +253,10 @@ hipError_t launch_dense_expand(const uint64_t* recs, uint64_t n, uint32_t k, uin
 // nullptr: size query).
 hipError_t launch_sort_updates(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
                                int begin_bit, int end_bit, hipStream_t s);
+hipError_t launch_group_votes(void* temp, size_t* temp_bytes, const uint32_t* keys, const uint32_t* vidx,
+                              const uint32_t* info, uint32_t n, int key_bits, uint32_t* keys_s, uint32_t* perm,
+                              uint32_t* perm_s, uint32_t* lanes, uint32_t* counts, uint32_t* offs, uint32_t* n_runs,
+                              uint32_t* entries, hipStream_t s);
 
 hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0,
                                 uint32_t tl1, const uint32_t* in, hipStream_t s);

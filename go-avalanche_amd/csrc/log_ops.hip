@@ -14,6 +14,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "kernels.h"
 #include "round_common.h"
 
@@ -156,6 +158,58 @@ hipError_t launch_dense_expand(const uint64_t* recs, uint64_t n, uint32_t k, uin
 hipError_t launch_sort_updates(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
                                int begin_bit, int end_bit, hipStream_t s) {
   return hipcub::DeviceRadixSort::SortKeys(temp, *temp_bytes, in, out, n, begin_bit, end_bit, s);
+}
+
+namespace {
+__global__ __launch_bounds__(256) void k_iota(uint32_t* out, uint32_t n) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i < n) out[i] = i;
+}
+// entries[2i] = vote index, entries[2i+1] = packed vote (k_register_votes)
+__global__ __launch_bounds__(256) void k_vote_entries(const uint32_t* perm, const uint32_t* vidx, const uint32_t* info,
+                                                      uint32_t n, uint32_t* entries) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t j = perm[i];
+  entries[2u * i] = vidx[j];
+  entries[2u * i + 1u] = info[j];
+}
+}  // namespace
+
+// Drop-in RegisterVotes batch (engine.cpp av_register_votes_batch): group the
+// votes by lane (node, 32-target block) keeping their order inside a lane —
+// a stable radix sort of (lane, position) pairs — then run-length encode the
+// sorted lanes into the (lanes, offs) CSR k_register_votes walks. temp ==
+// nullptr: *temp_bytes = the scratch the three hipcub passes need.
+hipError_t launch_group_votes(void* temp, size_t* temp_bytes, const uint32_t* keys, const uint32_t* vidx,
+                              const uint32_t* info, uint32_t n, int key_bits, uint32_t* keys_s, uint32_t* perm,
+                              uint32_t* perm_s, uint32_t* lanes, uint32_t* counts, uint32_t* offs, uint32_t* n_runs,
+                              uint32_t* entries, hipStream_t s) {
+  size_t b_sort = 0, b_rle = 0, b_scan = 0;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, b_sort, keys, keys_s, perm, perm_s, n, 0, key_bits, s);
+  if (e == hipSuccess) e = hipcub::DeviceRunLengthEncode::Encode(nullptr, b_rle, keys_s, lanes, counts, n_runs, n, s);
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, b_scan, counts, offs, n + 1u, s);
+  if (e != hipSuccess) return e;
+  const size_t need = std::max(b_sort, std::max(b_rle, b_scan));
+  if (!temp) {
+    *temp_bytes = need;
+    return hipSuccess;
+  }
+  if (*temp_bytes < need) return hipErrorInvalidValue;
+  const uint32_t g = (n + 255u) / 256u;
+  hipLaunchKernelGGL(k_iota, dim3(g), dim3(256), 0, s, perm, n);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  size_t t = need;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(temp, t, keys, keys_s, perm, perm_s, n, 0, key_bits, s)) != hipSuccess) return e;
+  // counts has n + 1 slots: the runs' counts, then zeros, so that the scan's
+  // entry n_runs is the total (offs[n_runs] = n)
+  if ((e = hipMemsetAsync(counts, 0, (size_t)(n + 1u) * 4, s)) != hipSuccess) return e;
+  t = need;
+  if ((e = hipcub::DeviceRunLengthEncode::Encode(temp, t, keys_s, lanes, counts, n_runs, n, s)) != hipSuccess) return e;
+  t = need;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(temp, t, counts, offs, n + 1u, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_vote_entries, dim3(g), dim3(256), 0, s, perm_s, vidx, info, n, entries);
+  return hipGetLastError();
 }
 
 }  // namespace avk

@@ -334,6 +334,7 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
   const uint32_t tot_u = wave_sum(cnt), tot_s = wave_sum(dense ? 0u : cnt);
   const uint32_t tot_d = (uint32_t)__popcll(dl);
   updates += tot_u;
+  if (p.ablate_emit) return 0u;  // diagnostics: the cost of the round without its log stores
   const uint32_t shard = wave_id % p.log_shards;
   uint32_t base = 0, dbase = 0;
   if (lane == 0) {

@@ -240,7 +240,14 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  *                    which re-adds a queried target it does not hold as
  *                    accepted and answers yes (main.go:175-182; unsharded
  *                    engines, M <= 4096). 1 and 2 run the first-generation
- *                    kernel. */
+ *                    kernel.
+ * Sweep-kernel tuning and A/B switches (defaults are the measured best;
+ * DESIGN.md §3-4): "tiles_per_wave" (4), "wave_runs" (1: a wave takes a run
+ * of consecutive tiles and draws their peers once), "settled_fast" (1),
+ * "sweep_nopipe" (1), "virtual_votes" (1), "vv_min_bl" (16), "count_lazy"
+ * (1), "fresh" (1), "dense_min" (6 at k = 8: updates per lane that make a
+ * dense log record). Diagnostics that make results invalid: "ablate_gather",
+ * "ablate_emit" (StatusUpdates counted, not stored), "unsynced_shard". */
 int av_set_option(av_engine* e, const char* name, int64_t value);
 
 /* ---- measurement ---- */

@@ -121,3 +121,39 @@ def test_register_votes_batch_vs_oracle(oracle, seed):
             have = [(int(targets[v]), int(got[v])) for v in range(a, b) if got[v] >= 0]
             assert have == exp, (batch, i)
         check(eng, sim, f"batch {batch}")
+
+
+def test_register_votes_batch_device_grouping(oracle):
+    """Batches of >= 65536 votes are grouped by lane on the device (radix sort
+    of (lane, position) + run-length encode, log_ops.hip launch_group_votes):
+    the same statuses and records as the oracle's RegisterVotes per Response,
+    with nodes repeated across the batch (their Responses apply in order)."""
+    rng = np.random.default_rng(77)
+    n, m = 300, 700
+    eng = avhip.Engine(n, m, k=8, seed=77)
+    eng.init_records(avhip.INIT_BERNOULLI, int(0.6 * 2**32))
+    sim = oracle.Sim(n, m, 8, seed=77, init_mode=3, init_param=int(0.6 * 2**32))
+    eng.set_valid(11, False)
+    sim.set_valid(11, False)
+    for _ in range(14):
+        eng.run_rounds(1)
+        sim.run_round()
+    eng.discard_updates()
+    for batch in range(2):
+        n_resp = 900
+        nodes = rng.integers(0, n, size=n_resp)
+        sizes = rng.integers(0, 200, size=n_resp)
+        offsets = np.concatenate([[0], np.cumsum(sizes)])
+        assert offsets[-1] >= 1 << 16
+        targets = rng.integers(-3, m + 3, size=int(offsets[-1]))
+        errs = rng.choice(ERRS, size=targets.size)
+        got = eng.register_votes_batch(nodes, offsets, targets, errs)
+        for i in range(n_resp):
+            a, b = int(offsets[i]), int(offsets[i + 1])
+            exp = sim.register_votes(int(nodes[i]), targets[a:b], errs[a:b])
+            have = [(int(targets[v]), int(got[v])) for v in range(a, b) if got[v] >= 0]
+            assert have == exp, (batch, i)
+        check(eng, sim, f"device batch {batch}")
+        eng.run_rounds(1)
+        exp_u, _ = sim.run_round()
+        assert np.array_equal(eng.fetch_updates(), exp_u)

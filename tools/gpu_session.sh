@@ -46,6 +46,7 @@ for s in "$@"; do
     capped) step capped 600 python -u -m pytest tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "capped or c2 or replay or fuzz or poll_sets" ;;
     fresh) step fresh 600 python -u -m pytest tests/test_gpu_fresh.py tests/test_gpu_count_lazy.py tests/test_gpu_virtual_votes.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     probe_c4) step probe_c4 300 python tools/round_probe.py --workload c4 --json $OUT/probe_c4.json ;;
+    probe_emit) step probe_emit 300 python tools/round_probe.py --workload c4 --option ablate_emit=1 --json $OUT/probe_c4_noemit.json ;;
     probe_c3) step probe_c3 300 python tools/round_probe.py --workload c3 --json $OUT/probe_c3.json ;;
     sq_c4a) step sq_c4a 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/sq_c4a -o probe -- \
             python3 tools/round_probe.py --workload c4 --warm-epochs 0 ;;
@@ -78,6 +79,14 @@ for s in "$@"; do
     bench_c5) step bench_c5 900 python bench.py --workload c5 --no-cpu-baseline ;;
     prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- \
             python3 bench.py --no-cpu-baseline ;;
+    pmcb_sq) step pmcb_sq_${WL:-c4} 600 timeout -s KILL 500 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+            --output-format csv -d $OUT/pmcb_sq_${WL:-c4} -o bench -- python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary ;;
+    pmcb_fetch) step pmcb_fetch_${WL:-c4} 600 timeout -s KILL 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmcb_fetch_${WL:-c4} -o bench -- \
+            python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary ;;
+    pmcb_write) step pmcb_write_${WL:-c4} 600 timeout -s KILL 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmcb_write_${WL:-c4} -o bench -- \
+            python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary ;;
+    pmcb_sum) step pmcb_sum_${WL:-c4} 300 python tools/pmc_bench.py --workload ${WL:-c4} --sq $OUT/pmcb_sq_${WL:-c4} --fetch $OUT/pmcb_fetch_${WL:-c4} \
+            --write $OUT/pmcb_write_${WL:-c4} --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write --out $OUT/pmc_${WL:-c4}.json ;;
     pmc_fetch) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o bench -- \
             python3 bench.py --no-cpu-baseline --no-secondary ;;
     pmc_write) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o bench -- \
