@@ -27,6 +27,8 @@ __device__ __forceinline__ void philox(uint32_t x[4], uint64_t seed, uint32_t a,
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   // opaque key: the 20-word key schedule is recomputed (SALU) per call instead
   // of being hoisted out of the tile loop into 20 live SGPRs (spills)
+  k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);  // the seed is uniform: keep it scalar
+  k1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
   asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -334,10 +336,13 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
   const uint32_t tot_u = wave_sum(cnt), tot_s = wave_sum(dense ? 0u : cnt);
   const uint32_t tot_d = (uint32_t)__popcll(dl);
   updates += tot_u;
-  if (p.ablate_emit) return 0u;  // diagnostics: the cost of the round without its log stores
+  if (p.ablate_emit == 1u) return 0u;  // diagnostics: the cost of the round without its log stores
   const uint32_t shard = wave_id % p.log_shards;
   uint32_t base = 0, dbase = 0;
-  if (lane == 0) {
+  if (p.ablate_emit == 2u) {  // diagnostics: stores at made-up positions, no reserving atomic (log invalid)
+    base = p.log_cap > 8192u ? (wave_id * 509u) % (p.log_cap - 4096u) : 0u;
+    dbase = p.dlog_cap > 128u ? (wave_id * 131u) % (p.dlog_cap - 64u) : 0u;
+  } else if (lane == 0) {
     if (tot_s) base = atomicAdd(&p.log_count[shard], tot_s);
     if (tot_d) dbase = atomicAdd(&p.dlog_count[shard], tot_d);
   }

@@ -47,9 +47,14 @@ for s in "$@"; do
     fresh) step fresh 600 python -u -m pytest tests/test_gpu_fresh.py tests/test_gpu_count_lazy.py tests/test_gpu_virtual_votes.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     probe_c4) step probe_c4 300 python tools/round_probe.py --workload c4 --json $OUT/probe_c4.json ;;
     probe_emit) step probe_emit 300 python tools/round_probe.py --workload c4 --option ablate_emit=1 --json $OUT/probe_c4_noemit.json ;;
+    probe_noatomic) step probe_noatomic 300 python tools/round_probe.py --workload c4 --option ablate_emit=2 --json $OUT/probe_c4_noatomic.json ;;
     probe_c3) step probe_c3 300 python tools/round_probe.py --workload c3 --json $OUT/probe_c3.json ;;
     sq_c4a) step sq_c4a 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/sq_c4a -o probe -- \
             python3 tools/round_probe.py --workload c4 --warm-epochs 0 ;;
+    sq_c4a_noemit) step sq_c4a_noemit 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/sq_c4a_noemit -o probe -- \
+            python3 tools/round_probe.py --workload c4 --warm-epochs 0 --option ablate_emit=1 ;;
+    sq_c4b_noemit) step sq_c4b_noemit 300 timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq_c4b_noemit -o probe -- \
+            python3 tools/round_probe.py --workload c4 --warm-epochs 0 --option ablate_emit=1 ;;
     sq_c4b) step sq_c4b 300 timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq_c4b -o probe -- \
             python3 tools/round_probe.py --workload c4 --warm-epochs 0 ;;
     probe_grid) step probe_grid 600 bash -c 'for o in "sweep_blocks=0" "sweep_blocks=-2" "sweep_blocks=62500" "sweep_blocks=31250" "sweep_blocks=62500 --option sweep_nopipe=1" "sweep_blocks=31250 --option sweep_nopipe=1" "sweep_blocks=7168 --option sweep_nopipe=1"; do echo "== $o"; python tools/round_probe.py --workload c4 --option $o | tail -1; done' ;;
