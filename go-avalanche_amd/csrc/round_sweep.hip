@@ -289,18 +289,52 @@ __device__ __forceinline__ uint32_t emit_updates_lds(const RoundParams& p, uint3
       // this lane's singles at its exclusive prefix, then one contiguous copy
       uint64_t* const s64 = reinterpret_cast<uint64_t*>(es);
       uint32_t pos = incl - scnt;
-      uint32_t par = 0;
+      if constexpr (K == 8) {
+        // one update per lane per iteration (emit_updates_flat)
+        uint32_t seen = 0u, T = 0u, nz = 0u;
 #pragma unroll
-      for (int j = K - 1; j >= 0; --j) {  // A after slot j = A_final ^ parity(later flips)
-        const uint32_t Aj = A_final ^ par;
-        par ^= E[j];
-        uint32_t e = dense ? 0u : E[j];
-        while (e) {
-          const uint32_t bit = (uint32_t)__ffs(e) - 1u;
-          e &= e - 1u;
-          const uint32_t a = (Aj >> bit) & 1u;
-          const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
-          s64[pos++] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
+        for (int j = 0; j < K; ++j) {
+          T |= seen & E[j];
+          seen |= E[j];
+          nz |= (E[j] != 0u ? 1u : 0u) << j;
+        }
+        if (dense) nz = 0u;
+        uint32_t S = 0u, j = 0u, cur = 0u;
+        const uint64_t hi = ((uint64_t)p.round_rel << 52) | ((uint64_t)node << 28);
+        for (uint32_t r = 0; r < 64u; ++r) {
+          const bool more = r < scnt;
+          if (__ballot(more) == 0ull) break;
+          if (more) {
+            if (cur == 0u) {
+              j = (uint32_t)__ffs(nz) - 1u;
+              nz &= nz - 1u;
+              cur = E[0];
+#pragma unroll
+              for (int q = 1; q < K; ++q) cur = j == (uint32_t)q ? E[q] : cur;
+            }
+            const uint32_t bit = (uint32_t)__ffs(cur) - 1u;
+            cur &= cur - 1u;
+            const uint32_t m = 1u << bit;
+            const uint32_t a = ((A_final ^ (T & ~S)) >> bit) & 1u;
+            S |= m;
+            const uint32_t st = (died & m) ? (a ? 3u : 0u) : (a ? 2u : 1u);
+            s64[pos++] = hi | ((uint64_t)j << 24) | ((uint64_t)(tbase + bit) << 2) | st;
+          }
+        }
+      } else {
+        uint32_t par = 0;
+#pragma unroll
+        for (int j = K - 1; j >= 0; --j) {  // A after slot j = A_final ^ parity(later flips)
+          const uint32_t Aj = A_final ^ par;
+          par ^= E[j];
+          uint32_t e = dense ? 0u : E[j];
+          while (e) {
+            const uint32_t bit = (uint32_t)__ffs(e) - 1u;
+            e &= e - 1u;
+            const uint32_t a = (Aj >> bit) & 1u;
+            const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
+            s64[pos++] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
+          }
         }
       }
       wave_lds_sync();

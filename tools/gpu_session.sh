@@ -48,6 +48,7 @@ for s in "$@"; do
     probe_c4) step probe_c4 300 python tools/round_probe.py --workload c4 --json $OUT/probe_c4.json ;;
     probe_emit) step probe_emit 300 python tools/round_probe.py --workload c4 --option ablate_emit=1 --json $OUT/probe_c4_noemit.json ;;
     probe_noatomic) step probe_noatomic 300 python tools/round_probe.py --workload c4 --option ablate_emit=2 --json $OUT/probe_c4_noatomic.json ;;
+    delivery) step delivery 600 python tools/delivery_probe.py --json $OUT/delivery_c4.json ;;
     probe_c3) step probe_c3 300 python tools/round_probe.py --workload c3 --json $OUT/probe_c3.json ;;
     sq_c4a) step sq_c4a 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $OUT/sq_c4a -o probe -- \
             python3 tools/round_probe.py --workload c4 --warm-epochs 0 ;;
