@@ -102,6 +102,7 @@ struct av_engine {
   bool c_monotone = true;
   bool plane_nt = true;  // tuning option "plane_nt" (A/B on MI355X: -8 % kernel time warm, -16 % cold)
   bool ablate_gather = false;  // diagnostics option "ablate_gather" (invalid results)
+  uint32_t ablate_node = 0;  // diagnostics option "ablate_node" (k_round_node, invalid results)
   int ablate_emit = 0;  // diagnostics option "ablate_emit": 1 = StatusUpdates counted, not stored; 2 = no reserving atomic
   // diagnostics option "unsynced_shard": a node-sharded engine runs rounds with no exchange (other
   // shards' preference rows keep their initial values; per-rank kernel timing only, invalid results)
@@ -243,6 +244,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.plane_nt = e->plane_nt ? 1u : 0u;
   p.ablate_gather = e->ablate_gather ? 1u : 0u;
   p.ablate_emit = (uint32_t)e->ablate_emit;
+  p.ablate_node = e->ablate_node;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
   p.log_shards = e->log_shards;
@@ -1505,6 +1507,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->plane_nt = value != 0;
   } else if (n == "ablate_emit") {
     e->ablate_emit = (int)std::max<int64_t>(0, std::min<int64_t>(2, value));
+  } else if (n == "ablate_node") {
+    e->ablate_node = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(7, value));
   } else if (n == "ablate_gather") {
     e->ablate_gather = value != 0;
   } else if (n == "kernel") {  // 2 = k_round_sweep (default where it applies), 1 = k_round_fast

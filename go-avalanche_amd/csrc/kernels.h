@@ -67,6 +67,8 @@ struct RoundParams {
   uint32_t plane_nt;         // stream state planes with non-temporal loads/stores
   uint32_t ablate_gather;    // diagnostics only: gather the node's own row (wrong results)
   uint32_t ablate_emit;      // diagnostics only: count StatusUpdates, store none (log left empty)
+  uint32_t ablate_node;      // diagnostics only (k_round_node, wrong results): 1 = only the lanes below the
+                             // cap run, 2 = no replay loads, 4 = no plane stores
   // k_round_sweep only
   uint32_t warm_all;         // every consider plane of every lane is all-ones (no per-tile check)
   uint32_t store_policy;     // 0/1: per plane_nt; 2: sc1 plane/pref stores; 3: nt sc1 (k = 8)

@@ -70,6 +70,14 @@ __device__ __forceinline__ void node_lane_load(const RoundParams& p, uint32_t* t
 #pragma unroll
   for (int i = 0; i < 8; ++i) in.C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
   if constexpr (REPLAY) {
+    if (p.ablate_node & 2u) {  // diagnostics: no replay loads
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        in.cw[j] = ~(g * 0x9E3779B9u + (uint32_t)j);
+        in.w[j] = g * 0x85EBCA6Bu ^ (uint32_t)j;
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       in.cw[j] = p.replay[(size_t)(2 * j + 1) * p.Lpad + g];
@@ -165,7 +173,8 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
   // their registers are free during it). A lane with no polled record keeps
   // its planes: no stores.
   const bool any = polled != 0u;
-  if (active && any) {
+  const bool st = !(p.ablate_node & 4u);  // diagnostics: no plane stores
+  if (active && any && st) {
     u32x4 o0, o1;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -199,7 +208,7 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
   }
 
   if (active) {
-    if (any) {
+    if (any && st) {
       u32x4 o2, o3;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -240,7 +249,8 @@ hipError_t launch_node_t(const RoundParams& p, bool replay, uint32_t bt, hipStre
 // (M <= 16384) leaves the register allocator room (no scratch)
 template <int K>
 hipError_t launch_node_k(const RoundParams& p, bool replay, hipStream_t s) {
-  const uint32_t bt = ((p.BL + 63u) / 64u) * 64u;
+  uint32_t bt = ((p.BL + 63u) / 64u) * 64u;
+  if ((p.ablate_node & 1u) && bt > kMaxPoll / 32u) bt = kMaxPoll / 32u;  // diagnostics: lanes past the cap never run
   return bt <= 512u ? launch_node_t<K, 512>(p, replay, bt, s) : launch_node_t<K, 1024>(p, replay, bt, s);
 }
 

@@ -28,7 +28,7 @@ step() {  # name, timeout-seconds, command...
 for s in "$@"; do
   case $s in
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step pytest_gpu 1500 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    tests) step pytest_gpu 1080 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testsnew) step pytest_new 1200 python -u -m pytest tests/test_gpu_delivery.py tests/test_gpu_fullsize.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py ;;
@@ -123,6 +123,9 @@ for s in "$@"; do
     gaps2) step gaps2 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps2 -o gap -- python3 tools/gap_probe.py --workload c2 ;;
     profc2) step profc2 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc2 -o c2 -- \
             python3 bench.py --workload c2 --no-cpu-baseline ;;
+    probe_c2abl) step probe_c2abl 600 bash -c 'for o in "ablate_node=0" "ablate_node=1" "ablate_node=2" "ablate_node=4" "ablate_node=7" "ablate_emit=1" "ablate_emit=1 --option ablate_node=7"; do echo "== $o"; python tools/round_probe.py --workload c2 --option $o | tail -2; done' ;;
+    profc2p) step profc2p 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc2p -o c2 -- \
+            python3 tools/round_probe.py --workload c2 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
