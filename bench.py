@@ -348,8 +348,13 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         applied_all, emitted_all = applied, emitted
     kavg_ms = kern_ms / launches if launches else None
     gen2 = k <= 8 and args.kernel != 1
-    kname = (("k_round_node" if gen2 else "k_round_capped") if info["capped"]
-             else ("k_round_sweep" if gen2 else "k_round_fast")) + f"<{k},{'true' if replay else 'false'}>"
+    if info["capped"] and replay and gen2:
+        # consecutive replay rounds fused per launch (engine option replay_fuse, default 16): one
+        # launch covers a timed segment's rounds, so kernel_ms_avg is per launch, not per round
+        kname = f"k_replay_node<{k}> (+ k_round_capped exact pass)"
+    else:
+        kname = (("k_round_node" if gen2 else "k_round_capped") if info["capped"]
+                 else ("k_round_sweep" if gen2 else "k_round_fast")) + f"<{k},{'true' if replay else 'false'}>"
     # SURVEY.md §8(d) bytes of this rank's launches in the roofline pass: every
     # applied vote is one live (node, target, round) triple / k; + 20 B per
     # emitted StatusUpdate
@@ -359,6 +364,7 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         "emitted": emitted_all, "value": applied_all / elapsed, "segments": segs, "info": info,
         "kavg_ms": kavg_ms, "launches": launches, "s8d_bytes": s8d,
         "moved_bytes": moved / launches if launches else None, "kernel": kname, "replicas_identical": replicas,
+        "rounds_per_launch": steps / launches if launches else None,
         "first_round": warmup % EPOCH,
     }
 
@@ -409,7 +415,7 @@ def roofline(r, window=None, world=1):
     ach = r["s8d_bytes"] / t / 1e9
     out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
            "traffic": None, "kernel": r["kernel"], "kernel_ms_avg": r["kavg_ms"], "launches": r["launches"],
-           "alg_bytes_s8d": r["s8d_bytes"],
+           "alg_bytes_s8d": r["s8d_bytes"], "rounds_per_launch": r["rounds_per_launch"],
            "bytes_moved": r["moved_bytes"], "frac_moved": r["moved_bytes"] / t / 1e9 / HBM_PEAK_GBS,
            "note": "achieved = SURVEY.md §8(d) bytes (9.125 B per live node-target-round + 20 B per "
                    "StatusUpdate) / kernel time; the bit-sliced kernel moves bytes_moved instead (DESIGN.md §3)"}

@@ -137,6 +137,7 @@ struct av_engine {
   // replay stream
   uint32_t* replay = nullptr;
   int64_t replay_cap_rounds = 0, replay_first = 0, replay_ready = 0;
+  int replay_fuse = 16;  // option "replay_fuse": replay rounds per k_replay_node launch (capped engines; <= 1: off)
   // timing
   bool timing = false;
   bool round_marker = false;  // option "round_marker" (diagnostics)
@@ -182,7 +183,7 @@ struct av_engine {
   size_t fetch_scratch_bytes = 0;
   unsigned long long* digest = nullptr;  // [3]
 
-  size_t round_replay_words() const { return (size_t)k * 2 * Lpad; }
+  size_t round_replay_words() const { return avk::replay_words(Lpad, k); }
 };
 
 namespace {
@@ -478,6 +479,51 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   }
   e->cur = av_engine::nxt(e->cur);
   e->round++;
+  return AV_OK;
+}
+
+// Replay rounds [round, round + R) of a capped engine in one k_replay_node
+// launch, followed per round by the exact pass over the nodes it left at that
+// round (count >= 120). Host-side round bookkeeping as launch_one_round.
+int launch_replay_fused(av_engine* e, const uint32_t* replay0, int32_t R) {
+  AV_CHECK(e->round + R - 1 - e->log_base < 4096, AV_ERR_OVERFLOW,
+           "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
+  int rc = materialize_votes_only(e);
+  if (rc != AV_OK) return rc;
+  rc = materialize_counts(e);
+  if (rc != AV_OK) return rc;
+  const size_t per = e->round_replay_words();
+  avk::RoundParams p = round_params(e, replay0);
+  p.node_flags = e->node_flags;
+  p.fuse_rounds = (uint32_t)R;
+  p.replay_stride = per;
+  p.ring_next = (uint32_t)av_engine::nxt(e->cur);
+  for (int i = 0; i < 3; ++i) p.pref_ring[i] = e->pref[i];
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (e->timing) {
+    AV_HIP(hipEventCreate(&ev0));
+    AV_HIP(hipEventCreate(&ev1));
+    AV_HIP(hipEventRecord(ev0, e->stream));
+  }
+  AV_HIP(avk::launch_replay_node(p, e->k, e->stream));
+  for (int32_t r = 0; r < R; ++r) {
+    if (e->count_bound >= 120) {  // a node may have reached count 120 by this round
+      avk::RoundParams q = round_params(e, replay0 + per * (size_t)r);
+      q.node_flags = e->node_flags;
+      q.exact_rel = (uint32_t)r;
+      q.exact_keep = r + 1 < R ? 1u : 0u;
+      AV_HIP(avk::launch_round(q, e->k, /*replay=*/true, /*capped=*/true, e->stream));
+    }
+    e->count_bound = std::min(127, e->count_bound + e->k);
+    e->fresh = false;
+    e->warm_all = false;
+    e->cur = av_engine::nxt(e->cur);
+    e->round++;
+  }
+  if (e->timing) {
+    AV_HIP(hipEventRecord(ev1, e->stream));
+    e->events.emplace_back(ev0, ev1);
+  }
   return AV_OK;
 }
 
@@ -1126,8 +1172,8 @@ int av_replay_round_errs(av_engine* e, const uint32_t* errs) {
           c |= ((int32_t)err >= 0 ? 1u : 0u) << i;     // vote.go:56
         }
         const size_t g = (size_t)nl * e->BL + b;
-        planes[(size_t)(2 * s) * e->Lpad + g] = y;
-        planes[(size_t)(2 * s + 1) * e->Lpad + g] = c;
+        planes[avk::replay_idx((uint32_t)g, e->k, s, 0)] = y;
+        planes[avk::replay_idx((uint32_t)g, e->k, s, 1)] = c;
       }
     }
   Scratch s;
@@ -1169,9 +1215,16 @@ int av_replay_rounds(av_engine* e, int32_t rounds) {
            AV_ERR_INVALID_ARG, "replay stream not prepared for these rounds");
   if (rounds > 0) e->c_monotone = false;
   const size_t per = e->round_replay_words();
-  for (int32_t r = 0; r < rounds; ++r) {
-    int rc = launch_one_round(e, e->replay + per * (size_t)(e->round - e->replay_first));
+  // capped engines (poll cap binds) fuse consecutive replay rounds: every node's
+  // records depend only on its own stream (k_replay_node)
+  const bool fuse = e->replay_fuse > 1 && e->kernel == 2 && e->k <= 8 && e->capped && e->pub_mode == 0 &&
+                    !e->any_nopoll && e->peer_world <= 1 && !e->comm && e->NL == (uint32_t)e->N;
+  for (int32_t r = 0; r < rounds;) {
+    const uint32_t* rp = e->replay + per * (size_t)(e->round - e->replay_first);
+    const int32_t n = fuse ? std::min<int32_t>(rounds - r, e->replay_fuse) : 1;
+    int rc = n > 1 ? launch_replay_fused(e, rp, n) : launch_one_round(e, rp);
     if (rc != AV_OK) return rc;
+    r += n;
   }
   return AV_OK;
 }
@@ -1507,6 +1560,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->plane_nt = value != 0;
   } else if (n == "ablate_emit") {
     e->ablate_emit = (int)std::max<int64_t>(0, std::min<int64_t>(2, value));
+  } else if (n == "replay_fuse") {  // replay rounds per fused launch on capped engines (<= 1: one launch per round)
+    AV_CHECK(value >= 0 && value <= 4096, AV_ERR_INVALID_ARG, "replay_fuse must be in [0, 4096]");
+    e->replay_fuse = (int)value;
   } else if (n == "ablate_node") {
     e->ablate_node = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(7, value));
   } else if (n == "ablate_gather") {

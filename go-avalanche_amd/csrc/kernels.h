@@ -32,13 +32,24 @@ constexpr uint32_t kMaxPoll = 4096;     // AvalancheMaxElementPoll, avalanche.go
 constexpr int kMaxK = 16;
 constexpr int kMaxPeers = 15;           // peer-push exchange: other ranks of a node-sharded network
 
+// Replay stream layout (one round): per tile of 64 lanes, ceil(k/2) groups of
+// 64 lane-interleaved 16-byte records; group q of lane g holds (yes, consider)
+// of slot 2q and of slot 2q+1. A wave reads two slots with one dwordx4 per
+// lane (1 KiB contiguous per wave-instruction), like the V/K plane groups.
+__host__ __device__ constexpr size_t replay_groups(int k) { return (size_t)((k + 1) / 2); }
+__host__ __device__ inline size_t replay_words(uint32_t Lpad, int k) { return replay_groups(k) * 4u * Lpad; }
+// word index of slot j's yes (c = 0) or consider (c = 1) word of lane g
+__host__ __device__ inline size_t replay_idx(uint32_t g, int k, int j, int c) {
+  return (((size_t)(g >> 6) * replay_groups(k) + (size_t)(j >> 1)) * 64u + (g & 63u)) * 4u + (size_t)((j & 1) * 2 + c);
+}
+
 struct RoundParams {
   uint32_t* planes;
   const uint32_t* pref_in;   // [N_pad][BL] published preference (round start)
   uint32_t* pref_out;        // [N_pad][BL] published preference (round end)
   const uint32_t* valid;     // [BL] Target.IsValid() bits
   const uint32_t* byz;       // [ceil(N/32)] Byzantine node bits
-  const uint32_t* replay;    // [k][2][Lpad] yes/consider planes (replay mode)
+  const uint32_t* replay;    // replay mode: yes/consider words of each lane and slot (replay_idx)
   uint64_t* log;             // [kLogShards][log_cap] single StatusUpdates
   uint32_t* log_count;       // [kLogShards] singles reserved per shard
   uint64_t* dlog;            // [kLogShards][dlog_cap][dense_words(k)] dense lane records
@@ -46,6 +57,18 @@ struct RoundParams {
   uint32_t* upd_count;       // [kLogShards] StatusUpdates emitted (singles + dense bits)
   uint32_t* log_overflow;    // [1]
   uint32_t* node_flags;      // [NL] capped path: nodes left to the exact pass (nullptr: none)
+  // exact pass (k_round_capped behind k_round_node / k_replay_node): node_flags[nl] = 1 + the first
+  // round, relative to the fused launch, that the exact pass takes the node (k_round_node: 1); the
+  // launch for relative round exact_rel takes the nodes with 0 < flag <= exact_rel + 1 and clears
+  // their flags unless exact_keep
+  uint32_t exact_rel;
+  uint32_t exact_keep;
+  // fused replay rounds (k_replay_node): rounds in the launch, replay words per round, the three
+  // preference snapshots and the index of the one the launch's first round writes
+  uint32_t fuse_rounds;
+  uint32_t ring_next;
+  uint64_t replay_stride;
+  uint32_t* pref_ring[3];
   unsigned long long* applied;  // [kLogShards] regsiterVote applications
   unsigned long long* bytes;    // [kLogShards] algorithmic bytes moved by the round kernel
   unsigned long long* finalized;  // [kLogShards] records finalized (deleted, processor.go:114-116)
@@ -68,7 +91,7 @@ struct RoundParams {
   uint32_t ablate_gather;    // diagnostics only: gather the node's own row (wrong results)
   uint32_t ablate_emit;      // diagnostics only: count StatusUpdates, store none (log left empty)
   uint32_t ablate_node;      // diagnostics only (k_round_node, wrong results): 1 = only the lanes below the
-                             // cap run, 2 = no replay loads, 4 = no plane stores
+                             // cap run, 4 = no plane stores
   // k_round_sweep only
   uint32_t warm_all;         // every consider plane of every lane is all-ones (no per-tile check)
   uint32_t store_policy;     // 0/1: per plane_nt; 2: sc1 plane/pref stores; 3: nt sc1 (k = 8)
@@ -163,6 +186,9 @@ __host__ __device__ inline uint64_t pack_update(uint32_t round_rel, uint32_t nod
 }
 
 hipError_t launch_round(const RoundParams& p, int k, bool replay, bool capped, hipStream_t s);
+// k_replay_node: p.fuse_rounds replay rounds of every node in one launch (capped engines, k <= 8);
+// nodes that reach count 120 are left to the exact pass from that round on (node_flags)
+hipError_t launch_replay_node(const RoundParams& p, int k, hipStream_t s);
 // Persistent streaming round kernel (round_sweep.hip), uncapped path, k <= 8:
 // `blocks` workgroups of 256 threads sweep the tiles; 0 = one wave per tile.
 hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s);

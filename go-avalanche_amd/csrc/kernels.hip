@@ -54,8 +54,8 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
   if (REPLAY) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      w[j] = active ? p.replay[(size_t)(2 * j) * p.Lpad + g] : 0u;
-      cw[j] = active ? p.replay[(size_t)(2 * j + 1) * p.Lpad + g] : 0u;
+      w[j] = active ? p.replay[replay_idx(g, K, j, 0)] : 0u;
+      cw[j] = active ? p.replay[replay_idx(g, K, j, 1)] : 0u;
     }
   } else {
     uint32_t peers[K];
@@ -180,9 +180,10 @@ __global__ __launch_bounds__(1024) void k_round_capped(const RoundParams p) {
   // only the ones it flagged (an almost empty pass costs ~1-2 us, not the
   // dispatch of one workgroup per node)
   for (uint32_t nl = blockIdx.x; nl < p.NL; nl += gridDim.x) {
-    if (p.node_flags[nl] == 0u) continue;  // workgroup-uniform
+    const uint32_t f = p.node_flags[nl];  // workgroup-uniform
+    if (f == 0u || f - 1u > p.exact_rel) continue;
     __syncthreads();
-    if (threadIdx.x == 0) p.node_flags[nl] = 0u;
+    if (threadIdx.x == 0 && !p.exact_keep) p.node_flags[nl] = 0u;
     capped_node<K, REPLAY>(p, nl, wsum);
     __syncthreads();  // wsum reuse by the next node
   }
@@ -205,8 +206,8 @@ __device__ __forceinline__ void capped_node(const RoundParams& p, uint32_t nl, u
   if (REPLAY) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      w[j] = active ? p.replay[(size_t)(2 * j) * p.Lpad + g] : 0u;
-      cw[j] = active ? p.replay[(size_t)(2 * j + 1) * p.Lpad + g] : 0u;
+      w[j] = active ? p.replay[replay_idx(g, K, j, 0)] : 0u;
+      cw[j] = active ? p.replay[replay_idx(g, K, j, 1)] : 0u;
     }
   } else {
     uint32_t peers[K];
@@ -579,15 +580,15 @@ __global__ void k_sample_peers(uint64_t seed, uint32_t n_nodes, uint32_t a, uint
 
 // Synthetic replayed vote stream (C2): class per (node, round, slot, target)
 // from philox(node, round, t>>1, REPLAY | slot<<8); same definition as
-// avo_replay_err in the oracle. Output planes [slot][yes|consider][Lpad].
+// avo_replay_err in the oracle. Output: the tiled replay layout (kernels.h replay_idx).
 __global__ void k_gen_replay(uint64_t seed, uint32_t n0, uint32_t BL, uint32_t L, uint32_t Lpad, uint32_t t0,
                              uint32_t n_targets, uint32_t round, int k, uint32_t* out) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= Lpad) return;
   if (g >= L) {
     for (int s = 0; s < k; ++s) {
-      out[(size_t)(2 * s) * Lpad + g] = 0u;
-      out[(size_t)(2 * s + 1) * Lpad + g] = 0u;
+      out[replay_idx(g, k, s, 0)] = 0u;
+      out[replay_idx(g, k, s, 1)] = 0u;
     }
     return;
   }
@@ -606,8 +607,8 @@ __global__ void k_gen_replay(uint64_t seed, uint32_t n0, uint32_t BL, uint32_t L
       y |= (v1 < kReplayYes ? 1u : 0u) << (2 * q + 1);
       c |= (v1 < kReplayNo ? 1u : 0u) << (2 * q + 1);
     }
-    out[(size_t)(2 * s) * Lpad + g] = y & tm;
-    out[(size_t)(2 * s + 1) * Lpad + g] = c & tm;
+    out[replay_idx(g, k, s, 0)] = y & tm;
+    out[replay_idx(g, k, s, 1)] = c & tm;
   }
 }
 

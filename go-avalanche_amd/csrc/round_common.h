@@ -79,6 +79,24 @@ __device__ __forceinline__ void pst4(u32x4* q, u32x4 v) {
     *q = v;
 }
 
+// The k replayed (yes, consider) word pairs of lane g (kernels.h replay_idx):
+// ceil(K/2) dwordx4 loads; the stream is read once per round (non-temporal).
+template <int K>
+__device__ __forceinline__ void replay_load(const uint32_t* rp, uint32_t g, uint32_t* w, uint32_t* cw) {
+  constexpr int G = (K + 1) / 2;
+  const u32x4* q = reinterpret_cast<const u32x4*>(rp) + (size_t)(g >> 6) * (G * 64) + (g & 63u);
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    const u32x4 v = pld4<true>(q + i * 64);
+    w[2 * i] = v[0];
+    cw[2 * i] = v[1];
+    if (2 * i + 1 < K) {
+      w[2 * i + 1] = v[2];
+      cw[2 * i + 1] = v[3];
+    }
+  }
+}
+
 // Byzantine flip-flop answer: err = ((r ^ t) & 1) ? 1 : 0, so
 // "yes" on even targets in even rounds. Blocks start at multiples of 32.
 __device__ __forceinline__ uint32_t byz_pattern(uint32_t round) { return (round & 1u) ? 0xAAAAAAAAu : 0x55555555u; }
@@ -409,6 +427,106 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
 // Per-wave counters: regsiterVote applications (the metric numerator) and the
 // algorithmic bytes this wave moved (state planes actually read/written,
 // gathered vote words, the published word, the StatusUpdate log bytes written).
+// StatusUpdate emission without LDS staging (k_round_sweep's warm modes,
+// where staging registers spill, and k_round_node): the same log as
+// emit_updates, but a sparse lane walks its own updates (fewer than dense_min) one per iteration
+// at its exclusive prefix, so the wave runs max(updates per sparse lane)
+// iterations instead of one ballot loop per slot. A record emits at most two
+// updates per round at k <= 8 (two flips are >= 6 votes apart; a record that
+// finalizes does not flip in the same round), so its status
+// after an update is A_final, flipped back once for the first of two (T: the
+// records with two updates, S: those whose first was already written).
+template <int K>
+__device__ __forceinline__ uint32_t emit_updates_flat(const RoundParams& p, uint32_t wave_id, uint32_t lane,
+                                                      uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
+                                                      uint32_t A_final, uint32_t died, uint32_t& updates,
+                                                      uint32_t round_rel) {
+  static_assert(K <= 8, "two updates per record per round at most: k <= 8 (and no finalization, died = 0, unless k = 8)");
+  uint32_t any = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) any |= E[j];
+  if (__ballot(any != 0u) == 0ull) return 0u;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) cnt += (uint32_t)__popc(E[j]);
+  constexpr uint32_t DW = dense_words(K);
+  const bool dense = cnt >= p.dense_min;
+  const uint64_t dl = __ballot(dense);
+  const uint32_t scnt = dense ? 0u : cnt;
+  const uint32_t incl = wave_incl_scan(scnt, lane);
+  const uint32_t tot_s = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  const uint32_t tot_d = (uint32_t)__popcll(dl);
+  updates += wave_sum(cnt);
+  if (p.ablate_emit == 1u) return 0u;  // diagnostics: the cost of the round without its log stores
+  const uint32_t shard = wave_id % p.log_shards;
+  uint32_t base = 0, dbase = 0;
+  if (p.ablate_emit == 2u) {  // diagnostics: stores at made-up positions, no reserving atomic (log invalid)
+    base = p.log_cap > 8192u ? (wave_id * 509u) % (p.log_cap - 4096u) : 0u;
+    dbase = p.dlog_cap > 128u ? (wave_id * 131u) % (p.dlog_cap - 64u) : 0u;
+  } else if (lane == 0) {
+    if (tot_s) base = atomicAdd(&p.log_count[shard], tot_s);
+    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard], tot_d);
+  }
+  base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+  dbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)dbase);
+  const uint32_t st_d = dbase >= p.dlog_cap ? 0u : min(tot_d, p.dlog_cap - dbase);
+  const uint32_t st_s = base >= p.log_cap ? 0u : min(tot_s, p.log_cap - base);
+  const bool ovf = st_d < tot_d || st_s < tot_s;
+  if (dense) {
+    const uint32_t pos = dbase + __builtin_amdgcn_mbcnt_hi((uint32_t)(dl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dl, 0u));
+    if (pos < p.dlog_cap) {
+      uint32_t* rec = reinterpret_cast<uint32_t*>(p.dlog + ((size_t)shard * p.dlog_cap + pos) * DW);
+      const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u);
+      rec[0] = (uint32_t)key;
+      rec[1] = (uint32_t)(key >> 32);
+#pragma unroll
+      for (int j = 0; j < K; ++j) rec[2 + j] = E[j];
+      rec[2 + K] = A_final;
+      rec[3 + K] = died;
+    }
+  }
+  if (tot_s) {
+    // T: records with two updates this round; nz: slots with updates left
+    uint32_t seen = 0u, T = 0u, nz = 0u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      T |= seen & E[j];
+      seen |= E[j];
+      nz |= (E[j] != 0u ? 1u : 0u) << j;
+    }
+    if (dense) nz = 0u;
+    uint64_t* const dst = p.log + (size_t)shard * p.log_cap;
+    uint32_t pos = base + incl - scnt;  // this lane's first entry
+    const uint32_t end = base + st_s;   // entries at or past it were dropped (overflow)
+    uint32_t S = 0u, j = 0u, cur = 0u;
+    const uint64_t hi = ((uint64_t)round_rel << 52) | ((uint64_t)node << 28);
+    for (uint32_t r = 0; r < 64u; ++r) {
+      const bool more = r < scnt;
+      if (__ballot(more) == 0ull) break;
+      if (more) {
+        if (cur == 0u) {  // next slot with updates
+          j = (uint32_t)__ffs(nz) - 1u;
+          nz &= nz - 1u;
+          cur = E[0];
+#pragma unroll
+          for (int q = 1; q < K; ++q) cur = j == (uint32_t)q ? E[q] : cur;
+        }
+        const uint32_t bit = (uint32_t)__ffs(cur) - 1u;
+        cur &= cur - 1u;
+        const uint32_t m = 1u << bit;
+        const uint32_t a = ((A_final ^ (T & ~S)) >> bit) & 1u;  // A after slot j (vote.go:77-91)
+        S |= m;
+        const uint32_t st = (died & m) ? (a ? 3u : 0u) : (a ? 2u : 1u);
+        if (pos < end) dst[pos] = hi | ((uint64_t)j << 24) | ((uint64_t)(tbase + bit) << 2) | st;
+        ++pos;
+      }
+    }
+  }
+  if (__ballot(ovf) != 0ull) note_overflow(p, lane);
+  // bytes actually stored (wave-uniform): entries past a full shard were dropped
+  return 8u * st_s + 8u * DW * st_d;
+}
+
 __device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied,
                                             bool active, uint32_t bytes_per_lane, uint32_t emitted_bytes,
                                             uint32_t updates, uint32_t died) {

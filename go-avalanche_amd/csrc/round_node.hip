@@ -70,19 +70,7 @@ __device__ __forceinline__ void node_lane_load(const RoundParams& p, uint32_t* t
 #pragma unroll
   for (int i = 0; i < 8; ++i) in.C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
   if constexpr (REPLAY) {
-    if (p.ablate_node & 2u) {  // diagnostics: no replay loads
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        in.cw[j] = ~(g * 0x9E3779B9u + (uint32_t)j);
-        in.w[j] = g * 0x85EBCA6Bu ^ (uint32_t)j;
-      }
-      return;
-    }
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      in.cw[j] = p.replay[(size_t)(2 * j + 1) * p.Lpad + g];
-      in.w[j] = p.replay[(size_t)(2 * j) * p.Lpad + g];
-    }
+    replay_load<K>(p.replay, g, in.w, in.cw);
   } else {
     uint32_t peers[K];
     draw_peers<K>(p, p.round, node, nl, nl, 1u, lane, peers);  // every lane of the workgroup is the same node
@@ -222,11 +210,192 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
     p.pref_out[prow] = pub_byz ? byz_pattern(p.round + 1u) : A;
   }
   uint32_t upd = 0;
-  const uint32_t emitted = emit_updates<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, died, upd);
+  const uint32_t emitted = emit_updates_flat<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, died, upd, p.round_rel);
   // bytes: a lane of a polling wave reads all 25 planes and its k vote words,
   // writes its published word, and writes its planes back if it polled a record
   const uint32_t lane_bytes = kPlanes * 4u + (REPLAY ? 8u : 4u) * K + 4u + (any ? kPlanes * 4u : 0u);
   count_stats(p, wave_id, lane, applied, active, lane_bytes, emitted, upd, died);
+}
+
+// Fused replay rounds: p.fuse_rounds consecutive replay rounds of one node
+// in one workgroup. In replay mode a node's votes come from its own stream,
+// never from another node's published preference (processor.go:92-117 on
+// recorded Responses), so its records evolve independently of every other
+// node and a workgroup can carry them through R rounds in registers: the 25
+// planes are read once and written once per launch instead of once per
+// round. The poll set (processor.go:165-167) can change inside a round only
+// when a polled record finalizes, so it is selected once; before each round
+// the workgroup checks whether a polled record has count >= 120 and, if so,
+// stores the state reached so far and leaves the node to the exact pass from
+// that round on (node_flags[nl] = 1 + round; k_round_capped runs it per
+// round). Every round's votes are applied and its StatusUpdates emitted with
+// its own round key; the published word is written for the last three rounds
+// of the launch (the three snapshot buffers; replay rounds do not read them).
+template <int K, bool NT, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
+  __shared__ uint32_t wsum[2][16];
+  const uint32_t nl = blockIdx.x;
+  const uint32_t b = threadIdx.x;
+  const uint32_t lane = b & 63u, wave = b >> 6;
+  const bool active = b < p.BL;
+  const uint32_t bc = active ? b : p.BL - 1u;  // inactive lanes read a valid lane, never store
+  const uint32_t g = nl * p.BL + bc;
+  const uint32_t node = p.n0 + nl;
+  const bool early = b < kMaxPoll / 32u;  // wave-uniform
+
+  uint32_t* const tp = p.planes + (size_t)(g >> 6) * (kPlanes * 64u);
+  const uint32_t tl = g & 63u;
+  u32x4* const grp = reinterpret_cast<u32x4*>(tp) + tl;
+  const u32x4 k1 = pld4<NT>(grp + 192);
+  uint32_t A = pld<NT>(tp + 1536u + tl);
+  const uint32_t vmask = active ? p.valid[bc] : 0u;
+  u32x4 v0 = u32x4{0u, 0u, 0u, 0u}, v1 = v0, k0 = v0;
+  uint32_t C[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) C[i] = 0u;
+  if (early) {
+    v0 = pld4<NT>(grp);
+    v1 = pld4<NT>(grp + 64);
+    k0 = pld4<NT>(grp + 128);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
+  }
+  const uint32_t P0 = ~k1[3] & vmask;  // live and IsValid (processor.go:95-103)
+  const uint32_t polled = cap_select(P0, lane, wave, wsum, 0u);
+  const bool heavy = early || __ballot(polled != 0u) != 0ull;  // wave-uniform
+  if (!early && heavy) {
+    v0 = pld4<NT>(grp);
+    v1 = pld4<NT>(grp + 64);
+    k0 = pld4<NT>(grp + 128);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
+  }
+  uint32_t V[8], Kp[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    V[i] = v0[i];
+    V[4 + i] = v1[i];
+    Kp[i] = k0[i];
+    Kp[4 + i] = k1[i];
+  }
+  const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
+  const uint32_t prow = node * p.BL + b;
+  const bool byz = is_byz(p.byz, node);
+  const uint32_t R = p.fuse_rounds;
+  // A count grows by at most K per round, so no polled record can reach 120
+  // before round J = ceil((120 - max count) / K): those rounds need no
+  // workgroup check (the waves run them without a barrier).
+  uint32_t hi = 0u;  // bit q: some polled record of the lane has count bit q set, ignoring lower bits
+  {
+    uint32_t m = polled;  // records whose count matches the maximum so far, bit by bit from the top
+#pragma unroll
+    for (int q = 6; q >= 0; --q) {
+      const uint32_t t = m & Kp[q];
+      if (t) {
+        m = t;
+        hi |= 1u << q;
+      }
+    }
+    if (!heavy || !polled) hi = 0u;
+  }
+  uint32_t wm = hi;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) wm = max(wm, (uint32_t)__shfl_xor((int)wm, o, 64));
+  if (lane == 0) wsum[1][wave] = wm;  // (cap_select used wsum[0])
+  __syncthreads();
+  uint32_t maxc = 0u;  // largest polled count of the node
+  for (uint32_t q = 0; q < (blockDim.x >> 6); ++q) maxc = max(maxc, wsum[1][q]);
+  const uint32_t J = maxc >= 120u ? 0u : (120u - maxc + (uint32_t)K - 1u) / (uint32_t)K;
+  uint32_t done = R, applied = 0u, upd = 0u, emitted = 0u, pubs = 0u;
+  for (uint32_t r = 0; r < R; ++r) {
+    // a polled record with count >= 120 may finalize (and leave the poll set) this round
+    if (r >= J) {
+      const uint32_t nearfin = heavy ? polled & Kp[6] & Kp[5] & Kp[4] & Kp[3] : 0u;
+      if (__syncthreads_or(nearfin != 0u)) {  // workgroup-uniform
+        done = r;
+        break;
+      }
+    }
+    uint32_t E[K];
+    if (heavy) {
+      uint32_t w[K], cw[K];
+      replay_load<K>(p.replay + (size_t)r * p.replay_stride, g, w, cw);
+      // ys/ns: y/n of [V_6..V_0, w_0..w_{K-1}] (vote.go:55-56)
+      uint32_t ys[7 + K], ns[7 + K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint32_t yw = w[j] & cw[j];  // err == 0 implies considered
+        ys[7 + j] = yw;
+        ns[7 + j] = ~yw & cw[j];
+      }
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        ys[i] = V[6 - i] & C[6 - i];
+        ns[i] = ~V[6 - i] & C[6 - i];
+      }
+      // every polled record shifts in the K votes (vote.go:55-56)
+#pragma unroll
+      for (int i = 7; i >= 0; --i) {
+        const uint32_t vs = i < K ? ys[6 + K - i] : V[i - K];
+        const uint32_t cs = i < K ? cw[K - 1 - i] : C[i - K];
+        V[i] = (vs & polled) | (V[i] & ~polled);
+        C[i] = (cs & polled) | (C[i] & ~polled);
+      }
+      uint32_t alive = polled, c[4] = {0u, 0u, 0u, 0u}, F = 0u, ap = 0u;
+      const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
+      round_slots<K, false>(ys, ns, low3, 0u, false, alive, A, E, c, F, ap);
+      applied += (uint32_t)K * (uint32_t)__popc(polled);
+      uint32_t cy = 0u;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const uint32_t ci = i < 4 ? c[i] : 0u;
+        const uint32_t t = Kp[i] ^ ci;
+        const uint32_t si = t ^ cy;
+        cy = (t & cy) | (Kp[i] & ci);
+        Kp[i] = (F & ci) | (~F & si);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < K; ++j) E[j] = 0u;
+    }
+    if (r + 3u >= R) {  // the last three rounds fill the three snapshot buffers
+      if (active) p.pref_ring[(p.ring_next + r) % 3u][prow] = byz ? byz_pattern(p.round + r + 1u) : A;
+      ++pubs;
+    }
+    if (heavy) emitted += emit_updates_flat<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, 0u, upd, p.round_rel + r);
+  }
+  if (done < R && b == 0) p.node_flags[nl] = done + 1u;  // the exact pass takes rounds done..R-1
+  const bool any = heavy && polled != 0u && done > 0u;
+  if (active && any) {
+    pst4<NT>(grp, u32x4{V[0], V[1], V[2], V[3]});
+    pst4<NT>(grp + 64, u32x4{V[4], V[5], V[6], V[7]});
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pst<NT>(tp + 1024u + (uint32_t)i * 64u + tl, C[i]);
+    pst4<NT>(grp + 128, u32x4{Kp[0], Kp[1], Kp[2], Kp[3]});
+    pst4<NT>(grp + 192, u32x4{Kp[4], Kp[5], Kp[6], Kp[7]});
+    pst<NT>(tp + 1536u + tl, A);
+  }
+  // bytes: state read once (heavy: 25 planes, light: K4-7 and A) and written
+  // once if a record was polled; 8 B per replayed vote word pair per round;
+  // the published words written
+  const uint32_t lane_bytes = (heavy ? kPlanes * 4u + 8u * K * done : 20u) + 4u + 4u * pubs +
+                              (any ? kPlanes * 4u : 0u);
+  count_stats(p, wave_id, lane, applied, active, lane_bytes, emitted, upd, 0u);
+}
+
+template <int K, int MAXT>
+hipError_t launch_replay_t(const RoundParams& p, uint32_t bt, hipStream_t s) {
+  if (p.plane_nt)
+    hipLaunchKernelGGL((k_replay_node<K, true, MAXT>), dim3(p.NL), dim3(bt), 0, s, p);
+  else
+    hipLaunchKernelGGL((k_replay_node<K, false, MAXT>), dim3(p.NL), dim3(bt), 0, s, p);
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_replay_k(const RoundParams& p, hipStream_t s) {
+  const uint32_t bt = ((p.BL + 63u) / 64u) * 64u;
+  return bt <= 512u ? launch_replay_t<K, 512>(p, bt, s) : launch_replay_t<K, 1024>(p, bt, s);
 }
 
 template <int K, int MAXT>
@@ -255,6 +424,21 @@ hipError_t launch_node_k(const RoundParams& p, bool replay, hipStream_t s) {
 }
 
 }  // namespace
+
+hipError_t launch_replay_node(const RoundParams& p, int k, hipStream_t s) {
+  if (!p.node_flags || p.fuse_rounds == 0u || !p.replay) return hipErrorInvalidValue;
+  switch (k) {
+    case 1: return launch_replay_k<1>(p, s);
+    case 2: return launch_replay_k<2>(p, s);
+    case 3: return launch_replay_k<3>(p, s);
+    case 4: return launch_replay_k<4>(p, s);
+    case 5: return launch_replay_k<5>(p, s);
+    case 6: return launch_replay_k<6>(p, s);
+    case 7: return launch_replay_k<7>(p, s);
+    case 8: return launch_replay_k<8>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 hipError_t launch_round_node(const RoundParams& p, int k, bool replay, bool exact_pass, hipStream_t s) {
   if (!p.node_flags) return hipErrorInvalidValue;

@@ -150,11 +150,7 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
   in.vmask = x.active ? p.valid[x.b] : 0u;
   in.byzw = p.byz[x.node >> 5];
   if constexpr (REPLAY) {
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      in.cw[j] = p.replay[(size_t)(2 * j + 1) * p.Lpad + x.gc];
-      in.w[j] = p.replay[(size_t)(2 * j) * p.Lpad + x.gc];
-    }
+    replay_load<K>(p.replay, x.gc, in.w, in.cw);
   } else {
     const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
     uint32_t peers[K];
@@ -358,104 +354,6 @@ __device__ __forceinline__ uint32_t emit_updates_lds(const RoundParams& p, uint3
           if (pos < st_s) dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
           ++pos;
         }
-      }
-    }
-  }
-  if (__ballot(ovf) != 0ull) note_overflow(p, lane);
-  // bytes actually stored (wave-uniform): entries past a full shard were dropped
-  return 8u * st_s + 8u * DW * st_d;
-}
-
-// StatusUpdate emission without LDS staging (the warm modes, where staging
-// registers spill): the same log as emit_updates (round_common.h), but a
-// sparse lane walks its own updates (fewer than dense_min) one per iteration
-// at its exclusive prefix, so the wave runs max(updates per sparse lane)
-// iterations instead of one ballot loop per slot. A record emits at most two
-// updates per round at k = 8 (two flips are >= 6 votes apart), so its status
-// after an update is A_final, flipped back once for the first of two (T: the
-// records with two updates, S: those whose first was already written).
-template <int K>
-__device__ __forceinline__ uint32_t emit_updates_flat(const RoundParams& p, uint32_t wave_id, uint32_t lane,
-                                                      uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
-                                                      uint32_t A_final, uint32_t died, uint32_t& updates) {
-  static_assert(K == 8, "two updates per record per round at most: k = 8");
-  uint32_t any = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) any |= E[j];
-  if (__ballot(any != 0u) == 0ull) return 0u;
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) cnt += (uint32_t)__popc(E[j]);
-  constexpr uint32_t DW = dense_words(K);
-  const bool dense = cnt >= p.dense_min;
-  const uint64_t dl = __ballot(dense);
-  const uint32_t scnt = dense ? 0u : cnt;
-  const uint32_t incl = wave_incl_scan(scnt, lane);
-  const uint32_t tot_s = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  const uint32_t tot_d = (uint32_t)__popcll(dl);
-  updates += wave_sum(cnt);
-  if (p.ablate_emit == 1u) return 0u;  // diagnostics: the cost of the round without its log stores
-  const uint32_t shard = wave_id % p.log_shards;
-  uint32_t base = 0, dbase = 0;
-  if (p.ablate_emit == 2u) {  // diagnostics: stores at made-up positions, no reserving atomic (log invalid)
-    base = p.log_cap > 8192u ? (wave_id * 509u) % (p.log_cap - 4096u) : 0u;
-    dbase = p.dlog_cap > 128u ? (wave_id * 131u) % (p.dlog_cap - 64u) : 0u;
-  } else if (lane == 0) {
-    if (tot_s) base = atomicAdd(&p.log_count[shard], tot_s);
-    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard], tot_d);
-  }
-  base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-  dbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)dbase);
-  const uint32_t st_d = dbase >= p.dlog_cap ? 0u : min(tot_d, p.dlog_cap - dbase);
-  const uint32_t st_s = base >= p.log_cap ? 0u : min(tot_s, p.log_cap - base);
-  const bool ovf = st_d < tot_d || st_s < tot_s;
-  if (dense) {
-    const uint32_t pos = dbase + __builtin_amdgcn_mbcnt_hi((uint32_t)(dl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dl, 0u));
-    if (pos < p.dlog_cap) {
-      uint32_t* rec = reinterpret_cast<uint32_t*>(p.dlog + ((size_t)shard * p.dlog_cap + pos) * DW);
-      const uint64_t key = pack_update(p.round_rel, node, 0u, tbase, 0u);
-      rec[0] = (uint32_t)key;
-      rec[1] = (uint32_t)(key >> 32);
-#pragma unroll
-      for (int j = 0; j < K; ++j) rec[2 + j] = E[j];
-      rec[2 + K] = A_final;
-      rec[3 + K] = died;
-    }
-  }
-  if (tot_s) {
-    // T: records with two updates this round; nz: slots with updates left
-    uint32_t seen = 0u, T = 0u, nz = 0u;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      T |= seen & E[j];
-      seen |= E[j];
-      nz |= (E[j] != 0u ? 1u : 0u) << j;
-    }
-    if (dense) nz = 0u;
-    uint64_t* const dst = p.log + (size_t)shard * p.log_cap;
-    uint32_t pos = base + incl - scnt;  // this lane's first entry
-    const uint32_t end = base + st_s;   // entries at or past it were dropped (overflow)
-    uint32_t S = 0u, j = 0u, cur = 0u;
-    const uint64_t hi = ((uint64_t)p.round_rel << 52) | ((uint64_t)node << 28);
-    for (uint32_t r = 0; r < 64u; ++r) {
-      const bool more = r < scnt;
-      if (__ballot(more) == 0ull) break;
-      if (more) {
-        if (cur == 0u) {  // next slot with updates
-          j = (uint32_t)__ffs(nz) - 1u;
-          nz &= nz - 1u;
-          cur = E[0];
-#pragma unroll
-          for (int q = 1; q < K; ++q) cur = j == (uint32_t)q ? E[q] : cur;
-        }
-        const uint32_t bit = (uint32_t)__ffs(cur) - 1u;
-        cur &= cur - 1u;
-        const uint32_t m = 1u << bit;
-        const uint32_t a = ((A_final ^ (T & ~S)) >> bit) & 1u;  // A after slot j (vote.go:77-91)
-        S |= m;
-        const uint32_t st = (died & m) ? (a ? 3u : 0u) : (a ? 2u : 1u);
-        if (pos < end) dst[pos] = hi | ((uint64_t)j << 24) | ((uint64_t)(tbase + bit) << 2) | st;
-        ++pos;
       }
     }
   }
@@ -697,7 +595,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   if constexpr (LE)
     emitted = emit_updates_lds<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, es);
   else if constexpr (K == 8)
-    emitted = emit_updates_flat<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates);
+    emitted = emit_updates_flat<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, p.round_rel);
   else
     emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates);
 

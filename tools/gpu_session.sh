@@ -123,9 +123,11 @@ for s in "$@"; do
     gaps2) step gaps2 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/gaps2 -o gap -- python3 tools/gap_probe.py --workload c2 ;;
     profc2) step profc2 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc2 -o c2 -- \
             python3 bench.py --workload c2 --no-cpu-baseline ;;
-    probe_c2abl) step probe_c2abl 600 bash -c 'for o in "ablate_node=0" "ablate_node=1" "ablate_node=2" "ablate_node=4" "ablate_node=7" "ablate_emit=1" "ablate_emit=1 --option ablate_node=7"; do echo "== $o"; python tools/round_probe.py --workload c2 --option $o | tail -2; done' ;;
+    probe_c2abl) step probe_c2abl 600 bash -c 'for o in "replay_prefetch=0" "replay_prefetch=1" "ablate_node=1" "ablate_node=2" "ablate_node=4" "ablate_emit=1" "ablate_emit=1 --option ablate_node=7"; do echo "== $o"; python tools/round_probe.py --workload c2 --option $o | tail -2; done' ;;
     profc2p) step profc2p 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc2p -o c2 -- \
             python3 tools/round_probe.py --workload c2 ;;
+    fused) step fused 600 python -u -m pytest tests/test_gpu_replay_fused.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    fuseprobe) step fuseprobe 300 bash -c 'for o in "ablate_emit=0" "ablate_emit=1" "ablate_emit=2"; do python tools/fuse_probe.py --option $o; done' ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
