@@ -65,6 +65,9 @@ struct av_engine {
   // (S_r) and writes pref[nxt(cur)] (S_r+1); pref[prv(cur)] (S_r-1) is kept
   // for tiles whose vote planes are recomputed (vstale)
   uint32_t* pref[3] = {nullptr, nullptr, nullptr};
+  // words per node row of the preference tables: BL rounded up to a power of two (BL <= 32) or to a
+  // multiple of 32 (BL > 32), so that a gathered row covers whole 128-B lines (avk::pref_stride)
+  uint32_t PS = 0;
   int cur = 0;
   static int nxt(int c) { return c == 2 ? 0 : c + 1; }
   static int prv(int c) { return c == 0 ? 2 : c - 1; }
@@ -253,6 +256,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.n0 = (uint32_t)e->n0;
   p.NL = e->NL;
   p.BL = e->BL;
+  p.PS = e->PS;
   p.L = e->L;
   p.Lpad = e->Lpad;
   p.t0 = (uint32_t)e->t0;
@@ -315,7 +319,7 @@ int push_own_rows(av_engine* e, int b) {
   uint32_t n = 0;
   for (int r = 0; r < e->peer_world; ++r)
     if (r != e->peer_rank) dst.p[n++] = e->peer_pref[b][r];
-  const uint64_t w0 = (uint64_t)e->n0 * e->BL, w1 = w0 + (uint64_t)e->NL * e->BL;
+  const uint64_t w0 = (uint64_t)e->n0 * e->PS, w1 = w0 + (uint64_t)e->NL * e->PS;
   AV_HIP(avk::launch_push_rows(e->pref[b], dst, n, w0, w1, e->stream));
   return AV_OK;
 }
@@ -389,7 +393,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   AV_CHECK(!(compat && e->capped && (e->pub_mode == 2 || e->any_nopoll)), AV_ERR_UNSUPPORTED,
            "the example responder and av_set_polling need M <= 4096 (uncapped)");
   // the sweep addresses the preference table by 32-bit byte offsets
-  const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped && !compat && (uint64_t)e->N * e->BL < (1ull << 30);
+  const bool sweep = e->kernel == 2 && e->k <= 8 && !e->capped && !compat && (uint64_t)e->N * e->PS < (1ull << 30);
   // the round after av_init_records: planes known to be zero are not read
   const bool fresh = e->fresh && sweep && !replay && !e->ablate_gather;
   // the sweep's warm sim modes (launch_sweep_k): every consider plane all-ones
@@ -472,9 +476,9 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     if (rc != AV_OK) return rc;
   }
   if (e->comm) {
-    const size_t count = (size_t)e->NL * e->BL;
+    const size_t count = (size_t)e->NL * e->PS;
     uint32_t* out = e->pref[av_engine::nxt(e->cur)];
-    ncclResult_t r = ncclAllGather(out + (size_t)e->n0 * e->BL, out, count, ncclUint32, e->comm, e->stream);
+    ncclResult_t r = ncclAllGather(out + (size_t)e->n0 * e->PS, out, count, ncclUint32, e->comm, e->stream);
     AV_CHECK(r == ncclSuccess, AV_ERR_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
   }
   e->cur = av_engine::nxt(e->cur);
@@ -549,7 +553,7 @@ uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
 
 int refresh_pref(av_engine* e) {
   AV_HIP(avk::launch_refresh_pref((uint32_t)e->pub_mode, e->planes, e->pref[e->cur], e->byz, (uint32_t)e->n0, e->NL,
-                                  e->BL, (uint32_t)e->round, e->stream));
+                                  e->BL, e->PS, (uint32_t)e->round, e->stream));
   return AV_OK;
 }
 
@@ -644,11 +648,12 @@ int av_create(const av_config* cfg, av_engine** out) {
   }
   e->NL = (uint32_t)(e->n1 - e->n0);
   e->BL = (uint32_t)((e->t1 - e->t0 + 31) / 32);
+  e->PS = avk::pref_stride(e->BL);
   if (e->capped && e->BL > 1024) return bad("capped path supports M <= 32768");
   const uint64_t L = (uint64_t)e->NL * e->BL;
   if (L >= (1ull << 31)) return bad("too many lanes for one engine: shard further");
-  // the round kernels index the published-preference table (all N nodes x BL words) in 32 bits
-  if ((uint64_t)e->N * e->BL >= (1ull << 31)) return bad("preference table over 2^31 words: shard targets further");
+  // the round kernels index the published-preference table (all N nodes x PS words) in 32 bits
+  if ((uint64_t)e->N * e->PS >= (1ull << 31)) return bad("preference table over 2^31 words: shard targets further");
   e->L = (uint32_t)L;
   e->Lpad = (uint32_t)((L + 63) / 64 * 64);
   avk::bl_divider(e->BL, e->bl_magic, e->bl_sh1, e->bl_sh2);
@@ -663,7 +668,7 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess)
     return hip_fail(he, "hipStreamCreate");
   const size_t plane_words = (size_t)(e->Lpad / 64) * avk::kPlanes * 64;
-  const size_t pref_words = (size_t)e->N * e->BL;
+  const size_t pref_words = (size_t)e->N * e->PS;
   int64_t cap = c.update_log_capacity;
   if (cap <= 0) cap = std::min<int64_t>(std::max<int64_t>((int64_t)L * 8, 1 << 20), 1ll << 28);
   // one shard per wave up to kLogShards: waves of the round kernel that runs
@@ -709,6 +714,7 @@ int av_create(const av_config* cfg, av_engine** out) {
   (void)hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
   (void)hipMemsetAsync(e->applied, 0, avk::kLogShards * 8, e->stream);
+  (void)hipMemsetAsync(e->pref[0], 0, pref_words * 4, e->stream);
   (void)hipMemsetAsync(e->pref[1], 0, pref_words * 4, e->stream);
   (void)hipMemsetAsync(e->pref[2], 0, pref_words * 4, e->stream);
   // every real target starts valid
@@ -756,6 +762,7 @@ int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
   p.n0 = (uint32_t)e->n0;
   p.NL = e->NL;
   p.BL = e->BL;
+  p.PS = e->PS;
   p.L = e->L;
   p.Lpad = e->Lpad;
   p.t0 = (uint32_t)e->t0;
@@ -834,6 +841,7 @@ int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uin
   p.node_local = (uint32_t)(node - e->n0);
   p.node = (uint32_t)node;
   p.BL = e->BL;
+  p.PS = e->PS;
   p.round = (uint32_t)e->round;
   p.pub_mode = (uint32_t)e->pub_mode;
   AV_HIP(avk::launch_add_targets(p, e->stream));
@@ -897,6 +905,7 @@ int register_votes_device(av_engine* e, const std::vector<std::pair<uint32_t, ui
   p.n_blocks = nb;
   p.n0 = (uint32_t)e->n0;
   p.BL = e->BL;
+  p.PS = e->PS;
   p.round = (uint32_t)e->round;
   p.pub_mode = (uint32_t)e->pub_mode;
   AV_HIP(avk::launch_register_votes(p, e->stream));
@@ -1006,6 +1015,7 @@ int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, 
   p.n_blocks = (uint32_t)nb;
   p.n0 = (uint32_t)e->n0;
   p.BL = e->BL;
+  p.PS = e->PS;
   p.round = (uint32_t)e->round;
   p.pub_mode = (uint32_t)e->pub_mode;
   AV_HIP(avk::launch_register_votes(p, e->stream));
@@ -1515,8 +1525,8 @@ int av_read_pref(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, u
   const size_t rows = (size_t)(n1 - n0);
   std::vector<uint32_t> w(rows * e->BL);
   if (rows) {
-    AV_HIP(hipMemcpyAsync(w.data(), e->pref[e->cur] + (size_t)n0 * e->BL, w.size() * 4, hipMemcpyDeviceToHost,
-                          e->stream));
+    AV_HIP(hipMemcpy2DAsync(w.data(), (size_t)e->BL * 4, e->pref[e->cur] + (size_t)n0 * e->PS, (size_t)e->PS * 4,
+                            (size_t)e->BL * 4, rows, hipMemcpyDeviceToHost, e->stream));
     AV_HIP(hipStreamSynchronize(e->stream));
   }
   const int64_t W = t1 - t0;
@@ -1534,7 +1544,8 @@ int av_read_pref_words(av_engine* e, int64_t n0, int64_t n1, uint32_t* out) {
   AV_CHECK(out && n0 >= 0 && n0 <= n1 && n1 <= e->N, AV_ERR_INVALID_ARG, "bad range");
   const size_t words = (size_t)(n1 - n0) * e->BL;
   if (!words) return AV_OK;
-  AV_HIP(hipMemcpyAsync(out, e->pref[e->cur] + (size_t)n0 * e->BL, words * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpy2DAsync(out, (size_t)e->BL * 4, e->pref[e->cur] + (size_t)n0 * e->PS, (size_t)e->PS * 4,
+                          (size_t)e->BL * 4, (size_t)(n1 - n0), hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
   return AV_OK;
 }
@@ -1700,9 +1711,9 @@ int av_comm_init(av_engine* e, int32_t world, int32_t rank, const uint8_t id[128
   e->world = world;
   e->rank = rank;
   // make every rank's initial preference rows visible everywhere
-  const size_t count = (size_t)e->NL * e->BL;
+  const size_t count = (size_t)e->NL * e->PS;
   uint32_t* cur = e->pref[e->cur];
-  r = ncclAllGather(cur + (size_t)e->n0 * e->BL, cur, count, ncclUint32, e->comm, e->stream);
+  r = ncclAllGather(cur + (size_t)e->n0 * e->PS, cur, count, ncclUint32, e->comm, e->stream);
   AV_CHECK(r == ncclSuccess, AV_ERR_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
   AV_HIP(hipStreamSynchronize(e->stream));
   return AV_OK;

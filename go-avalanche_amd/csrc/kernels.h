@@ -43,10 +43,19 @@ __host__ __device__ inline size_t replay_idx(uint32_t g, int k, int j, int c) {
   return (((size_t)(g >> 6) * replay_groups(k) + (size_t)(j >> 1)) * 64u + (g & 63u)) * 4u + (size_t)((j & 1) * 2 + c);
 }
 
+// Words per node row of the published-preference tables: BL rounded up to a
+// power of two (BL <= 32) or to a multiple of 32 (BL > 32), so that the k
+// rows a node gathers each round start on 128-B line boundaries (an
+// unaligned 63-word row touches 3 lines instead of 2). Padding words are
+// never read.
+__host__ __device__ constexpr uint32_t pref_stride(uint32_t BL) {
+  return BL > 32u ? (BL + 31u) / 32u * 32u : (BL <= 1u ? 1u : 1u << (32 - __builtin_clz(BL - 1u)));
+}
+
 struct RoundParams {
   uint32_t* planes;
-  const uint32_t* pref_in;   // [N_pad][BL] published preference (round start)
-  uint32_t* pref_out;        // [N_pad][BL] published preference (round end)
+  const uint32_t* pref_in;   // [N_pad][PS] published preference (round start)
+  uint32_t* pref_out;        // [N_pad][PS] published preference (round end)
   const uint32_t* valid;     // [BL] Target.IsValid() bits
   const uint32_t* byz;       // [ceil(N/32)] Byzantine node bits
   const uint32_t* replay;    // replay mode: yes/consider words of each lane and slot (replay_idx)
@@ -80,6 +89,7 @@ struct RoundParams {
   uint32_t n0;               // first local node (global id)
   uint32_t NL;               // local nodes
   uint32_t BL;               // local blocks per node
+  uint32_t PS;               // words per node row of the preference tables (pref_stride(BL))
   uint32_t L;                // lanes = NL * BL
   uint32_t Lpad;             // tiles * 64
   uint32_t t0;               // first local target (global id, multiple of 32)
@@ -109,7 +119,7 @@ struct RoundParams {
   // (after 8 sim votes every consider bit of the tile is 1; no record of the
   // tile is live-but-invalid) and read as all-ones until written back.
   uint32_t* vstale;
-  const uint32_t* pref_prev; // [N_pad][BL] snapshot of round - 1 (read by stale tiles)
+  const uint32_t* pref_prev; // [N_pad][PS] snapshot of round - 1 (read by stale tiles)
   // Peer-push exchange (node-sharded engines, k_round_sweep only):
   // every replica of a snapshot buffer is identical between rounds, so the
   // word a lane is about to overwrite in its own row of pref_out is also what
@@ -221,10 +231,10 @@ hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, u
 
 struct InitParams {
   uint32_t* planes;
-  uint32_t* pref;       // [N_pad][BL]
+  uint32_t* pref;       // [N_pad][PS]
   const uint32_t* byz;
   uint64_t seed;
-  uint32_t n_nodes, n0, NL, BL, L, Lpad, t0, n_targets, round;
+  uint32_t n_nodes, n0, NL, BL, PS, L, Lpad, t0, n_targets, round;
   int32_t mode;
   uint32_t param;
   uint32_t pub_mode;    // RoundParams::pub_mode
@@ -241,7 +251,7 @@ struct DropInParams {
   const uint32_t* offs;    // [n_blocks + 1] into entries
   const uint32_t* entries; // pairs (pos, meta = bit | yes<<5 | considered<<6)
   int32_t* status_out;     // per vote position, -1 = no update
-  uint32_t n_blocks, n0, BL, round;
+  uint32_t n_blocks, n0, BL, PS, round;
   uint32_t pub_mode;
 };
 hipError_t launch_register_votes(const DropInParams& p, hipStream_t s);
@@ -254,7 +264,7 @@ struct AddParams {
   const uint32_t* targets;  // local target index
   const uint8_t* accepted;
   uint8_t* added;
-  uint32_t n, node_local, node, BL, round;
+  uint32_t n, node_local, node, BL, PS, round;
   uint32_t pub_mode;
 };
 hipError_t launch_add_targets(const AddParams& p, hipStream_t s);
@@ -292,7 +302,7 @@ hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uin
 // records queried this round that their responder did not hold.
 hipError_t launch_readd(const RoundParams& p, hipStream_t s);
 hipError_t launch_refresh_pref(uint32_t pub_mode, const uint32_t* planes, uint32_t* pref, const uint32_t* byz,
-                               uint32_t n0, uint32_t NL, uint32_t BL, uint32_t round, hipStream_t s);
+                               uint32_t n0, uint32_t NL, uint32_t BL, uint32_t PS, uint32_t round, hipStream_t s);
 hipError_t launch_sample_peers(uint64_t seed, uint32_t n_nodes, uint32_t a, uint32_t b, uint32_t round,
                                int k, int mode, uint32_t* out, hipStream_t s);
 hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t BL, uint32_t L, uint32_t Lpad,

@@ -65,7 +65,7 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
       // peer's published preference; the ablation (timing diagnostics only,
       // results invalid) reads the node's own row instead: coalesced, same count
       const uint32_t src = p.ablate_gather ? (node ^ (uint32_t)j) % p.n_nodes : peers[j];
-      w[j] = active ? p.pref_in[(size_t)src * p.BL + b] : 0u;
+      w[j] = active ? p.pref_in[(size_t)src * p.PS + b] : 0u;
       cw[j] = ~0u;  // honest/Byzantine votes are 0 or 1
       peer_of[j] = src - p.n0;  // local row of the peer (responder re-adds: single-engine networks only)
     }
@@ -120,7 +120,7 @@ __device__ __forceinline__ void round_fast_body(const RoundParams& p, uint32_t g
       for (int i = 0; i < 8; ++i) pst<NT>(tile + plane_off(kPC + i, lane), (s.C[i] & alive) | (Co[i] & keep) | dead);
     }
     pst<NT>(tile + plane_off(kPA, lane), s.A);
-    p.pref_out[(size_t)node * p.BL + b] =
+    p.pref_out[(size_t)node * p.PS + b] =
         is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : publish_word(s.A, s.K[7], p.pub_mode);
   }
   const uint32_t wave_id = g >> 6;
@@ -214,7 +214,7 @@ __device__ __forceinline__ void capped_node(const RoundParams& p, uint32_t nl, u
     sample_peers<K>(p.seed, node, p.round, p.n_nodes, p.peer_mode, peers);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      w[j] = active ? p.pref_in[(size_t)peers[j] * p.BL + b] : 0u;
+      w[j] = active ? p.pref_in[(size_t)peers[j] * p.PS + b] : 0u;
       cw[j] = ~0u;
     }
   }
@@ -258,7 +258,7 @@ __device__ __forceinline__ void capped_node(const RoundParams& p, uint32_t nl, u
       s.C[i] |= died;
     }
     store_state(p.planes, g, s);
-    p.pref_out[(size_t)node * p.BL + b] =
+    p.pref_out[(size_t)node * p.PS + b] =
         is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : publish_word(s.A, s.K[7], p.pub_mode);
   }
   const uint32_t wave_id = nl * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
@@ -303,7 +303,7 @@ __global__ void k_register_votes(const DropInParams p) {
     s.C[q] |= died;
   }
   store_state(p.planes, g, s);
-  p.pref[(size_t)node * p.BL + b] =
+  p.pref[(size_t)node * p.PS + b] =
       is_byz(p.byz, node) ? byz_pattern(p.round) : publish_word(s.A, s.K[7], p.pub_mode);
 }
 
@@ -329,7 +329,7 @@ __global__ void k_add_targets(const AddParams p) {
     uint32_t* a = pw(p.planes, g, kPA);
     *a = p.accepted[i] ? (*a | m) : (*a & ~m);
     p.added[i] = 1;
-    p.pref[(size_t)p.node * p.BL + b] = is_byz(p.byz, p.node) ? byz_pattern(p.round)
+    p.pref[(size_t)p.node * p.PS + b] = is_byz(p.byz, p.node) ? byz_pattern(p.round)
                                                                : publish_word(*a, *pw(p.planes, g, kPK + 7), p.pub_mode);
   }
 }
@@ -391,6 +391,7 @@ __global__ void k_init_pref(const InitParams p) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)p.n_nodes * p.BL) return;
   const uint32_t node = (uint32_t)(i / p.BL), b = (uint32_t)(i - (size_t)node * p.BL);
+  const size_t o = (size_t)node * p.PS + b;
   const uint32_t tb = p.t0 + 32u * b;
   uint32_t v;
   if (is_byz(p.byz, node))
@@ -398,7 +399,7 @@ __global__ void k_init_pref(const InitParams p) {
   else
     v = p.mode == 0 ? (p.pub_mode == 2u ? target_mask(tb, p.n_targets) : 0u)  // no records (K7 set)
                     : (init_accept_block(p.seed, p.mode, p.param, node, tb) & target_mask(tb, p.n_targets));
-  p.pref[i] = v;
+  p.pref[o] = v;
 }
 
 __global__ void k_byz(uint32_t* byz, uint32_t n_nodes, uint64_t seed, uint32_t threshold) {
@@ -463,7 +464,7 @@ __global__ __launch_bounds__(256) void k_read_records_v(const RoundParams p, uin
     uint32_t pp[8];
     sample_peers<8>(p.seed, p.n0 + nl, p.round - 1u, p.n_nodes, p.peer_mode, pp);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) s.V[q] = p.pref_prev[pp[7 - q] * p.BL + b];
+    for (int q = 0; q < 8; ++q) s.V[q] = p.pref_prev[pp[7 - q] * p.PS + b];
   } else if (st == kVUniform) {  // every polled record's vote register = its accepted bit
 #pragma unroll
     for (int q = 0; q < 8; ++q) s.V[q] = s.A;
@@ -536,11 +537,11 @@ __global__ void k_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uin
 }
 
 __global__ void k_refresh_pref(uint32_t pub_mode, const uint32_t* planes, uint32_t* pref, const uint32_t* byz,
-                               uint32_t n0, uint32_t NL, uint32_t BL, uint32_t round) {
+                               uint32_t n0, uint32_t NL, uint32_t BL, uint32_t PS, uint32_t round) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= NL * BL) return;
   const uint32_t nl = g / BL, b = g - nl * BL, node = n0 + nl;
-  pref[(size_t)node * BL + b] =
+  pref[(size_t)node * PS + b] =
       is_byz(byz, node) ? byz_pattern(round) : publish_word(*pw(planes, g, kPA), *pw(planes, g, kPK + 7), pub_mode);
 }
 
@@ -832,11 +833,11 @@ hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uin
 }
 
 hipError_t launch_refresh_pref(uint32_t pub_mode, const uint32_t* planes, uint32_t* pref, const uint32_t* byz,
-                               uint32_t n0, uint32_t NL, uint32_t BL, uint32_t round, hipStream_t s) {
+                               uint32_t n0, uint32_t NL, uint32_t BL, uint32_t PS, uint32_t round, hipStream_t s) {
   const uint32_t n = NL * BL;
   if (!n) return hipSuccess;
   hipLaunchKernelGGL(k_refresh_pref, dim3((n + 255) / 256), dim3(256), 0, s, pub_mode, planes, pref, byz, n0, NL, BL,
-                     round);
+                     PS, round);
   return hipGetLastError();
 }
 

@@ -75,7 +75,7 @@ __device__ __forceinline__ void node_lane_load(const RoundParams& p, uint32_t* t
     uint32_t peers[K];
     draw_peers<K>(p, p.round, node, nl, nl, 1u, lane, peers);  // every lane of the workgroup is the same node
 #pragma unroll
-    for (int j = 0; j < K; ++j) in.w[j] = p.pref_in[peers[j] * p.BL + bc];  // < N * BL < 2^31 (engine check)
+    for (int j = 0; j < K; ++j) in.w[j] = p.pref_in[peers[j] * p.PS + bc];  // < N * BL < 2^31 (engine check)
   }
 }
 
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(MAXT) void k_round_node(const RoundParams p) {
     return;
   }
   const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
-  const uint32_t prow = node * p.BL + b;
+  const uint32_t prow = node * p.PS + b;
   const uint32_t pub_byz = is_byz(p.byz, node) ? 1u : 0u;
   if (!heavy) {  // nothing polled in this wave: records unchanged, A republished
     if (active) p.pref_out[prow] = pub_byz ? byz_pattern(p.round + 1u) : A;
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
     Kp[4 + i] = k1[i];
   }
   const uint32_t wave_id = blockIdx.x * (blockDim.x >> 6) + wave;  // dense: matches log_shards sizing
-  const uint32_t prow = node * p.BL + b;
+  const uint32_t prow = node * p.PS + b;
   const bool byz = is_byz(p.byz, node);
   const uint32_t R = p.fuse_rounds;
   // A count grows by at most K per round, so no polled record can reach 120

@@ -157,7 +157,7 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
     // the gathers address the preference table by 32-bit byte offsets (SGPR
     // base + VGPR offset: one add per gather): the engine runs the sweep only
     // for tables below 4 GiB (N * BL < 2^30)
-    const uint32_t rb = p.BL * 4u, bo = x.b * 4u;
+    const uint32_t rb = p.PS * 4u, bo = x.b * 4u;
     uint32_t rows[K];  // byte offsets of the peers' rows
     bool drawn = false, have_rows = false;
     if constexpr (VV) {
@@ -182,9 +182,9 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
           uint32_t pp[K];
           pick_peers(p, pd, 0u, p.round, x.node, x.nl, nlA, nn, lane, pp);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) in.v0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
+          for (int i = 0; i < 4; ++i) in.v0[i] = p.pref_prev[pp[7 - i] * p.PS + x.b];
 #pragma unroll
-          for (int i = 0; i < 3; ++i) in.v1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
+          for (int i = 0; i < 3; ++i) in.v1[i] = p.pref_prev[pp[3 - i] * p.PS + x.b];
           in.v1[3] = 0u;
         }
         pick_peers(p, pd, 1u, p.round, x.node, x.nl, nlA, nn, lane, peers);
@@ -551,7 +551,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
       st4<POL>(tr, grp + 192, 3072u + lane * 16u, o3);
     }
     if (astore) st1<POL>(tr, tp + 1536u + lane, (1536u + lane) * 4u, A);
-    const uint32_t prow = node * p.BL + b;  // < N * BL < 2^31
+    const uint32_t prow = node * p.PS + b;  // < N * PS < 2^31
     const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
     if (p.push_n) {
       // peer-push exchange (kernels.h): the word being overwritten is what
@@ -640,7 +640,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
                              : *reinterpret_cast<const uint32_t*>(ta + ao);
   const uint32_t P0 = active ? at_byte(p.valid, b * 4u) : 0u;  // polled = live (kPendAllLive) and valid
   uint32_t rows[8];
-  pick_parked(p, wd.sd, wd.bad, (nl - wd.nlA) * 2u + (wd.pair ? 32u : 0u), p.n0 + nl, p.round, p.BL * 4u, rows);
+  pick_parked(p, wd.sd, wd.bad, (nl - wd.nlA) * 2u + (wd.pair ? 32u : 0u), p.n0 + nl, p.round, p.PS * 4u, rows);
   const uint32_t bo = b * 4u;
   uint32_t dis = 0u;
 #pragma unroll
@@ -652,7 +652,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   if (__ballot(((dis ^ A) | (all ^ A)) & P0) != 0ull) return false;
   if (active) {
     const uint32_t node = p.n0 + nl;
-    const uint32_t prow = node * p.BL + b;  // < N * BL < 2^30 (sweep gate)
+    const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
     const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
     if (p.push_n) {  // peer-push exchange: as process_tile
       const uint32_t old = p.pref_out[prow];
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           wd.ok = !d.fallback;
           wd.bad = d.bad;
           wd.sd = s_draw[threadIdx.x >> 6];
-          if (wd.ok) park_draw(d, s_draw[threadIdx.x >> 6], lane, p.BL * 4u);
+          if (wd.ok) park_draw(d, s_draw[threadIdx.x >> 6], lane, p.PS * 4u);
         }
       }
     }
@@ -866,8 +866,8 @@ __global__ __launch_bounds__(256) void k_vv_materialize(const RoundParams p) {
     draw_peers<8>(p, p.round - 1u, x.node, x.nl, nlA, nn, lane, pp);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      o0[i] = p.pref_prev[pp[7 - i] * p.BL + x.b];
-      o1[i] = p.pref_prev[pp[3 - i] * p.BL + x.b];
+      o0[i] = p.pref_prev[pp[7 - i] * p.PS + x.b];
+      o1[i] = p.pref_prev[pp[3 - i] * p.PS + x.b];
     }
   }
   if (x.active) {
