@@ -68,6 +68,16 @@ struct av_engine {
   // words per node row of the preference tables: BL rounded up to a power of two (BL <= 32) or to a
   // multiple of 32 (BL > 32), so that a gathered row covers whole 128-B lines (avk::pref_stride)
   uint32_t PS = 0;
+  // reference rows (kernels.h ref_node / rflag_*): one flag byte per node after the preference words
+  // of every snapshot buffer (so rotation, IPC export and peer pushes carry them); rflag_ok[b]: the
+  // flags of buffer b were written by the round that wrote its rows, against ref_node's row of the
+  // buffer that round read, and nothing has written either buffer since
+  // option "ref_rows" (default off: measured slower): the flag loads, the reference
+  // word and the writer's ballot + byte store cost more issue/latency than the 8 gathers they replace
+  bool ref_rows = false;
+  int64_t ref_node = -1;  // first honest node (chosen at the first round that can use it); -2: none
+  size_t rflag_off = 0;   // byte offset of the flags in a snapshot buffer
+  bool rflag_ok[3] = {false, false, false};
   int cur = 0;
   static int nxt(int c) { return c == 2 ? 0 : c + 1; }
   static int prv(int c) { return c == 0 ? 2 : c - 1; }
@@ -223,6 +233,11 @@ struct Scratch {
     return e;
   }
 };
+
+// Anything but a reference-row sweep round that writes a snapshot buffer
+// (drop-in votes, adds, writes, init, validity/publish-rule refreshes, peer
+// and RCCL set-up, other round kernels) leaves its flags stale.
+void ref_invalidate(av_engine* e) { e->rflag_ok[0] = e->rflag_ok[1] = e->rflag_ok[2] = false; }
 
 avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   avk::RoundParams p{};
@@ -380,6 +395,23 @@ int engine_scratch(av_engine* e, size_t bytes, void** out) {
   return AV_OK;
 }
 
+// The reference node: the first honest node (a Byzantine row changes every
+// round and would never match).
+int ref_pick(av_engine* e) {
+  if (e->ref_node != -1) return AV_OK;
+  e->ref_node = -2;
+  const size_t words = std::min<size_t>((e->N + 31) / 32, 1024);
+  std::vector<uint32_t> w(words);
+  AV_HIP(hipMemcpyAsync(w.data(), e->byz, words * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipStreamSynchronize(e->stream));
+  for (size_t i = 0; i < words && e->ref_node < 0; ++i)
+    if (~w[i]) {
+      const int64_t n = (int64_t)i * 32 + __builtin_ctz(~w[i]);
+      if (n < e->N) e->ref_node = n;
+    }
+  return AV_OK;
+}
+
 int launch_one_round(av_engine* e, const uint32_t* replay) {
   AV_CHECK(e->round - e->log_base < 4096, AV_ERR_OVERFLOW,
            "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
@@ -435,14 +467,29 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     p.push_n = (uint32_t)e->peer_world - 1u;
     p.push_dst = e->push_tbl + (size_t)nb * avk::kMaxPeers;
   }
+  // reference rows: sweep rounds at k = 8 with a node's lanes inside one wave
+  bool refr = e->ref_rows && sweep && e->k == 8 && !replay && 64 % e->BL == 0 && !e->comm && !e->ablate_gather;
+  if (refr) {
+    int rc = ref_pick(e);
+    if (rc != AV_OK) return rc;
+    refr = e->ref_node >= 0;
+  }
+  if (refr) {
+    p.ref_node = (uint32_t)e->ref_node;
+    p.ps_shift = (uint32_t)__builtin_ctz(e->PS * 4u);
+    p.rflag_off = (uint32_t)e->rflag_off;
+    p.rflag_out = reinterpret_cast<uint8_t*>(e->pref[nb]) + e->rflag_off;
+    p.rflag_in = e->rflag_ok[e->cur] ? reinterpret_cast<const uint8_t*>(e->pref[e->cur]) + e->rflag_off : nullptr;
+  }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (e->timing) {
     AV_HIP(hipEventCreate(&ev0));
     AV_HIP(hipEventCreate(&ev1));
     AV_HIP(hipEventRecord(ev0, e->stream));
   }
+  bool refw = false;  // the round wrote reference-row flags for the snapshot it published
   if (sweep)
-    AV_HIP(avk::launch_round_sweep(p, e->k, replay != nullptr, e->sweep_blocks, e->stream));
+    AV_HIP(avk::launch_round_sweep(p, e->k, replay != nullptr, e->sweep_blocks, e->stream, &refw));
   else if (e->kernel == 2 && e->k <= 8 && e->capped && !compat) {
     p.node_flags = e->node_flags;
     AV_HIP(avk::launch_round_node(p, e->k, replay != nullptr, /*exact_pass=*/e->count_bound >= 120, e->stream));
@@ -456,6 +503,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   }
   e->count_bound = std::min(127, e->count_bound + e->k);
   e->fresh = false;
+  e->rflag_ok[nb] = refr && refw;
   if (replay)
     e->warm_all = false;
   else if (e->c_monotone && e->k >= 8 && !e->capped && all_valid)
@@ -490,6 +538,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
 // launch, followed per round by the exact pass over the nodes it left at that
 // round (count >= 120). Host-side round bookkeeping as launch_one_round.
 int launch_replay_fused(av_engine* e, const uint32_t* replay0, int32_t R) {
+  if (e) ref_invalidate(e);
   AV_CHECK(e->round + R - 1 - e->log_base < 4096, AV_ERR_OVERFLOW,
            "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
   int rc = materialize_votes_only(e);
@@ -551,7 +600,9 @@ uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
   return (uint32_t)std::max<uint64_t>(1, (waves + 3) / 4);
 }
 
+
 int refresh_pref(av_engine* e) {
+  ref_invalidate(e);
   AV_HIP(avk::launch_refresh_pref((uint32_t)e->pub_mode, e->planes, e->pref[e->cur], e->byz, (uint32_t)e->n0, e->NL,
                                   e->BL, e->PS, (uint32_t)e->round, e->stream));
   return AV_OK;
@@ -677,7 +728,8 @@ int av_create(const av_config* cfg, av_engine** out) {
   e->log_cap = (uint32_t)std::max<int64_t>((cap + e->log_shards - 1) / e->log_shards, 64);
   if ((he = dev_alloc(&e->planes, plane_words)) != hipSuccess) return hip_fail(he, "alloc planes");
   // whole 2-MiB units: each snapshot buffer is an allocation of its own (IPC export, av_peer_handles)
-  const size_t pref_alloc = ((pref_words * 4 + (2u << 20) - 1) / (2u << 20)) * (2u << 20) / 4;
+  e->rflag_off = (pref_words * 4 + 255) / 256 * 256;
+  const size_t pref_alloc = ((e->rflag_off + (size_t)e->N + (2u << 20) - 1) / (2u << 20)) * (2u << 20) / 4;
   e->pref_alloc_words = pref_alloc;
   if ((he = dev_alloc(&e->pref[0], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->pref[1], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
@@ -714,9 +766,9 @@ int av_create(const av_config* cfg, av_engine** out) {
   (void)hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
   (void)hipMemsetAsync(e->applied, 0, avk::kLogShards * 8, e->stream);
-  (void)hipMemsetAsync(e->pref[0], 0, pref_words * 4, e->stream);
-  (void)hipMemsetAsync(e->pref[1], 0, pref_words * 4, e->stream);
-  (void)hipMemsetAsync(e->pref[2], 0, pref_words * 4, e->stream);
+  (void)hipMemsetAsync(e->pref[0], 0, e->pref_alloc_words * 4, e->stream);
+  (void)hipMemsetAsync(e->pref[1], 0, e->pref_alloc_words * 4, e->stream);
+  (void)hipMemsetAsync(e->pref[2], 0, e->pref_alloc_words * 4, e->stream);
   // every real target starts valid
   e->valid_host.assign(e->BL, 0u);
   for (uint32_t b = 0; b < e->BL; ++b) {
@@ -741,6 +793,7 @@ int av_create(const av_config* cfg, av_engine** out) {
 }
 
 int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
+  if (e) ref_invalidate(e);
   AV_ENTER(e);
   e->warm_all = false;
   e->count_bound = 0;  // every record starts at count 0 (NewVoteRecord, vote.go:33-35)
@@ -782,6 +835,7 @@ int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
 }
 
 int av_set_valid(av_engine* e, int64_t target, int32_t valid) {
+  if (e) ref_invalidate(e);
   AV_ENTER(e);
   AV_CHECK(target >= 0 && target < e->M, AV_ERR_INVALID_ARG, "target out of range");
   if (!local_target(e, target)) return AV_OK;
@@ -797,6 +851,7 @@ int av_set_valid(av_engine* e, int64_t target, int32_t valid) {
 
 int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uint8_t* accepted, int64_t n,
                    uint8_t* added) {
+  if (e) ref_invalidate(e);
   AV_ENTER(e);
   {
     int rc = peer_local_write_check(e);
@@ -917,12 +972,14 @@ int register_votes_device(av_engine* e, const std::vector<std::pair<uint32_t, ui
 
 int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const uint32_t* errs, int64_t n,
                       int32_t* status_out) {
+  if (e) ref_invalidate(e);
   const int64_t offs[2] = {0, n};
   return av_register_votes_batch(e, 1, &node, offs, targets, errs, status_out);
 }
 
 int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, const int64_t* offsets,
                             const int64_t* targets, const uint32_t* errs, int32_t* status_out) {
+  if (e) ref_invalidate(e);
   AV_ENTER(e);
   {
     int rc = peer_local_write_check(e);
@@ -1048,6 +1105,7 @@ int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1
 }
 
 int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, const uint32_t* in) {
+  if (e) ref_invalidate(e);
   AV_ENTER(e);
   {
     int rc = peer_local_write_check(e);
@@ -1268,6 +1326,7 @@ int av_set_round(av_engine* e, int64_t node, int64_t round) {
 }
 
 int av_set_polling(av_engine* e, int64_t node, int32_t polls) {
+  if (e) ref_invalidate(e);
   AV_ENTER(e);
   AV_CHECK(local_node(e, node), AV_ERR_INVALID_ARG, "node %lld not in this shard", (long long)node);
   AV_CHECK(e->peer_world <= 1, AV_ERR_UNSUPPORTED, "av_set_polling on a peer-push engine");
@@ -1565,12 +1624,15 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
 }
 
 int av_set_option(av_engine* e, const char* name, int64_t value) {
+  if (e) ref_invalidate(e);
   AV_CHECK(e && name, AV_ERR_INVALID_ARG, "null argument");
   const std::string n(name);
   if (n == "plane_nt") {
     e->plane_nt = value != 0;
   } else if (n == "ablate_emit") {
     e->ablate_emit = (int)std::max<int64_t>(0, std::min<int64_t>(2, value));
+  } else if (n == "ref_rows") {  // reference-row flags in converged sweep rounds (kernels.h)
+    e->ref_rows = value != 0;
   } else if (n == "replay_fuse") {  // replay rounds per fused launch on capped engines (<= 1: one launch per round)
     AV_CHECK(value >= 0 && value <= 4096, AV_ERR_INVALID_ARG, "replay_fuse must be in [0, 4096]");
     e->replay_fuse = (int)value;
@@ -1699,6 +1761,7 @@ int av_comm_unique_id(uint8_t out[128]) {
 }
 
 int av_comm_init(av_engine* e, int32_t world, int32_t rank, const uint8_t id[128]) {
+  if (e) ref_invalidate(e);
   AV_ENTER(e);
   AV_CHECK(id && world >= 1 && rank >= 0 && rank < world, AV_ERR_INVALID_ARG, "bad world/rank");
   AV_CHECK(e->N % world == 0 && (int64_t)e->NL * world == e->N && e->n0 == (int64_t)rank * e->NL,
@@ -1772,6 +1835,7 @@ int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]) {
 }
 
 int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handles) {
+  if (e) ref_invalidate(e);
   AV_ENTER(e);
   AV_CHECK(handles && world >= 1 && world <= avk::kMaxPeers + 1 && rank >= 0 && rank < world, AV_ERR_INVALID_ARG,
            "bad world/rank (at most %d ranks)", avk::kMaxPeers + 1);

@@ -143,6 +143,17 @@ struct RoundParams {
   // applies the tiles' pending steps itself before it tests for count 120
   // (instead of a separate write-back pass) and clears kpend.
   uint32_t kconsume;
+  // Reference rows (converged networks; k_round_sweep with BL dividing 64, so a node's lanes sit in
+  // one wave): rflag_out[node] = 1 iff the row the node publishes into pref_out equals node
+  // ref_node's row in pref_in (written for every node by every such round); rflag_in = the same
+  // flags of pref_in, against ref_node's row in pref_prev. A settled-tile candidate whose 8 peers
+  // are all flagged reads that reference row once instead of gathering 8 peer rows: each of them
+  // IS the reference row, bit for bit. nullptr: not used / not written.
+  uint32_t ref_node;
+  uint32_t ps_shift;         // log2(PS * 4): peer index of a row byte offset
+  const uint8_t* rflag_in;
+  uint8_t* rflag_out;
+  uint32_t rflag_off;        // byte offset of the flag bytes in every snapshot buffer (peer pushes)
   // fresh: the round right after av_init_records: every record is a
   // NewVoteRecord (votes = consider = 0, count 0, vote.go:33-35), so the
   // kernel reads only the A plane; the live mask of a block is its existing
@@ -201,7 +212,9 @@ hipError_t launch_round(const RoundParams& p, int k, bool replay, bool capped, h
 hipError_t launch_replay_node(const RoundParams& p, int k, hipStream_t s);
 // Persistent streaming round kernel (round_sweep.hip), uncapped path, k <= 8:
 // `blocks` workgroups of 256 threads sweep the tiles; 0 = one wave per tile.
-hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s);
+// ref_written (may be null): whether the launch wrote p.rflag_out (only the walking warm mode does)
+hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s,
+                              bool* ref_written = nullptr);
 // Capped round (M > 4096, k <= 8; round_node.hip): one workgroup per node;
 // nodes that may finalize a record this round are flagged in p.node_flags and
 // left to the exact pass (k_round_capped over the flagged nodes only), which

@@ -364,7 +364,29 @@ __device__ __forceinline__ uint32_t emit_updates_lds(const RoundParams& p, uint3
 
 // The round step of one loaded tile. WARM: consider planes all-ones (neither
 // loaded nor stored; sim votes only). POL: plane-stream cache policy.
-template <int K, bool REPLAY, bool WARM, int POL, bool VVM = false, bool LE = false>
+// Reference-row flag of the node whose lanes include this one (kernels.h
+// rflag_out): every lane of the node published REF's word. BL divides 64, so
+// the node's lanes are the aligned BL-lane segment of this wave that holds
+// the lane; the node's block-0 lane stores the byte (and pushes it to the
+// peers' replicas when it changed, as the published words).
+__device__ __forceinline__ void ref_flag_store(const RoundParams& p, uint32_t lane, bool active, uint32_t b,
+                                               uint32_t node, uint32_t pub) {
+  const uint32_t ref = p.pref_in[p.ref_node * p.PS + (active ? b : 0u)];
+  const uint64_t eq = __ballot(!active || pub == ref);
+  const uint32_t s0 = lane - b;  // the node's first lane (active lanes only)
+  const uint64_t seg = (p.BL >= 64u ? ~0ull : ((1ull << p.BL) - 1ull)) << (s0 & 63u);
+  if (active && b == 0u) {
+    const uint8_t f = (eq & seg) == seg ? 1u : 0u;
+    if (p.push_n && p.rflag_out[node] != f) {
+      for (uint32_t r = 0; r < p.push_n; ++r)
+        __hip_atomic_store(reinterpret_cast<uint8_t*>(p.push_dst[r]) + p.rflag_off + node, f, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    p.rflag_out[node] = f;
+  }
+}
+
+template <int K, bool REPLAY, bool WARM, int POL, bool VVM = false, bool LE = false, bool REF = false>
 __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
                                              const TileIn<K, REPLAY, WARM>& in, uint32_t extra_bytes, SweepAcc& acc,
                                              uint32_t* es) {
@@ -570,6 +592,10 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
   }
+  if (REF && p.rflag_out) {  // reference-row flag of the row just published (kernels.h)
+    ref_flag_store(p, lane, active, b, node, is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A);
+    if (active) acc.lane_bytes += 4u + (b == 0u ? 1u : 0u);
+  }
   if constexpr (VVM && !REPLAY && K == 8) {
     // a settled tile's 8 new votes all equal its accepted plane on the polled
     // records: its vote register is A next round (no regather)
@@ -625,7 +651,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
 // more): no flip, no StatusUpdate, no deletion, V stays uniform, A and K
 // unchanged. This reads A, the validity word and the 8 votes and does exactly
 // that; any other tile returns false and takes the general load + step.
-template <int POL>
+template <int POL, bool REF>
 __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile, uint32_t lane, uint32_t kw,
                                              const WaveDraw& wd, SweepAcc& acc) {
   const uint32_t g = tile * 64u + lane;
@@ -642,18 +668,35 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   uint32_t rows[8];
   pick_parked(p, wd.sd, wd.bad, (nl - wd.nlA) * 2u + (wd.pair ? 32u : 0u), p.n0 + nl, p.round, p.PS * 4u, rows);
   const uint32_t bo = b * 4u;
-  uint32_t dis = 0u;
+  uint32_t dis = 0u, all = ~0u;
+  bool gather = true;
+  uint32_t rbytes = 0u;  // reference-row reads
+  if (REF && p.rflag_in) {
+    // peers whose published row is the reference row (kernels.h rflag_in):
+    // when all 8 are, each of the 8 votes is that row's word (the reference
+    // word is loaded beside the flags, not after them)
+    const uint32_t rw = p.pref_prev[p.ref_node * p.PS + b];
+    uint32_t fl = 1u;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) dis |= at_byte(p.pref_in, rows[j] + bo);
-  uint32_t all = ~0u;
+    for (int j = 0; j < 8; ++j) fl &= p.rflag_in[rows[j] >> p.ps_shift];
+    rbytes = 4u + (b == 0u ? 8u : 0u);
+    if (fl) {
+      dis = all = rw;
+      gather = false;
+    }
+  }
+  if (gather) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) all &= at_byte(p.pref_in, rows[j] + bo);
+    for (int j = 0; j < 8; ++j) dis |= at_byte(p.pref_in, rows[j] + bo);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) all &= at_byte(p.pref_in, rows[j] + bo);
+  }
   // every vote equals A  <=>  (OR of votes) == A == (AND of votes) on P0
   if (__ballot(((dis ^ A) | (all ^ A)) & P0) != 0ull) return false;
+  const uint32_t node = p.n0 + nl;
+  const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
   if (active) {
-    const uint32_t node = p.n0 + nl;
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-    const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
     if (p.push_n) {  // peer-push exchange: as process_tile
       const uint32_t old = p.pref_out[prow];
       if (pub != old) {
@@ -664,12 +707,18 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
     const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, 0x7FFFFFFF, kRsrcWord3);
     st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
   }
+  if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub);
   if (lane == 0) p.kpend[tile] = ((kw & 0xFFu) + 1u) | kPendAllLive;
   acc.applied += 8u * (uint32_t)__popc(P0);
   // process_tile's accounting for this case: 17 plane words + 8 vote words +
   // valid read, minus V (uniform), V store (virtual), K read + store (deferred),
   // A store (unchanged) = 40 B per lane (+ 4 B push read); kpend read + write
-  acc.lane_bytes += (active ? 40u + (p.push_n ? 4u : 0u) : 0u) + (lane == 0 ? 8u : 0u);
+  // reference rows: 8 flag bytes per node read, the reference word instead of
+  // the 32 B of gathered votes, the next reference word + the flag written
+  acc.lane_bytes += (active ? 40u + (p.push_n ? 4u : 0u) + rbytes - (gather ? 0u : 32u) +
+                                  (REF && p.rflag_out ? 4u + (b == 0u ? 1u : 0u) : 0u)
+                            : 0u) +
+                    (lane == 0 ? 8u : 0u);
   return true;
 }
 
@@ -679,7 +728,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
 // the node's own row: timing diagnostics only, results invalid), kModeWarmPipe
 // (kModeWarm for a resident grid: the next tile's loads are issued before the
 // current tile is computed; 93 VGPRs, 5 waves per SIMD).
-template <int K, int MODE, int POL>
+template <int K, int MODE, int POL, bool REF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeReplay || MODE == kModeWarm || MODE == kModeFresh ? 6 : 7))) void k_round_sweep(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave0 = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -745,13 +794,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         if constexpr (K == 8) {
           if (wd.ok && p.settled_fast && p.klazy && p.vv) {
             const uint32_t m = meta_of(wd, tile);
-            if (((m >> 8) & kVMask) == kVUniform && (m & kPendAllLive) && settled_tile<POL>(p, tile, lane, m & 0x800000FFu, wd, acc))
+            if (((m >> 8) & kVMask) == kVUniform && (m & kPendAllLive) && settled_tile<POL, REF>(p, tile, lane, m & 0x800000FFu, wd, acc))
               continue;
           }
         }
         TileIn<K, false, true> in;
         load_tile<K, false, true, POL, false, true>(p, tile, lane, in, &wd);
-        process_tile<K, false, true, POL, true>(p, tile, lane, in, 0u, acc, es);
+        process_tile<K, false, true, POL, true, false, REF>(p, tile, lane, in, 0u, acc, es);
       } else if constexpr (MODE == kModeFresh) {
         TileIn<K, false, false> in;
         load_tile<K, false, false, POL, false, true, true>(p, tile, lane, in);
@@ -799,6 +848,16 @@ template <int K, int MODE>
 hipError_t launch_mode(const RoundParams& p, uint32_t grid, hipStream_t s) {
   // write-through store policies are built for k = 8 only (the measured workloads)
   const uint32_t pol = (K == 8 && p.store_policy >= 2) ? p.store_policy : (p.plane_nt ? 1u : 0u);
+  if constexpr (K == 8 && MODE == kModeWarm) {
+    // reference rows (kernels.h): the walking warm mode writes the flags and settled tiles read them
+    if (p.rflag_out) {
+      if (pol == 1)
+        hipLaunchKernelGGL((k_round_sweep<K, MODE, 1, true>), dim3(grid), dim3(256), 0, s, p);
+      else
+        hipLaunchKernelGGL((k_round_sweep<K, MODE, 0, true>), dim3(grid), dim3(256), 0, s, p);
+      return hipGetLastError();
+    }
+  }
   switch (pol) {
     case 0: hipLaunchKernelGGL((k_round_sweep<K, MODE, 0>), dim3(grid), dim3(256), 0, s, p); break;
     case 1: hipLaunchKernelGGL((k_round_sweep<K, MODE, 1>), dim3(grid), dim3(256), 0, s, p); break;
@@ -814,7 +873,8 @@ hipError_t launch_mode(const RoundParams& p, uint32_t grid, hipStream_t s) {
 }
 
 template <int K>
-hipError_t launch_sweep_k(const RoundParams& p_in, bool replay, uint32_t blocks, hipStream_t s) {
+hipError_t launch_sweep_k(const RoundParams& p_in, bool replay, uint32_t blocks, hipStream_t s, bool* ref_written) {
+  if (ref_written) *ref_written = false;
   const uint32_t need = (p_in.Lpad / 64u + 3u) / 4u;
   const uint32_t grid = std::max(1u, blocks ? std::min(blocks, need) : need);
   RoundParams p = p_in;
@@ -824,8 +884,13 @@ hipError_t launch_sweep_k(const RoundParams& p_in, bool replay, uint32_t blocks,
     const uint32_t tiles = p.Lpad / 64u, waves = grid * 4u;
     p.tpw = (tiles + waves - 1u) / waves;
     if (p.tpw > 16u) p.tpw = 0u;  // long runs: grid stride (their nodes overflow the shared draw anyway)
-    if (p.tpw) return launch_mode<K, kModeWarm>(p, grid, s);
+    if (p.tpw) {
+      if (ref_written) *ref_written = p.rflag_out != nullptr;
+      return launch_mode<K, kModeWarm>(p, grid, s);
+    }
   }
+  p.rflag_out = nullptr;  // only the walking warm mode writes reference-row flags
+  p.rflag_in = nullptr;
   if (replay) return launch_mode<K, kModeReplay>(p, grid, s);
   if (p.ablate_gather) return launch_mode<K, kModeAblate>(p, grid, s);
   if (p.fresh) return launch_mode<K, kModeFresh>(p, grid, s);
@@ -940,8 +1005,9 @@ hipError_t occupancy_k(bool replay, int* bpc) {
     default: return hipErrorInvalidValue; \
   }
 
-hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s) {
-#define AVK_SW(K) launch_sweep_k<K>(p, replay, blocks, s)
+hipError_t launch_round_sweep(const RoundParams& p, int k, bool replay, uint32_t blocks, hipStream_t s,
+                              bool* ref_written) {
+#define AVK_SW(K) launch_sweep_k<K>(p, replay, blocks, s, ref_written)
   AVK_SWEEP_SWITCH(k, AVK_SW)
 #undef AVK_SW
 }

@@ -246,8 +246,14 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  * of consecutive tiles and draws their peers once), "settled_fast" (1),
  * "sweep_nopipe" (1), "virtual_votes" (1), "vv_min_bl" (16), "count_lazy"
  * (1), "fresh" (1), "dense_min" (6 at k = 8: updates per lane that make a
- * dense log record). Diagnostics that make results invalid: "ablate_gather",
- * "ablate_emit" (StatusUpdates counted, not stored), "unsynced_shard". */
+ * dense log record), "ref_rows" (0; 1: in converged sweep rounds a settled
+ * tile whose 8 peers published the reference node's row reads that row once
+ * instead of gathering 8 copies of it; exact, measured slower), "replay_fuse" (16: replay
+ * rounds per k_replay_node launch on capped engines, <= 1 = one launch per
+ * round). Diagnostics that make results invalid: "ablate_gather",
+ * "ablate_emit" (StatusUpdates counted, not stored), "ablate_node"
+ * (k_round_node: 1 = lanes past the cap skipped, 4 = no plane stores),
+ * "unsynced_shard". */
 int av_set_option(av_engine* e, const char* name, int64_t value);
 
 /* ---- measurement ---- */
