@@ -92,7 +92,7 @@ for s in "$@"; do
     pmcb_write) step pmcb_write_${WL:-c4} 600 timeout -s KILL 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmcb_write_${WL:-c4} -o bench -- \
             python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary ;;
     pmcb_sum) step pmcb_sum_${WL:-c4} 300 python tools/pmc_bench.py --workload ${WL:-c4} --sq $OUT/pmcb_sq_${WL:-c4} --fetch $OUT/pmcb_fetch_${WL:-c4} \
-            --write $OUT/pmcb_write_${WL:-c4} --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write --out $OUT/pmc_${WL:-c4}.json ;;
+            --write $OUT/pmcb_write_${WL:-c4} --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write ${PMC_LAUNCHES:+--launches $PMC_LAUNCHES} --out $OUT/pmc_${WL:-c4}.json ;;
     pmc_fetch) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o bench -- \
             python3 bench.py --no-cpu-baseline --no-secondary ;;
     pmc_write) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o bench -- \

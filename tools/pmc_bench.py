@@ -34,7 +34,10 @@ import os
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROUND_KERNELS = ("k_round_sweep", "k_round_node", "k_round_fast", "k_round_capped")
+ROUND_KERNELS = ("k_round_sweep", "k_round_node", "k_replay_node", "k_round_fast", "k_round_capped")
+# the kernel a launch of the bench's roofline pass is counted by (k_round_capped also runs as the
+# exact pass behind k_round_node / k_replay_node)
+PRIMARY = ("k_round_sweep", "k_round_node", "k_replay_node", "k_round_fast")
 
 
 def dispatches(d):
@@ -52,18 +55,23 @@ def dispatches(d):
     return [(k, v[0], v[1]) for k, v in sorted(rows.items())]
 
 
-def window(d, steps):
+def window(d, launches):
+    """The round-kernel dispatches of the roofline pass: from the launches-th
+    last primary round kernel on (C2: k_replay_node launches with the exact
+    passes between them; otherwise one round kernel per step)."""
     rounds = [x for x in dispatches(d) if any(k in x[1] for k in ROUND_KERNELS)]
-    if len(rounds) < steps:
-        raise SystemExit(f"{d}: {len(rounds)} round-kernel dispatches, need {steps}")
-    return rounds[-steps:]
+    prim = [i for i, x in enumerate(rounds) if any(k in x[1] for k in PRIMARY)]
+    if len(prim) < launches:
+        raise SystemExit(f"{d}: {len(prim)} round-kernel launches, need {launches}")
+    return rounds[prim[-launches]:]
 
 
-def mean_of(win, counter):
+def mean_of(win, counter, launches):
+    """Per launch: the counter summed over the window's dispatches / launches."""
     vals = [c[counter] for _, _, c in win if counter in c]
     if len(vals) != len(win):
         raise SystemExit(f"counter {counter} missing in some dispatches")
-    return sum(vals) / len(vals)
+    return sum(vals) / launches
 
 
 def calib_ratio(d, needle, counter, true_bytes):
@@ -85,6 +93,8 @@ def main():
     ap.add_argument("--workload", default="c4")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=None,
+                    help="roofline-pass launches (default: steps; C2 fuses replay rounds: 2 at the defaults)")
     ap.add_argument("--sq", required=True)
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
@@ -100,18 +110,20 @@ def main():
     rw1 = calib_ratio(a.calib_write, "calib_write_dword", "WRITE_SIZE", a.calib_bytes)
     read_ratio, write_ratio = (rf + rf1) / 2, (rw + rw1) / 2
 
-    wf, ww, wq = window(a.fetch, a.steps), window(a.write, a.steps), window(a.sq, a.steps)
+    n = a.launches or a.steps
+    wf, ww, wq = window(a.fetch, n), window(a.write, n), window(a.sq, n)
     names = sorted({n for _, n, _ in wq})
-    read = mean_of(wf, "FETCH_SIZE") * 1024 / read_ratio
-    write = mean_of(ww, "WRITE_SIZE") * 1024 / write_ratio
-    cyc = mean_of(wq, "GRBM_GUI_ACTIVE") / 8.0
-    valu, salu = mean_of(wq, "SQ_INSTS_VALU"), mean_of(wq, "SQ_INSTS_SALU")
+    read = mean_of(wf, "FETCH_SIZE", n) * 1024 / read_ratio
+    write = mean_of(ww, "WRITE_SIZE", n) * 1024 / write_ratio
+    cyc = mean_of(wq, "GRBM_GUI_ACTIVE", n) / 8.0
+    valu, salu = mean_of(wq, "SQ_INSTS_VALU", n), mean_of(wq, "SQ_INSTS_SALU", n)
     out = {
         "workload": a.workload,
         "window": f"{a.warmup}+{a.steps}",
         "src_sha": bench_src_digest(),
         "kernels": names,
         "dispatches": len(wq),
+        "launches": n,
         "calibration_measured_over_true": {"read_x4": rf, "read_x1": rf1, "write_x4": rw, "write_x1": rw1},
         "hbm_read_bytes_per_launch": read,
         "hbm_write_bytes_per_launch": write,
@@ -120,19 +132,19 @@ def main():
             "cycles_per_launch": cyc,
             "valu_per_launch": valu,
             "salu_per_launch": salu,
-            "vmem_rd_per_launch": mean_of(wq, "SQ_INSTS_VMEM_RD"),
-            "vmem_wr_per_launch": mean_of(wq, "SQ_INSTS_VMEM_WR"),
-            "lds_per_launch": mean_of(wq, "SQ_INSTS_LDS"),
-            "waves_per_launch": mean_of(wq, "SQ_WAVES"),
-            "wait_any_frac": mean_of(wq, "SQ_WAIT_ANY") / max(1.0, mean_of(wq, "SQ_WAVE_CYCLES")),
+            "vmem_rd_per_launch": mean_of(wq, "SQ_INSTS_VMEM_RD", n),
+            "vmem_wr_per_launch": mean_of(wq, "SQ_INSTS_VMEM_WR", n),
+            "lds_per_launch": mean_of(wq, "SQ_INSTS_LDS", n),
+            "waves_per_launch": mean_of(wq, "SQ_WAVES", n),
+            "wait_any_frac": mean_of(wq, "SQ_WAIT_ANY", n) / max(1.0, mean_of(wq, "SQ_WAVE_CYCLES", n)),
             "frac_valu": valu * 2.0 / (1024.0 * cyc),
             "frac_salu": salu / (256.0 * cyc),
             "note": "wave64 VALU = 2 SIMD cycles, 1024 SIMDs; SALU = 1 cycle on one scalar unit per CU, 256 CUs; "
                     "cycles = GRBM_GUI_ACTIVE / 8 XCDs",
         },
         "source": {"sq": a.sq, "fetch": a.fetch, "write": a.write},
-        "note": "mean over the bench's roofline pass (the last `steps` round-kernel dispatches: the same rounds "
-                "as the timed steps); FETCH_SIZE / WRITE_SIZE corrected by bin/pmc_calib's measured/true ratios",
+        "note": "per launch of the bench's roofline pass (its round-kernel dispatches, summed, / launches: the same "
+                "rounds as the timed steps); FETCH_SIZE / WRITE_SIZE corrected by bin/pmc_calib's measured/true ratios",
     }
     print(json.dumps(out, indent=1))
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
