@@ -131,6 +131,7 @@ for s in "$@"; do
     probe_c3opt) step probe_c3opt 600 bash -c 'for o in "virtual_votes=1" "virtual_votes=0" "count_lazy=0" "tiles_per_wave=2" "tiles_per_wave=8" "plane_nt=0" "store_policy=2"; do echo "== $o"; python tools/round_probe.py --workload c3 --option $o | tail -1; done' ;;
     refrows) step refrows 600 python -u -m pytest tests/test_gpu_ref_rows.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     probe_ref) step probe_ref 300 bash -c 'for o in "ref_rows=1" "ref_rows=0"; do echo "== $o"; python tools/round_probe.py --workload c4 --option $o; done' ;;
+    nstpw) step nstpw 600 bash -c 'for o in "tiles_per_wave=4" "tiles_per_wave=2" "tiles_per_wave=1"; do python tools/node_shard_probe.py --shards 1,2,4,8 --kinds nodes --option $o; done' ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=14)
     ap.add_argument("--workload", default="c4")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--kinds", default="nodes,targets")
+    ap.add_argument("--option", action="append", default=[], help="name=value, set on every engine")
     args = ap.parse_args()
     N, M, K, init_mode, init_param, byz, replay, _ = WORKLOADS[args.workload]
     out = {}
@@ -52,7 +54,7 @@ def main():
         return (time.perf_counter() - t0) / rounds * 1e3
 
     for g in [int(x) for x in args.shards.split(",")]:
-        for kind in ("nodes", "targets"):
+        for kind in args.kinds.split(","):
             if kind == "nodes":
                 e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz,
                                  node_range=sharding.node_shard(N, g, 0), log_capacity=1 << 26)
@@ -60,9 +62,12 @@ def main():
             else:
                 e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz,
                                  target_range=sharding.target_shard(M, g, 0), log_capacity=1 << 26)
+            for o in args.option:
+                name, v = o.split("=")
+                e.set_option(name, int(v))
             ms = [timed(e, args.rounds) for _ in range(3)]
             e.close()
-            key = f"{args.workload}_{kind}shard{g}"
+            key = f"{args.workload}_{kind}shard{g}" + "".join("_" + o for o in args.option)
             out[key] = {"ms_per_round": ms, "median_ms": statistics.median(ms)}
             print(key, out[key], flush=True)
     if args.json:
