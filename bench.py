@@ -474,6 +474,8 @@ def main():
                                  "ms_per_step": s["elapsed"] / args.steps * 1e3, "updates_emitted": int(s["emitted"]),
                                  "rounds": f"steps {args.warmup}..{args.warmup + args.steps - 1} of 16-round epochs",
                                  "roofline": roofline(s, f"{args.warmup}+{args.steps}", world)}
+                if world > 1:
+                    secondary[wl]["replicas_identical"] = s["replicas_identical"]
     except BenchFailure as ex:
         if rank == 0:
             print(str(ex), file=sys.stderr, flush=True)
