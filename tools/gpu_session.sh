@@ -132,6 +132,7 @@ for s in "$@"; do
     refrows) step refrows 600 python -u -m pytest tests/test_gpu_ref_rows.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     probe_ref) step probe_ref 300 bash -c 'for o in "ref_rows=1" "ref_rows=0"; do echo "== $o"; python tools/round_probe.py --workload c4 --option $o; done' ;;
     nstpw) step nstpw 600 bash -c 'for o in "tiles_per_wave=4" "tiles_per_wave=2" "tiles_per_wave=1"; do python tools/node_shard_probe.py --shards 1,2,4,8 --kinds nodes --option $o; done' ;;
+    probe_settled) step probe_settled 600 bash -c 'for o in "ablate_settled=0" "ablate_settled=1" "ablate_settled=2" "ablate_settled=4" "ablate_settled=8" "ablate_settled=15" "ablate_settled=7"; do echo "== $o"; python tools/round_probe.py --workload c4 --option $o | grep "\"round\": 1[0-2],"; done' ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
