@@ -161,7 +161,12 @@ int av_replay_round_errs(av_engine* e, const uint32_t* errs);
 /* Synthetic replayed stream (C2 workload): generate the vote classes of the
  * next `rounds` rounds on the device (avo_replay_err definition) ... */
 int av_replay_prepare(av_engine* e, int32_t rounds);
-/* ... and consume them (asynchronous). */
+/* ... and consume them (asynchronous). On engines where the 4096 poll cap
+ * binds (M > 4096) consecutive replay rounds run fused, up to option
+ * "replay_fuse" (16) per launch: every node's records depend only on its own
+ * stream, so a workgroup carries them through the rounds in registers; nodes
+ * that reach count 120 continue in the per-round exact pass. Results are
+ * identical to one launch per round (tests/test_gpu_replay_fused.py). */
 int av_replay_rounds(av_engine* e, int32_t rounds);
 int av_synchronize(av_engine* e);
 /* Batched rounds run so far (the engine's round counter: the RNG counter of
