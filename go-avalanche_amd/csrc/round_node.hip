@@ -306,6 +306,19 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
   uint32_t maxc = 0u;  // largest polled count of the node
   for (uint32_t q = 0; q < (blockDim.x >> 6); ++q) maxc = max(maxc, wsum[1][q]);
   const uint32_t J = maxc >= 120u ? 0u : (120u - maxc + (uint32_t)K - 1u) / (uint32_t)K;
+  if (!heavy) {
+    // no polled record in this wave: its records and published words stay
+    // as they are through the launch (a record leaves or joins the poll set
+    // only in the exact pass, which rewrites the node's rows of its rounds
+    // afterwards). Publish the last three rounds now and end the wave: its
+    // registers go to other workgroups, and the barriers below count only the
+    // waves still running.
+    const uint32_t r0 = R > 3u ? R - 3u : 0u;
+    for (uint32_t r = r0; r < R; ++r)
+      if (active) p.pref_ring[(p.ring_next + r) % 3u][prow] = byz ? byz_pattern(p.round + r + 1u) : A;
+    count_stats(p, wave_id, lane, 0u, active, 20u + 4u + 4u * (R - r0), 0u, 0u, 0u);
+    return;
+  }
   uint32_t done = R, applied = 0u, upd = 0u, emitted = 0u, pubs = 0u;
   for (uint32_t r = 0; r < R; ++r) {
     // a polled record with count >= 120 may finalize (and leave the poll set) this round
