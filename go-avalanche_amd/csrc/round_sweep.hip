@@ -659,11 +659,13 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   const uint32_t gc = active ? g : p.L - 1u;
   const uint32_t nl = div_bl(p, gc);
   const uint32_t b = gc - nl * p.BL;
-  // A plane: SGPR tile base + the lane's constant byte offset
-  const char* const ta = reinterpret_cast<const char*>(p.planes + (size_t)tile * (kPlanes * 64u));
-  const uint32_t ao = (1536u + lane) * 4u;
-  const uint32_t A = POL > 0 ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(ta + ao))
-                             : *reinterpret_cast<const uint32_t*>(ta + ao);
+  // A plane: a buffer resource on the tile (SGPRs) + the lane's constant byte
+  // offset, so no 64-bit per-lane address is kept live across the tile loop
+  // (the flat form was hoisted into a VGPR pair that spilled and was reloaded
+  // from scratch, with a full vmcnt wait, at every settled tile)
+  const __amdgpu_buffer_rsrc_t ta =
+      __builtin_amdgcn_make_buffer_rsrc(p.planes + (size_t)tile * (kPlanes * 64u), 0, kPlanes * 64 * 4, kRsrcWord3);
+  const uint32_t A = __builtin_amdgcn_raw_buffer_load_b32(ta, (1536u + lane) * 4u, 0, POL > 0 ? 2 : 0);
   const uint32_t P0 = active ? at_byte(p.valid, b * 4u) : 0u;  // polled = live (kPendAllLive) and valid
   uint32_t rows[8];
   pick_parked(p, wd.sd, wd.bad, (nl - wd.nlA) * 2u + (wd.pair ? 32u : 0u), p.n0 + nl, p.round, p.PS * 4u, rows);
