@@ -247,7 +247,8 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  *                    engines, M <= 4096). 1 and 2 run the first-generation
  *                    kernel.
  * Sweep-kernel tuning and A/B switches (defaults are the measured best;
- * DESIGN.md §3-4): "tiles_per_wave" (4), "wave_runs" (1: a wave takes a run
+ * DESIGN.md §3-4): "tiles_per_wave" (0 = by size: 8
+ * from 256k tiles at BL >= 16, else 4), "wave_runs" (1: a wave takes a run
  * of consecutive tiles and draws their peers once), "settled_fast" (1),
  * "sweep_nopipe" (1), "virtual_votes" (1), "vv_min_bl" (16), "count_lazy"
  * (1), "fresh" (1), "dense_min" (6 at k = 8: updates per lane that make a

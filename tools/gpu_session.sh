@@ -134,6 +134,7 @@ for s in "$@"; do
     nstpw) step nstpw 600 bash -c 'for o in "tiles_per_wave=4" "tiles_per_wave=2" "tiles_per_wave=1"; do python tools/node_shard_probe.py --shards 1,2,4,8 --kinds nodes --option $o; done' ;;
     probe_settled) step probe_settled 600 bash -c 'for o in "ablate_settled=0" "ablate_settled=1" "ablate_settled=2" "ablate_settled=4" "ablate_settled=8" "ablate_settled=15" "ablate_settled=7"; do echo "== $o"; python tools/round_probe.py --workload c4 --option $o | grep "\"round\": 1[0-2],"; done' ;;
     benchwin) step benchwin 900 bash -c 'python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-secondary && python bench.py --steps 5 --warmup 0 --no-cpu-baseline --no-secondary && python bench.py --steps 100 --warmup 3 --no-cpu-baseline --no-secondary' ;;
+    probe_tpw) step probe_tpw 600 bash -c 'for w in c4 c3; do for o in "tiles_per_wave=4" "tiles_per_wave=6" "tiles_per_wave=8" "tiles_per_wave=3"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o | tail -1 | grep -o "kernel_ms_total.*"; done; done' ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
