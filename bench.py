@@ -74,6 +74,12 @@ WORKLOADS = {
            "C3: 100k nodes x 1000 double-spend pairs, k=8, 20% Byzantine flip-flop voters"),
     "c5": (10_000_000, 256, 8, avhip.INIT_BERNOULLI, P80, 0, False,
            "C5: 10M nodes x 256 targets, k=8, Bernoulli(0.8), honest"),
+    # the north star's "1M nodes x 1k conflicting targets": 500 double-spend pairs per node with
+    # complementary initial IsAccepted, honest / 20 % Byzantine flip-flop voters
+    "c4p": (1_000_000, 1000, 8, avhip.INIT_PAIRS, 0, 0, False,
+            "C4p: 1M nodes x 1000 targets as 500 conflicting double-spend pairs, k=8, honest"),
+    "c4pb": (1_000_000, 1000, 8, avhip.INIT_PAIRS, 0, BYZ20, False,
+             "C4pb: 1M nodes x 500 double-spend pairs, k=8, 20% Byzantine flip-flop voters"),
 }
 
 PARALLELISM = {
@@ -134,6 +140,27 @@ def cpu_model():
     return "unknown"
 
 
+def host_cpus():
+    """The host cores this process may use: the affinity mask, capped by the
+    cgroup CPU quota (cpu.max) when one is set — a 1-GPU box exposes every
+    CPU of the machine in its affinity mask but grants a share of them."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    threads = affinity if quota is None else max(1, min(affinity, int(round(quota))))
+    return {"threads": threads, "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(wl, seed, budget_s):
     """Oracle ("port": the C restatement of the reference semantics,
     oracle/avalanche_oracle.c) on host cores, on a bounded sample of the same
@@ -141,13 +168,9 @@ def cpu_baseline(wl, seed, budget_s):
     from oracle import cabi
 
     n, m, k, init_mode, init_param, byz, replay, _ = WORKLOADS[wl]
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
-    threads = max(1, min(threads, 16, avail))
-    # ~10-20 s of CPU work on a 16-core host (the branch-free oracle runs ~6e9 updates/s there)
+    hc = host_cpus()
+    threads = hc["threads"]
+    # ~10-20 s of CPU work (the branch-free oracle runs ~6e9 updates/s on 16 cores)
     ns = min(n, 500_000 if wl != "c2" else 1000)
     sim = cabi.Sim(ns, m, k, seed=seed, byz_threshold=byz, init_mode=init_mode, init_param=init_param,
                    threads=threads)
@@ -163,7 +186,7 @@ def cpu_baseline(wl, seed, budget_s):
         rounds += 1
     sim.close()
     return {"value": applied / dt, "unit": "vote-record updates/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+            "cpu_model": cpu_model(), "host_cpus": hc,
             "sample": f"oracle/avalanche_oracle.c (C restatement of vote.go/processor.go, the parity oracle), "
                       f"{ns} nodes x {m} targets, k={k}, rounds 0..{rounds - 1} ({applied} regsiterVote "
                       f"applications, {dt:.1f}s, OpenMP over nodes, {threads} threads on {cpu_model()})"}
@@ -236,13 +259,17 @@ class Runner:
     def steps(self, count, timed):
         """Run `count` steps from the current position. timed: every segment
         inside one epoch is bracketed by barrier + synchronize and its wall
-        time summed. Returns (seconds, applied, emitted, segments)."""
+        time summed. Untimed steps run one round at a time with the log
+        emptied after each (a conflicting workload emits ~1e8 StatusUpdates
+        per round). Returns (seconds, applied, emitted, segments)."""
         eng = self.eng
         elapsed, applied, emitted, segs = 0.0, 0, 0, 0
         while count > 0:
             if self.pos % EPOCH == 0 and self.pos > 0:
                 self.reset()
             seg = min(EPOCH - self.pos % EPOCH, count)
+            if not timed and not self.replay:
+                seg = 1
             eng.synchronize()
             eng.discard_updates()
             a0 = eng.applied_votes()
@@ -286,10 +313,10 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     `warmup` untimed steps, `steps` timed steps; then a second pass over the
     same steps with HIP events around every round kernel (roofline)."""
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
-    # the log holds every StatusUpdate of one epoch segment (~0.2 N*M at most in
-    # the all-live rounds of these workloads: C4 rounds 0-1 ~1e8 each, C3 ~3e7 per
-    # round); 16 B of device memory per entry (singles + dense records)
-    log_cap = min(int(0.5 * n * m) + (1 << 20), 1 << 31)
+    # the log holds every StatusUpdate of one timed segment (up to 16 rounds:
+    # C4 ~2e8 in rounds 0-2, the conflicting C4p/C4pb ~1e9 over rounds 0-8);
+    # 16 B of device memory per entry (singles + dense records): 20 GB at 1M x 1000
+    log_cap = min(int(1.25 * n * m) + (1 << 20), (1 << 31) - 1)
     run = Runner(wl, args, world, rank, local_rank, log_cap)
     if run.fallback is not None:
         args.shard = "targets"
@@ -304,22 +331,37 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     run.goto(warmup)
     elapsed, applied, emitted, segs = run.steps(steps, timed=True)
 
-    # ---- roofline pass: the same steps again, every round kernel bracketed by
-    # HIP events on the engine's stream
+    # ---- roofline pass: the same steps again, every round's kernels bracketed
+    # by HIP events on the engine's stream; sim rounds one step at a time so
+    # that every round's kernel time, model bytes and re-read bytes are known
     kern_ms = launches = 0
-    moved = 0
+    moved = reread = 0
     applied2 = emitted2 = 0
+    per_round = []
     if not args.no_roofline_pass:
         # the same steps of fresh epochs; the peer draws follow the engine's
         # absolute round counter, so the StatusUpdate count differs slightly
         # from the timed pass (the applied votes do not: every record is live)
         run.goto(warmup)
-        b0 = eng.alg_bytes()
         eng.set_timing(True)
-        _, applied2, emitted2, _ = run.steps(steps, timed=False)
+        left = steps
+        while left > 0:
+            rnd = run.pos % EPOCH
+            seg = min(EPOCH - rnd, left) if replay else 1
+            b0, r0 = eng.alg_bytes(), eng.alg_bytes_reread()
+            _, a, em, _ = run.steps(seg, timed=False)
+            ms, nl = eng.kernel_stats()
+            db, dr = eng.alg_bytes() - b0, eng.alg_bytes_reread() - r0
+            per_round.append({"round": rnd, "rounds": seg, "kernel_ms": ms, "launches": nl, "model_bytes": db,
+                              "reread_bytes": dr, "applied": a, "emitted": em})
+            kern_ms += ms
+            launches += nl
+            moved += db
+            reread += dr
+            applied2 += a
+            emitted2 += em
+            left -= seg
         eng.set_timing(False)
-        kern_ms, launches = eng.kernel_stats()
-        moved = eng.alg_bytes() - b0
         if applied2 != applied:
             raise BenchFailure(f"bench: roofline pass applied {applied2} votes, the timed pass {applied}")
     replicas = None
@@ -359,11 +401,16 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     # applied vote is one live (node, target, round) triple / k; + 20 B per
     # emitted StatusUpdate
     s8d = (applied2 / k * S8D_TRIPLE_BYTES[replay] + emitted2 * S8D_UPDATE_BYTES) / launches if launches else None
+    for pr in per_round:
+        pr["s8d_bytes"] = pr["applied"] / k * S8D_TRIPLE_BYTES[replay] + pr["emitted"] * S8D_UPDATE_BYTES
     return {
         "wl": wl, "desc": desc, "n": n, "m": m, "k": k, "elapsed": elapsed, "applied": applied_all,
         "emitted": emitted_all, "value": applied_all / elapsed, "segments": segs, "info": info,
         "kavg_ms": kavg_ms, "launches": launches, "s8d_bytes": s8d,
         "moved_bytes": moved / launches if launches else None, "kernel": kname, "replicas_identical": replicas,
+        "reread_bytes": reread / launches if launches else None, "per_round": per_round, "replay": replay,
+        "kernel_ms_total": kern_ms, "steps": steps,
+        "lanes": info["lanes"] if info else None,
         "rounds_per_launch": steps / launches if launches else None,
         "first_round": warmup % EPOCH,
     }
@@ -389,10 +436,13 @@ def allgather_probe(world, local_rank, total_bytes=1_000_000 * 128, reps=5):
             "note": "C4 node-sharded round exchange (1M x 1000 bits), torch.distributed all_gather_into_tensor"}
 
 
+PMC_DIR = os.path.join(ROOT, "profiles", "r03")
+
+
 def load_pmc(wl, window, world):
     """The committed rocprofv3 PMC summary of this bench window (tools/
-    pmc_summary.py), used only if it was measured on these kernel sources."""
-    path = os.path.join(ROOT, "profiles", "r02", f"pmc_{wl}.json")
+    pmc_bench.py), used only if it was measured on these kernel sources."""
+    path = os.path.join(PMC_DIR, f"pmc_{wl}.json")
     if world != 1 or not os.path.exists(path):
         return None
     with open(path) as f:
@@ -402,37 +452,111 @@ def load_pmc(wl, window, world):
     return d
 
 
+# round kinds of a fresh sim network at k = 8 (engine: launch_one_round): round 0 reads only A
+# (fresh), rounds 1-3 carry the convergence storm, 4-14 may defer count planes (klazy; a tile that
+# stays unanimous takes the settled path), 15 applies the deferred steps (kconsume)
+def round_kind(r, replay):
+    if replay:
+        return "replay (fused rounds per launch)"
+    return "fresh" if r == 0 else "storm" if r <= 3 else "klazy" if r <= 14 else "kconsume"
+
+
+def binding(fr):
+    """The resource closest to its peak; 'latency' when none is above half of
+    its peak while waves wait on memory most of their cycles (SQ_WAIT_ANY)."""
+    c = {k: v for k, v in fr.items() if k in ("fabric", "hbm_compulsory", "valu_issue", "salu_issue") and v is not None}
+    top = max(c, key=c.get)
+    if c[top] < 0.5 and (fr.get("wait_any") or 0.0) >= 0.5:
+        return "latency"
+    return top
+
+
 def roofline(r, window=None, world=1):
-    """Roofline of the round kernel. achieved/frac: SURVEY.md
-    §8(d)'s algorithmic bytes per launch / the HIP-event launch time. The
-    bit-sliced kernel moves fewer bytes than that 4-B-per-record model, so frac
-    can exceed 1; bytes_moved is what the kernel actually streams and gathers.
-    pmc (when the committed profile matches the sources and window): the HBM
-    traffic from FETCH_SIZE/WRITE_SIZE and the instruction-issue fractions."""
+    """Roofline of the round kernel.
+
+    achieved/frac: the bit-sliced kernel's byte model (state
+    planes read/written per round type, every gathered preference word, the
+    published word, the StatusUpdate log; counted by the kernel itself per
+    tile, av_alg_bytes) per launch / the HIP-event launch time, against the
+    8 TB/s HBM peak. alg_bytes_s8d/frac_s8d: SURVEY.md §8(d)'s 4-B-per-record
+    model, which this layout beats (3.1 B per record), hence > 1.
+    hbm_bytes_compulsory: the model minus the preference words re-read by
+    other lanes of the same round = a lower bound on the HBM bytes.
+    traffic (PMC, when the committed profile matches sources and window):
+    FETCH_SIZE + WRITE_SIZE, calibrated = bytes crossing the L2 <-> fabric
+    boundary, Infinity-Cache hits included (MI355X_MICROARCH.md §HBM), i.e. an
+    upper bound on the HBM bytes. Per round kind: the same fractions, issue
+    rates and the binding resource."""
     if r["kavg_ms"] is None:
         return None
     t = r["kavg_ms"] * 1e-3
-    ach = r["s8d_bytes"] / t / 1e9
+    ach = r["moved_bytes"] / t / 1e9
+    comp = r["moved_bytes"] - r["reread_bytes"]
     out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-           "traffic": None, "kernel": r["kernel"], "kernel_ms_avg": r["kavg_ms"], "launches": r["launches"],
-           "alg_bytes_s8d": r["s8d_bytes"], "rounds_per_launch": r["rounds_per_launch"],
-           "bytes_moved": r["moved_bytes"], "frac_moved": r["moved_bytes"] / t / 1e9 / HBM_PEAK_GBS,
-           "note": "achieved = SURVEY.md §8(d) bytes (9.125 B per live node-target-round + 20 B per "
-                   "StatusUpdate) / kernel time; the bit-sliced kernel moves bytes_moved instead (DESIGN.md §3)"}
+           "traffic": None, "traffic_kind": "fabric (L2<->EA requests incl. Infinity-Cache hits: upper bound on HBM)",
+           "kernel": r["kernel"], "kernel_ms_avg": r["kavg_ms"], "launches": r["launches"],
+           # the timed pass (wall clock, barrier + synchronize) and the HIP-event pass run the same
+           # rounds separately: the difference per step is launch gaps and host work (+- noise)
+           "kernel_ms_per_step": r["kernel_ms_total"] / r["steps"],
+           "host_gap_ms_per_step": r["elapsed"] / r["steps"] * 1e3 - r["kernel_ms_total"] / r["steps"],
+           "rounds_per_launch": r["rounds_per_launch"],
+           "model": "bit-sliced byte model per round type (DESIGN.md §3), counted by the kernel (av_alg_bytes)",
+           "model_bytes": r["moved_bytes"],
+           "hbm_bytes_compulsory": comp, "frac_hbm_compulsory": comp / t / 1e9 / HBM_PEAK_GBS,
+           "alg_bytes_s8d": r["s8d_bytes"], "frac_s8d": r["s8d_bytes"] / t / 1e9 / HBM_PEAK_GBS,
+           "note": "frac = model bytes / kernel time / 8 TB/s; frac_s8d = SURVEY.md §8(d) bytes (9.125 B per live "
+                   "node-target-round + 20 B per StatusUpdate), a model this layout beats"}
     pmc = load_pmc(r["wl"], window, world) if window else None
+    pr_pmc = {}
     if pmc:
-        out["traffic"] = pmc.get("hbm_bytes_per_launch")
-        if pmc.get("issue"):
-            iss = pmc["issue"]
-            out["issue"] = iss
-            # the binding resource: whichever of HBM traffic / VALU issue / SALU issue is closest to its peak
-            cands = {"hbm": (out["traffic"] or 0) / t / 1e9 / HBM_PEAK_GBS,
-                     "valu_issue": iss.get("frac_valu", 0.0), "salu_issue": iss.get("frac_salu", 0.0)}
-            out["binding"] = max(cands, key=cands.get)
-            out["binding_fracs"] = cands
-            # the resource closest to its peak in this window (PMC): HBM traffic or instruction issue
-            out["bound"] = "hbm" if out["binding"] == "hbm" else "issue"
+        out["traffic"] = pmc.get("fabric_bytes_per_launch")
         out["pmc_source"] = pmc.get("source")
+        for row in pmc.get("per_round", []):
+            pr_pmc.setdefault(row["round"], []).append(row)
+    # per round kind (sim: one round per launch; replay: one fused launch per row)
+    kinds = {}
+    for pr in r["per_round"]:
+        kd = kinds.setdefault(round_kind(pr["round"], r["replay"]),
+                              {"rounds": [], "ms": 0.0, "launches": 0, "model": 0, "reread": 0, "pmc": []})
+        kd["rounds"].append(pr["round"])
+        kd["ms"] += pr["kernel_ms"]
+        kd["launches"] += pr["launches"]
+        kd["model"] += pr["model_bytes"]
+        kd["reread"] += pr["reread_bytes"]
+    if pmc and len(pmc.get("per_round", [])) == len(r["per_round"]):
+        for pr, row in zip(r["per_round"], pmc["per_round"]):
+            kinds[round_kind(pr["round"], r["replay"])]["pmc"].append((pr, row))
+    rt = {}
+    for name, kd in kinds.items():
+        ts = kd["ms"] * 1e-3
+        fr = {"model": kd["model"] / ts / 1e9 / HBM_PEAK_GBS,
+              "hbm_compulsory": (kd["model"] - kd["reread"]) / ts / 1e9 / HBM_PEAK_GBS,
+              "fabric": None, "valu_issue": None, "salu_issue": None, "wait_any": None}
+        if kd["pmc"]:
+            cyc = sum(row["cycles"] for _, row in kd["pmc"])
+            fab = sum(row["fabric_bytes"] for _, row in kd["pmc"])
+            fr["fabric"] = fab / ts / 1e9 / HBM_PEAK_GBS
+            fr["valu_issue"] = sum(row["valu"] for _, row in kd["pmc"]) * 2.0 / (1024.0 * cyc)
+            fr["salu_issue"] = sum(row["salu"] for _, row in kd["pmc"]) / (256.0 * cyc)
+            fr["wait_any"] = (sum(row["wait_any"] for _, row in kd["pmc"]) /
+                              max(1.0, sum(row["wave_cycles"] for _, row in kd["pmc"])))
+        ent = {"rounds": sorted(set(kd["rounds"])), "launches": kd["launches"],
+               "kernel_ms_avg": kd["ms"] / max(1, kd["launches"]),
+               "model_bytes_per_launch": kd["model"] / max(1, kd["launches"]),
+               "model_bytes_per_lane": kd["model"] / max(1, kd["launches"]) / r["lanes"] if r["lanes"] else None,
+               "fracs": fr}
+        ent["binding"] = binding(fr) if kd["pmc"] else None
+        rt[name] = ent
+    out["round_kinds"] = rt
+    # the whole window's binding resource (PMC window sums)
+    if pmc:
+        iss = pmc["issue"]
+        fr = {"fabric": (out["traffic"] or 0.0) / t / 1e9 / HBM_PEAK_GBS,
+              "hbm_compulsory": out["frac_hbm_compulsory"], "valu_issue": iss["frac_valu"],
+              "salu_issue": iss["frac_salu"], "wait_any": iss["wait_any_frac"]}
+        out["binding_fracs"] = fr
+        out["binding"] = binding(fr)
+        out["issue"] = iss
     return out
 
 
@@ -465,7 +589,7 @@ def main():
                     secondary["xgmi_allgather"] = allgather_probe(world, local_rank)
                 except Exception as exc:
                     secondary["xgmi_allgather"] = {"error": repr(exc)[:200]}
-            others = ["c3"] + (["c2"] if world == 1 else [])
+            others = ["c4p", "c4pb", "c3"] + (["c2"] if world == 1 else [])
             for wl in others:
                 if wl == args.workload:
                     continue

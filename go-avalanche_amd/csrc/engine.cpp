@@ -124,6 +124,7 @@ struct av_engine {
   // 1 = k_round_fast / k_round_capped (the first versions; any k, A/B baseline)
   int kernel = 2;
   uint32_t sweep_blocks = 0;  // resident workgroups of the sweep grid (option "sweep_blocks"; 0 = one wave per tile)
+  bool sweep_blocks_explicit = false;  // "sweep_blocks" set to a value >= 0: "tiles_per_wave" leaves it alone
   // option "sweep_nopipe": a walking grid runs without next-tile prefetch
   // (kModeWarm; default); 0 = the prefetching kModeWarmPipe (A/B)
   bool sweep_nopipe = true;
@@ -132,6 +133,9 @@ struct av_engine {
   bool wave_runs = true;
   // option "settled_fast": settled warm tiles skip the round step's bookkeeping
   bool settled_fast = true;
+  // option "settled_lean": with BL dividing 64, a wave tests its run's settled candidates in one
+  // lean loop first (round_sweep.hip settled_run)
+  bool settled_lean = true;
   // option "tiles_per_wave" (default grid, default_sweep_blocks); 0 = by size: 8 from 256k tiles on
   // at BL >= 16 (C4: 500k tiles, 6.13 -> 5.99 ms per epoch), else 4 (C3's 98k tiles: 8 per wave leaves two
   // generations of waves and was 6 % slower)
@@ -295,6 +299,8 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.nopipe = e->sweep_nopipe ? 1u : 0u;
   p.tpw = e->wave_runs && e->sweep_blocks ? 1u : 0u;
   p.settled_fast = e->settled_fast ? 1u : 0u;
+  p.lean = e->settled_lean && 64 % e->BL == 0 ? 1u : 0u;
+  p.bl_log2 = (uint32_t)__builtin_ctz(e->BL);
   p.pub_mode = (uint32_t)e->pub_mode;
   p.readd = e->pub_mode == 2 ? e->readd : nullptr;
   p.died_out = e->pub_mode == 2 ? e->died_out : nullptr;
@@ -434,12 +440,15 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   // the sweep's warm sim modes (launch_sweep_k): every consider plane all-ones
   const bool warm = sweep && !replay && e->c_monotone && e->warm_all && !e->ablate_gather && !fresh;
   // vote planes may be left unstored: warm (or fresh) k = 8 sim rounds
-  const bool vv = e->virtual_votes && e->k == 8 && e->BL >= e->vv_min_bl && (warm || fresh);
+  // below vv_min_bl only the uniform form (a settled tile's V = A: nothing to regather)
+  const bool vv = e->virtual_votes && e->k == 8 && (warm || fresh);
+  const bool vv_uniform = vv && e->BL < e->vv_min_bl;
   if (!vv) {
     int rc = materialize_votes_only(e);
     if (rc != AV_OK) return rc;
   }
   p.vv = vv ? 1u : 0u;
+  p.vv_uniform = vv_uniform ? 1u : 0u;
   if (vv) e->v_stale = true;
   p.fresh = fresh ? 1u : 0u;
   // count planes may be deferred: warm k = 8 sim rounds while no record can
@@ -763,8 +772,10 @@ int av_create(const av_config* cfg, av_engine** out) {
     (void)hipMemsetAsync(e->node_flags, 0, (size_t)e->NL * 4, e->stream);
   }
   if ((he = dev_alloc(&e->applied, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
-  if ((he = dev_alloc(&e->bytes, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
-  (void)hipMemsetAsync(e->bytes, 0, avk::kLogShards * 8, e->stream);
+  // [0, kLogShards): model bytes moved; [kLogShards, 2 kLogShards): the part of them that re-reads a
+  // preference word another lane of the same round already gathered (av_alg_bytes_reread)
+  if ((he = dev_alloc(&e->bytes, 2 * avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
+  (void)hipMemsetAsync(e->bytes, 0, 2 * avk::kLogShards * 8, e->stream);
   if ((he = dev_alloc(&e->finalized, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
   (void)hipMemsetAsync(e->finalized, 0, avk::kLogShards * 8, e->stream);
   if ((he = dev_alloc(&e->scratch_count, 1)) != hipSuccess) return hip_fail(he, "alloc counters");
@@ -1568,18 +1579,24 @@ int av_discard_updates(av_engine* e) {
   return clear_log(e);
 }
 
-int av_alg_bytes(av_engine* e, int64_t* out) {
+namespace {
+int sum_byte_counters(av_engine* e, size_t first, int64_t* out) {
   AV_ENTER(e);
   AV_PEER_SYNC_CHECK(e);
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
   std::vector<unsigned long long> c(avk::kLogShards);
-  AV_HIP(hipMemcpyAsync(c.data(), e->bytes, avk::kLogShards * 8, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpyAsync(c.data(), e->bytes + first, avk::kLogShards * 8, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
   unsigned long long t = 0;
   for (auto v : c) t += v;
   *out = (int64_t)t;
   return AV_OK;
 }
+}  // namespace
+
+int av_alg_bytes(av_engine* e, int64_t* out) { return sum_byte_counters(e, 0, out); }
+
+int av_alg_bytes_reread(av_engine* e, int64_t* out) { return sum_byte_counters(e, avk::kLogShards, out); }
 
 int av_read_pref(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint8_t* out) {
   AV_ENTER(e);
@@ -1656,11 +1673,15 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     if (value < 0) {
       AV_ENTER(e);
       e->sweep_blocks = default_sweep_blocks(e, value == -2);
+      e->sweep_blocks_explicit = false;
     } else {
       e->sweep_blocks = (uint32_t)value;
+      e->sweep_blocks_explicit = true;
     }
   } else if (n == "settled_fast") {
     e->settled_fast = value != 0;
+  } else if (n == "settled_lean") {
+    e->settled_lean = value != 0;
   } else if (n == "wave_runs") {
     e->wave_runs = value != 0;
   } else if (n == "sweep_nopipe") {
@@ -1668,7 +1689,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   } else if (n == "tiles_per_wave") {
     AV_CHECK(value >= 0 && value <= 4096, AV_ERR_INVALID_ARG, "bad tiles_per_wave");
     e->tiles_per_wave = (uint32_t)value;
-    e->sweep_blocks = default_sweep_blocks(e);
+    // the default grid depends on the run length; an explicit sweep_blocks stays as set
+    if (!e->sweep_blocks_explicit) e->sweep_blocks = default_sweep_blocks(e);
   } else if (n == "unsynced_shard") {
     e->unsynced_shard = value != 0;
   } else if (n == "round_marker") {

@@ -79,7 +79,8 @@ struct RoundParams {
   uint64_t replay_stride;
   uint32_t* pref_ring[3];
   unsigned long long* applied;  // [kLogShards] regsiterVote applications
-  unsigned long long* bytes;    // [kLogShards] algorithmic bytes moved by the round kernel
+  unsigned long long* bytes;    // [2 kLogShards] model bytes moved by the round kernel; [kLogShards + i]: the part
+                                // that re-reads preference words already gathered this round (not compulsory)
   unsigned long long* finalized;  // [kLogShards] records finalized (deleted, processor.go:114-116)
   uint64_t seed;
   uint32_t log_cap;          // entries per shard
@@ -111,6 +112,7 @@ struct RoundParams {
   // gathered words, so a tile may skip storing its V planes and the next
   // round regathers them from the previous snapshot instead of reading them.
   uint32_t vv;               // this round may leave V planes unstored (vstale)
+  uint32_t vv_uniform;       // ... only in the uniform form (kVUniform: settled tiles; never kVStale)
   // [tiles] kVStale: the tile's V planes are stale, V = votes of round - 1
   // (regathered with round - 1's peers); kVUniform: the tile was settled (all
   // 8 votes of round - 1 equal the accepted bit of every polled record), so V
@@ -162,6 +164,10 @@ struct RoundParams {
   uint32_t tn;
   uint32_t tpw;     // kModeWarm, k = 8: run length of consecutive tiles per wave with one shared peer draw (0 = grid stride)
   uint32_t settled_fast;  // kModeWarm, k = 8: settled tiles skip process_tile (round_sweep.hip settled_fast)
+  // kModeWarm, k = 8, BL dividing 64 (a lane's block is lane % BL): the settled candidates of a wave's
+  // run are tested first in one lean loop (round_sweep.hip settled_run); bl_log2 = log2(BL)
+  uint32_t lean;
+  uint32_t bl_log2;
   uint32_t nopipe;  // tuning: a grid smaller than the tile count runs kModeWarm (no next-tile prefetch)
   // Responder variants (engine option "responder", first-generation kernel
   // only; see publish_word): pub_mode 0 = R2 decision, 1 = IsAccepted

@@ -41,6 +41,7 @@ namespace {
 
 struct SweepAcc {
   uint32_t applied = 0, died = 0, lane_bytes = 0;
+  uint32_t reread = 0;  // per lane: gathered preference bytes beyond the one compulsory read of each word
   uint32_t emitted_bytes = 0, updates = 0;  // wave-uniform: StatusUpdate log bytes written, updates emitted
 };
 
@@ -70,7 +71,7 @@ struct TileIn {
 struct WaveDraw {
   const uint32_t* sd;  // the draw, parked in LDS (round_slots.h park_draw)
   unsigned long long bad;
-  uint32_t nlA, t0;
+  uint32_t nlA, t0, nn;
   uint32_t meta;  // lane i: tile t0 + i's vstale << 8 | kpend & (kPendAllLive | 0xFF)
   bool pair, ok;
 };
@@ -370,8 +371,7 @@ __device__ __forceinline__ uint32_t emit_updates_lds(const RoundParams& p, uint3
 // the lane; the node's block-0 lane stores the byte (and pushes it to the
 // peers' replicas when it changed, as the published words).
 __device__ __forceinline__ void ref_flag_store(const RoundParams& p, uint32_t lane, bool active, uint32_t b,
-                                               uint32_t node, uint32_t pub) {
-  const uint32_t ref = p.pref_in[p.ref_node * p.PS + (active ? b : 0u)];
+                                               uint32_t node, uint32_t pub, uint32_t ref) {
   const uint64_t eq = __ballot(!active || pub == ref);
   const uint32_t s0 = lane - b;  // the node's first lane (active lanes only)
   const uint64_t seg = (p.BL >= 64u ? ~0ull : ((1ull << p.BL) - 1ull)) << (s0 & 63u);
@@ -436,7 +436,24 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   // a warm sim wave with no live-but-invalid record leaves its V planes
   // unstored: next round (or av materialize) regathers them (kernels.h vv)
   bool virt = false;
-  if constexpr (VVM && !REPLAY && K == 8) virt = p.vv && __ballot(keep != 0u) == 0ull;
+  if constexpr (VVM && !REPLAY && K == 8) {
+    virt = p.vv && __ballot(keep != 0u) == 0ull;
+    if (virt && p.vv_uniform) {
+      // uniform form only (narrow rows, BL < vv_min_bl): a tile leaves V unstored only if it is
+      // settled this round (V = A next round, nothing to regather); the test is the settled test
+      // below, made early (klazy rounds: no record is near 128)
+      bool st = false;
+      if constexpr (SYM) {
+        if (klazy) {
+          uint32_t agree = P0;
+#pragma unroll
+          for (int i = 0; i < 7 + K; ++i) agree &= ~(ys[i] ^ in.A);
+          st = __ballot(agree != P0) == 0ull;
+        }
+      }
+      virt = st;
+    }
+  }
   if (active && !virt) {
     u32x4 o0, o1;
 #pragma unroll
@@ -586,14 +603,15 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
           __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, 0x7FFFFFFF, kRsrcWord3);
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
     st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
     // a record deleted this round keeps the vote/consider planes stored
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
   }
   if (REF && p.rflag_out) {  // reference-row flag of the row just published (kernels.h)
-    ref_flag_store(p, lane, active, b, node, is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A);
+    ref_flag_store(p, lane, active, b, node, is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A,
+                   p.pref_in[p.ref_node * p.PS + (active ? b : 0u)]);
     if (active) acc.lane_bytes += 4u + (b == 0u ? 1u : 0u);
   }
   if constexpr (VVM && !REPLAY && K == 8) {
@@ -640,6 +658,9 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
                                  kbytes - (astore ? 0u : 4u)
                            : 0u;
   acc.emitted_bytes += emitted;
+  // sim rounds gather 8 peer words per lane (each word of the round-start snapshot is gathered by
+  // ~k lanes: 28 of the 32 B re-read), stale tiles 7 more from the previous snapshot (24 B re-read)
+  if constexpr (!REPLAY) acc.reread += active ? 4u * K - 4u + (in.stale == kVStale ? 24u : 0u) : 0u;
 }
 
 // Settled-tile fast path (kModeWarm, k = 8, klazy round, the wave's parked
@@ -706,10 +727,10 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
           __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, 0x7FFFFFFF, kRsrcWord3);
+    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
     st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
   }
-  if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub);
+  if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, p.pref_in[p.ref_node * p.PS + (active ? b : 0u)]);
   if (lane == 0) p.kpend[tile] = ((kw & 0xFFu) + 1u) | kPendAllLive;
   acc.applied += 8u * (uint32_t)__popc(P0);
   // process_tile's accounting for this case: 17 plane words + 8 vote words +
@@ -717,11 +738,125 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   // A store (unchanged) = 40 B per lane (+ 4 B push read); kpend read + write
   // reference rows: 8 flag bytes per node read, the reference word instead of
   // the 32 B of gathered votes, the next reference word + the flag written
+  acc.reread += active && gather ? 28u : 0u;
   acc.lane_bytes += (active ? 40u + (p.push_n ? 4u : 0u) + rbytes - (gather ? 0u : 32u) +
                                   (REF && p.rflag_out ? 4u + (b == 0u ? 1u : 0u) : 0u)
                             : 0u) +
                     (lane == 0 ? 8u : 0u);
   return true;
+}
+
+// The settled candidates of a wave's run in one lean loop (p.lean: kModeWarm,
+// k = 8, klazy round, BL dividing 64, the run's draw parked with no repeated
+// candidate). Same test and outputs as settled_tile, with everything that does
+// not depend on the tile hoisted out of the loop: a lane's block b = lane % BL
+// and its validity word, the run's Byzantine bits (one ballot), the A-plane
+// buffer resource (the tile moves the scalar offset only), the node index
+// (shift, no division); the kpend words of the settled tiles are written by one
+// store per run (lane i: tile t0 + i) and the counters accumulated per tile
+// without a branch. Per settled tile: the A load, 8 gathers, 2 LDS reads, one
+// ballot, the published-word store. Returns the run's settled tiles (bit i =
+// tile t0 + i); the others take the general load + step afterwards.
+//
+// REF (reference rows, kernels.h rflag_*): a tile whose 8 peers' rows are all
+// flagged equal to the reference row takes the reference word (one hoisted
+// load per run) for all 8 votes instead of gathering them; the flag bytes
+// (1 MB at C4) are L2-resident where the rows (128 MB) are not. Every settled
+// tile writes its nodes' flags for the row it published.
+template <int POL, bool REF>
+__device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t lane, uint32_t tile_end,
+                                                const WaveDraw& wd, SweepAcc& acc) {
+  const uint32_t t0 = wd.t0, ntiles = tile_end - t0;
+  const uint32_t b = lane & (p.BL - 1u), bo = b * 4u;
+  const uint32_t vw = at_byte(p.valid, bo);
+  // Byzantine bits of the run's nodes (local nodes nlA .. nlA + nn - 1, nn <= 64)
+  const unsigned long long byzm = __ballot(lane < wd.nn && is_byz(p.byz, p.n0 + wd.nlA + lane));
+  const uint32_t bpat = byz_pattern(p.round + 1u);
+  const __amdgpu_buffer_rsrc_t ta =
+      __builtin_amdgcn_make_buffer_rsrc(p.planes + (size_t)t0 * (kPlanes * 64u), 0, (int)(ntiles * kPlanes * 64u * 4u),
+                                        kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
+  const uint32_t aoff = (1536u + lane) * 4u;
+  // reference words of this lane's block: the snapshot being written is flagged against rin, the
+  // flags of the snapshot being read were written against rprev
+  const uint32_t rin = REF ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
+  const uint32_t rprev = REF && p.rflag_in ? at_byte(p.pref_prev, p.ref_node * p.PS * 4u + bo) : 0u;
+  uint32_t done = 0u;
+  uint32_t applied = 0u, bytes = 0u, reread = 0u;  // per lane
+  for (uint32_t i = 0; i < ntiles; ++i) {
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)wd.meta, (int)i);
+    if ((m & (kPendAllLive | (kVMask << 8))) != (kPendAllLive | (kVUniform << 8))) continue;
+    const uint32_t tile = t0 + i;
+    const uint32_t A = __builtin_amdgcn_raw_buffer_load_b32(ta, aoff + i * (kPlanes * 64u * 4u), 0, POL > 0 ? 2 : 0);
+    const uint32_t g = tile * 64u + lane;
+    const bool active = g < p.L;
+    const uint32_t nl = (active ? g : p.L - 1u) >> p.bl_log2;
+    const uint32_t P0 = active ? vw : 0u;  // polled = live (kPendAllLive) and valid
+    const uint32_t rel = nl - wd.nlA;
+    uint32_t rows[8];
+    {
+      const uint32_t* q = wd.sd + (rel * 2u + (wd.pair ? 32u : 0u)) * 4u;
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(q);
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(q + 4);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        rows[c] = lo[c];
+        rows[c + 4] = hi[c];
+      }
+    }
+    uint32_t dis = 0u, all = ~0u;
+    bool gather = true;
+    if (REF && p.rflag_in) {
+      uint32_t fl = 1u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fl &= p.rflag_in[rows[j] >> p.ps_shift];
+      if (fl) {
+        dis = all = rprev;
+        gather = false;
+      }
+    }
+    if (gather) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t w = at_byte(p.pref_in, rows[j] + bo);
+        dis |= w;
+        all &= w;
+      }
+    }
+    // every vote equals A  <=>  (OR of votes) == A == (AND of votes) on P0
+    if (__ballot(((dis ^ A) | (all ^ A)) & P0) != 0ull) continue;
+    const uint32_t node = p.n0 + nl;
+    const uint32_t pub = ((byzm >> rel) & 1ull) ? bpat : A;
+    if (active) {
+      const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
+      if (p.push_n) {  // peer-push exchange: as process_tile
+        const uint32_t old = p.pref_out[prow];
+        if (pub != old) {
+          for (uint32_t r = 0; r < p.push_n; ++r)
+            __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
+    }
+    if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, rin);
+    done |= 1u << i;
+    applied += 8u * (uint32_t)__popc(P0);
+    // settled_tile's accounting: 40 B per active lane (+ 4 B push read), 28 of the 32 gathered re-read;
+    // reference rows: the 8 flag bytes per node instead of the 32 B of votes, the flag byte written
+    bytes += active ? 40u + (p.push_n ? 4u : 0u) - (gather ? 0u : 32u) +
+                          (REF && p.rflag_in ? (b == 0u ? 8u : 0u) : 0u) + (REF && p.rflag_out ? (b == 0u ? 1u : 0u) : 0u)
+                    : 0u;
+    reread += active && gather ? 28u : 0u;
+  }
+  // the settled tiles' pending count steps: +1 deferred +8 step each (lane i: tile t0 + i)
+  if (lane < ntiles && ((done >> lane) & 1u)) {
+    p.kpend[t0 + lane] = ((wd.meta & 0xFFu) + 1u) | kPendAllLive;
+    bytes += 8u;  // kpend read (prologue) + written
+  }
+  acc.applied += applied;
+  acc.lane_bytes += bytes;
+  acc.reread += reread;
+  return done;
 }
 
 // MODE: kModeWarm (sim, every consider plane all-ones), kModeCheck (sim, per
@@ -757,6 +892,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     wd.ok = false;
     wd.pair = false;
     wd.nlA = 0u;
+    wd.nn = 0u;
     wd.t0 = 0u;
     wd.meta = 0u;
     wd.bad = 0ull;
@@ -782,6 +918,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][256];
           const PairDraw d = any_stale ? pair_draw(p, p.round, nlA, nn, lane) : single_draw(p, p.round, nlA, nn, lane);
           wd.nlA = nlA;
+          wd.nn = nn;
           wd.pair = any_stale;
           wd.ok = !d.fallback;
           wd.bad = d.bad;
@@ -790,11 +927,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         }
       }
     }
+    uint32_t lean_done = 0u;  // run tiles the lean settled loop completed (bit i: tile wd.t0 + i)
+    bool lean_ran = false;    // the run's settled candidates were all tested by it
+    if constexpr (MODE == kModeWarm && K == 8) {
+      if (wd.ok && wd.bad == 0ull && p.lean && p.settled_fast && p.klazy && p.vv && tile < tile_end) {
+        lean_done = settled_run<POL, REF>(p, lane, tile_end, wd, acc);
+        lean_ran = true;
+      }
+    }
     for (; tile < tile_end; tile += stride) {
       constexpr bool AB = MODE == kModeAblate;
       if constexpr (MODE == kModeWarm) {
         if constexpr (K == 8) {
-          if (wd.ok && p.settled_fast && p.klazy && p.vv) {
+          if (lean_done && ((lean_done >> (tile - wd.t0)) & 1u)) continue;
+          if (wd.ok && p.settled_fast && p.klazy && p.vv && !lean_ran) {
             const uint32_t m = meta_of(wd, tile);
             if (((m >> 8) & kVMask) == kVUniform && (m & kPendAllLive) && settled_tile<POL, REF>(p, tile, lane, m & 0x800000FFu, wd, acc))
               continue;
@@ -837,11 +983,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   const unsigned long long s = wave_sum(acc.applied);
   const unsigned long long f = __ballot(acc.died != 0u) ? wave_sum(acc.died) : 0ull;
   const unsigned long long by = (unsigned long long)wave_sum(acc.lane_bytes) + acc.emitted_bytes;
+  const unsigned long long rr = wave_sum(acc.reread);
   if (lane == 0) {
     const uint32_t shard = wave0 % p.log_shards;
     if (s) atomicAdd(&p.applied[shard], s);
     if (f) atomicAdd(&p.finalized[shard], f);
     if (by) atomicAdd(&p.bytes[shard], by);
+    if (rr) atomicAdd(&p.bytes[kLogShards + shard], rr);
     if (acc.updates) atomicAdd(&p.upd_count[shard], acc.updates);
   }
 }

@@ -78,7 +78,7 @@ EXPORTED = [
     "av_init_records", "av_add_targets", "av_set_valid", "av_register_votes", "av_is_accepted",
     "av_get_confidence", "av_get_invs", "av_get_invs_batch", "av_run_rounds", "av_replay_round_errs", "av_replay_prepare",
     "av_replay_rounds", "av_synchronize", "av_round_index", "av_updates_count", "av_fetch_updates",
-    "av_update_log_overflowed", "av_applied_votes", "av_alg_bytes", "av_finalized_count", "av_live_records", "av_discard_updates", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
+    "av_update_log_overflowed", "av_applied_votes", "av_alg_bytes", "av_alg_bytes_reread", "av_finalized_count", "av_live_records", "av_discard_updates", "av_read_records", "av_write_records", "av_read_pref", "av_sample_peers",
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
     "av_peer_handles", "av_peer_init", "av_get_round", "av_set_round", "av_log_base_round", "av_updates_digest",
     "av_updates_digest_range", "av_read_pref_words", "av_set_polling",
@@ -124,6 +124,7 @@ def lib():
         "av_update_log_overflowed": (i32, [_vp, P(i32)]),
         "av_applied_votes": (i32, [_vp, P(i64)]),
         "av_alg_bytes": (i32, [_vp, P(i64)]),
+        "av_alg_bytes_reread": (i32, [_vp, P(i64)]),
         "av_finalized_count": (i32, [_vp, P(i64)]),
         "av_live_records": (i32, [_vp, i32, P(i64)]),
         "av_discard_updates": (i32, [_vp]),
@@ -258,7 +259,14 @@ class Engine:
         of = np.ascontiguousarray(offsets, np.int64)
         t = np.ascontiguousarray(targets, np.int64)
         e = np.ascontiguousarray(errs, np.uint32)
-        assert of.size == nd.size + 1 and t.size == e.size == (of[-1] if of.size else 0)
+        # the C entry point reads targets/errs up to offsets[n]: check the lengths here (not with
+        # assert, which `python -O` strips)
+        if of.size != nd.size + 1:
+            raise ValueError(f"offsets has {of.size} entries, expected len(nodes) + 1 = {nd.size + 1}")
+        if of[0] != 0 or np.any(np.diff(of) < 0):
+            raise ValueError("offsets must start at 0 and be non-decreasing")
+        if not (t.size == e.size == of[-1]):
+            raise ValueError(f"targets ({t.size}) and errs ({e.size}) must both have offsets[-1] = {of[-1]} entries")
         st = np.zeros(max(1, t.size), np.int32)
         _check(lib().av_register_votes_batch(self._h, nd.size, _ptr(nd), _ptr(of), _ptr(t), _ptr(e), _ptr(st)))
         return st[: t.size]
@@ -399,6 +407,12 @@ class Engine:
     def alg_bytes(self):
         out = C.c_int64(0)
         _check(lib().av_alg_bytes(self._h, C.byref(out)))
+        return out.value
+
+    def alg_bytes_reread(self):
+        """Part of alg_bytes() that re-reads preference words already gathered in the same round."""
+        out = C.c_int64(0)
+        _check(lib().av_alg_bytes_reread(self._h, C.byref(out)))
         return out.value
 
     def read_records(self, n0=None, n1=None, t0=None, t1=None):

@@ -214,6 +214,12 @@ int av_discard_updates(av_engine* e);
  * read/written, gathered vote words, published words, 8 B per StatusUpdate
  * (DESIGN.md §3). */
 int av_alg_bytes(av_engine* e, int64_t* out);
+/* The part of av_alg_bytes that re-reads a published preference word another
+ * lane already gathered in the same round (k_round_sweep: 28 B of the 8 peer
+ * words per lane, 24 B of a stale tile's 7 regathered words). av_alg_bytes
+ * minus this = the compulsory bytes (every word read or written once), a lower
+ * bound on HBM traffic. Diagnostics; no reference counterpart. */
+int av_alg_bytes_reread(av_engine* e, int64_t* out);
 /* Canonical words for local nodes [n0,n1) x targets [t0,t1) (global ids). */
 int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint32_t* out);
 int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, const uint32_t* in);

@@ -126,6 +126,78 @@ def test_c4_fullsize_rounds_16_20(c4_pair):
     assert eng.live_records() == 0
 
 
+# ------------------------------------------------------------------ C4p / C4pb
+# The north star's "1M nodes x 1k conflicting targets": targets (2p, 2p+1) are
+# double-spend pairs with complementary initial IsAccepted per node (SURVEY.md
+# R4), honest (c4p) or with 20 % Byzantine flip-flop voters (c4pb, as C3).
+# Flips go on round after round (no record settles), so every round takes the
+# general step and emits StatusUpdates.
+C4P = dict(n=1_000_000, m=1000)
+
+
+def c4p_fixture(byz):
+    n, m = C4P["n"], C4P["m"]
+    eng = avhip.Engine(n, m, k=8, seed=SEED, byz_threshold=byz, log_capacity=600_000_000)
+    eng.init_records(avhip.INIT_PAIRS, 0)
+    return eng
+
+
+@pytest.fixture(scope="module")
+def c4pb_pair(oracle):
+    n, m = C4P["n"], C4P["m"]
+    eng = c4p_fixture(BYZ20)
+    sim = oracle.Sim(n, m, 8, seed=SEED, byz_threshold=BYZ20, init_mode=avhip.INIT_PAIRS, threads=T)
+    st = {"applied": 0, "round": 0, "emitted": []}
+    yield eng, sim, st
+    eng.close()
+    sim.close()
+
+
+def run_c4p(pair, last, states):
+    eng, sim, st = pair
+    n, m = C4P["n"], C4P["m"]
+    while st["round"] <= last:
+        r = st["round"]
+        applied, nupd = step(eng, sim, r)
+        print(f"C4pb round {r}: {nupd} StatusUpdates, digest equal", flush=True)
+        st["applied"] += applied
+        st["emitted"].append(nupd)
+        st["round"] += 1
+        if r < 16:  # nothing can finalize before round 16 (>= 134 votes): all N*M*k applied
+            assert applied == n * m * 8, r
+        assert eng.applied_votes() == st["applied"], r
+        if r in states:
+            compare_state(eng, sim, n, f"C4pb after round {r}")
+
+
+def test_c4pb_fullsize_rounds_0_10(c4pb_pair):
+    """1M x 500 double-spend pairs with 20 % Byzantine flip-flop voters: the
+    update digest every round, the full state at rounds 3 and 10."""
+    run_c4p(c4pb_pair, 10, {3, 10})
+    # conflicting preferences keep flipping: every round emits StatusUpdates
+    assert all(e > 0 for e in c4pb_pair[2]["emitted"]), c4pb_pair[2]["emitted"]
+
+
+def test_c4pb_fullsize_rounds_11_20(c4pb_pair):
+    """Through the first finalizations (round 16 on) to round 20."""
+    run_c4p(c4pb_pair, 20, {16, 20})
+
+
+def test_c4p_honest_rounds_0_6(oracle):
+    """The honest pairs network (c4p), rounds 0-6: digests every round, state at round 6."""
+    n, m = C4P["n"], C4P["m"]
+    eng = c4p_fixture(0)
+    sim = oracle.Sim(n, m, 8, seed=SEED, init_mode=avhip.INIT_PAIRS, threads=T)
+    try:
+        for r in range(7):
+            applied, _ = step(eng, sim, r)
+            assert applied == n * m * 8, r
+        compare_state(eng, sim, n, "C4p after round 6")
+    finally:
+        eng.close()
+        sim.close()
+
+
 # ------------------------------------------------------------------ C3
 C3 = dict(n=100_000, m=2000)
 

@@ -92,7 +92,7 @@ for s in "$@"; do
     pmcb_write) step pmcb_write_${WL:-c4} 600 timeout -s KILL 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmcb_write_${WL:-c4} -o bench -- \
             python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary ;;
     pmcb_sum) step pmcb_sum_${WL:-c4} 300 python tools/pmc_bench.py --workload ${WL:-c4} --sq $OUT/pmcb_sq_${WL:-c4} --fetch $OUT/pmcb_fetch_${WL:-c4} \
-            --write $OUT/pmcb_write_${WL:-c4} --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write ${PMC_LAUNCHES:+--launches $PMC_LAUNCHES} --out $OUT/pmc_${WL:-c4}.json ;;
+            --write $OUT/pmcb_write_${WL:-c4} --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write ${PMC_LAUNCHES:+--launches $PMC_LAUNCHES} ${PMC_REPLAY:+--replay} --out $OUT/pmc_${WL:-c4}.json ;;
     pmc_fetch) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o bench -- \
             python3 bench.py --no-cpu-baseline --no-secondary ;;
     pmc_write) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o bench -- \
@@ -135,6 +135,15 @@ for s in "$@"; do
     probe_settled) step probe_settled 600 bash -c 'for o in "ablate_settled=0" "ablate_settled=1" "ablate_settled=2" "ablate_settled=4" "ablate_settled=8" "ablate_settled=15" "ablate_settled=7"; do echo "== $o"; python tools/round_probe.py --workload c4 --option $o | grep "\"round\": 1[0-2],"; done' ;;
     benchwin) step benchwin 900 bash -c 'python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-secondary && python bench.py --steps 5 --warmup 0 --no-cpu-baseline --no-secondary && python bench.py --steps 100 --warmup 3 --no-cpu-baseline --no-secondary' ;;
     probe_tpw) step probe_tpw 600 bash -c 'for w in c4 c3; do for o in "tiles_per_wave=4" "tiles_per_wave=6" "tiles_per_wave=8" "tiles_per_wave=3"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o | tail -1 | grep -o "kernel_ms_total.*"; done; done' ;;
+    c4ptests) step c4ptests 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread -k "c4p" ;;
+    hostcpu) step hostcpu 300 bash -c 'cat /sys/fs/cgroup/cpu.max; nproc; python -c "import bench, json; print(json.dumps(bench.host_cpus()))"; for t in 16 32 64 128; do python tools/cpu_scaling.py --threads $t; done' ;;
+    bench_c4p) step bench_c4p 900 python bench.py --workload c4p --no-cpu-baseline --no-secondary ;;
+    bench_c4pb) step bench_c4pb 900 python bench.py --workload c4pb --no-cpu-baseline --no-secondary ;;
+    probe_lean) step probe_lean 600 bash -c 'for w in c4 c5; do for o in "settled_lean=1" "settled_lean=0"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
+    fullc4) step fullc4 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread -k "c4_fullsize" ;;
+    probe_ref2) step probe_ref2 600 bash -c 'for w in c4 c5; do for o in "ref_rows=1" "ref_rows=0"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
+    reftests) step reftests 900 python -u -m pytest tests/test_gpu_ref_rows.py tests/test_gpu_virtual_votes.py tests/test_gpu_fresh.py tests/test_gpu_count_lazy.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    fullc5) step fullc5 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread -k "c5" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """PMC summary of exactly the bench window, for bench.py's roofline
-(profiles/r02/pmc_<workload>.json, used only while its src_sha matches the
-kernel sources).
+(profiles/r03/pmc_<workload>.json, used only while its src_sha matches the
+kernel sources): window averages and one row per roofline-pass step.
 
 bench.py runs, per workload: one untimed device warm-up epoch, goto(warmup),
 the timed steps, goto(warmup) again and the roofline pass — the same rounds
@@ -16,9 +16,11 @@ group, MI355X_MICROARCH.md §HBM / the 8-SQ-counter limit):
           SQ_INSTS_LDS SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
   --fetch FETCH_SIZE      --write WRITE_SIZE
   --calib-fetch / --calib-write: bin/pmc_calib under FETCH_SIZE / WRITE_SIZE
-HBM bytes = FETCH_SIZE (KiB) / measured-over-true read ratio + WRITE_SIZE /
+Fabric bytes = FETCH_SIZE (KiB) / measured-over-true read ratio + WRITE_SIZE /
 write ratio (the calibration kernels move a known 1 GiB with dword and dwordx4
 accesses; both read widths measure 0.5, both write widths 1.0 on gfx950).
+These are the L2's memory-side (EA) requests: Infinity-Cache hits are
+included (MI355X_MICROARCH.md §HBM), so they bound the HBM bytes from above.
 
 Issue fractions (MI355X_MICROARCH.md: a wave64 VALU instruction occupies its
 SIMD for 2 cycles; one scalar unit per CU issues one SALU instruction per
@@ -34,7 +36,9 @@ import os
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROUND_KERNELS = ("k_round_sweep", "k_round_node", "k_replay_node", "k_round_fast", "k_round_capped")
+ROUND_KERNELS = ("k_round_sweep", "k_round_node", "k_replay_node", "k_round_fast", "k_round_capped", "k_peer_table")
+# launched before the round kernel of the same round (counted with the next primary dispatch)
+PRE = ("k_peer_table",)
 # the kernel a launch of the bench's roofline pass is counted by (k_round_capped also runs as the
 # exact pass behind k_round_node / k_replay_node)
 PRIMARY = ("k_round_sweep", "k_round_node", "k_replay_node", "k_round_fast")
@@ -64,6 +68,34 @@ def window(d, launches):
     if len(prim) < launches:
         raise SystemExit(f"{d}: {len(prim)} round-kernel launches, need {launches}")
     return rounds[prim[-launches]:]
+
+
+def groups(win):
+    """The window's dispatches grouped per launch of the bench's roofline pass:
+    PRE kernels with the primary that follows them, the exact passes
+    (k_round_capped) with the primary before them."""
+    out, pending = [], []
+    for x in win:
+        if any(k in x[1] for k in PRE):
+            pending.append(x)
+        elif any(k in x[1] for k in PRIMARY):
+            out.append(pending + [x])
+            pending = []
+        elif out:
+            out[-1].append(x)
+    return out
+
+
+def step_rounds(warmup, steps, replay, epoch=16):
+    """bench.py's roofline-pass segmentation: the first round of each launch."""
+    rows, pos, left = [], warmup, steps
+    while left > 0:
+        rnd = pos % epoch
+        seg = min(epoch - rnd, left) if replay else 1
+        rows.append(rnd)
+        pos += seg
+        left -= seg
+    return rows
 
 
 def mean_of(win, counter, launches):
@@ -101,6 +133,7 @@ def main():
     ap.add_argument("--calib-fetch", required=True)
     ap.add_argument("--calib-write", required=True)
     ap.add_argument("--calib-bytes", type=int, default=1 << 30)
+    ap.add_argument("--replay", action="store_true", help="replay workload (C2): fused launches per segment")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -112,6 +145,23 @@ def main():
 
     n = a.launches or a.steps
     wf, ww, wq = window(a.fetch, n), window(a.write, n), window(a.sq, n)
+    gf, gw, gq = groups(wf), groups(ww), groups(wq)
+    rounds = step_rounds(a.warmup, a.steps, a.replay)
+    if not (len(gf) == len(gw) == len(gq) == len(rounds) == n):
+        raise SystemExit(f"window groups {len(gf)}/{len(gw)}/{len(gq)} vs {len(rounds)} roofline-pass launches")
+
+    def tot(g, c):
+        return sum(x[2][c] for x in g)
+
+    per_round = []
+    for r, f_, w_, q_ in zip(rounds, gf, gw, gq):
+        per_round.append({
+            "round": r, "kernels": [x[1].split("(")[0].split("::")[-1] for x in q_],
+            "fabric_bytes": tot(f_, "FETCH_SIZE") * 1024 / read_ratio + tot(w_, "WRITE_SIZE") * 1024 / write_ratio,
+            "cycles": tot(q_, "GRBM_GUI_ACTIVE") / 8.0, "valu": tot(q_, "SQ_INSTS_VALU"), "salu": tot(q_, "SQ_INSTS_SALU"),
+            "wait_any": tot(q_, "SQ_WAIT_ANY"), "wave_cycles": tot(q_, "SQ_WAVE_CYCLES"),
+            "waves": tot(q_, "SQ_WAVES"), "vmem_rd": tot(q_, "SQ_INSTS_VMEM_RD"), "lds": tot(q_, "SQ_INSTS_LDS"),
+        })
     names = sorted({n for _, n, _ in wq})
     read = mean_of(wf, "FETCH_SIZE", n) * 1024 / read_ratio
     write = mean_of(ww, "WRITE_SIZE", n) * 1024 / write_ratio
@@ -125,9 +175,10 @@ def main():
         "dispatches": len(wq),
         "launches": n,
         "calibration_measured_over_true": {"read_x4": rf, "read_x1": rf1, "write_x4": rw, "write_x1": rw1},
-        "hbm_read_bytes_per_launch": read,
-        "hbm_write_bytes_per_launch": write,
-        "hbm_bytes_per_launch": read + write,
+        "fabric_read_bytes_per_launch": read,
+        "fabric_write_bytes_per_launch": write,
+        "fabric_bytes_per_launch": read + write,
+        "per_round": per_round,
         "issue": {
             "cycles_per_launch": cyc,
             "valu_per_launch": valu,
@@ -144,7 +195,8 @@ def main():
         },
         "source": {"sq": a.sq, "fetch": a.fetch, "write": a.write},
         "note": "per launch of the bench's roofline pass (its round-kernel dispatches, summed, / launches: the same "
-                "rounds as the timed steps); FETCH_SIZE / WRITE_SIZE corrected by bin/pmc_calib's measured/true ratios",
+                "rounds as the timed steps); FETCH_SIZE / WRITE_SIZE corrected by bin/pmc_calib's measured/true ratios "
+                "= fabric bytes (L2 <-> EA, Infinity-Cache hits included)",
     }
     print(json.dumps(out, indent=1))
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
