@@ -10,8 +10,10 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -78,6 +80,7 @@ struct av_engine {
   int64_t ref_node = -1;  // first honest node (chosen at the first round that can use it); -2: none
   size_t rflag_off = 0;   // byte offset of the flags in a snapshot buffer
   bool rflag_ok[3] = {false, false, false};
+
   int cur = 0;
   static int nxt(int c) { return c == 2 ? 0 : c + 1; }
   static int prv(int c) { return c == 0 ? 2 : c - 1; }
@@ -185,6 +188,9 @@ struct av_engine {
   std::vector<void*> peer_opened;                    // IPC mappings to close
   avk::PeerPtrs peer_arrive{};
   uint32_t** push_tbl = nullptr;                     // device [3][kMaxPeers]: peers' replicas of each buffer
+  uint32_t** arrive_tbl = nullptr;                   // device [world]: every rank's arrival array
+  uint32_t* wave_done = nullptr;                     // device [2]: waves of the round counted (kernels.h)
+  bool fold_arrival = true;                          // option "fold_arrival": the sweep stores the arrival
 
   // responder variant (option "responder", kernels.h pub_mode) and the nodes
   // that no longer poll (av_set_polling); both run the first-generation kernel
@@ -202,6 +208,11 @@ struct av_engine {
   void* fetch_scratch = nullptr;
   size_t fetch_scratch_bytes = 0;
   unsigned long long* digest = nullptr;  // [3]
+  // drop-in batches (av_register_votes_batch): pinned host staging; option "dropin_fast" (0: always the
+  // sort-grouped general path, A/B and tests)
+  void* dropin_host = nullptr;
+  size_t dropin_host_bytes = 0;
+  bool dropin_fast = true;
 
   size_t round_replay_words() const { return avk::replay_words(Lpad, k); }
 };
@@ -478,6 +489,13 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   if (peer && sweep && !replay) {
     p.push_n = (uint32_t)e->peer_world - 1u;
     p.push_dst = e->push_tbl + (size_t)nb * avk::kMaxPeers;
+    if (e->fold_arrival) {  // the round kernel's last wave stores this rank's arrival
+      p.arrive_dst = e->arrive_tbl;
+      p.arrive_n = (uint32_t)e->peer_world;
+      p.arrive_rank = (uint32_t)e->peer_rank;
+      p.arrive_seq = ++e->barrier_seq;
+      p.wave_done = e->wave_done;
+    }
   }
   // reference rows: sweep rounds at k = 8 with a node's lanes inside one wave
   bool refr = e->ref_rows && sweep && e->k == 8 && !replay && 64 % e->BL == 0 && !e->comm && !e->ablate_gather;
@@ -486,10 +504,18 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     if (rc != AV_OK) return rc;
     refr = e->ref_node >= 0;
   }
+  if (refr && ((e->round + 1) & 127) == 0) {
+    // flag bytes carry a 7-bit snapshot tag (round_sweep.hip ref_tag): clear every buffer's flags
+    // every 128 rounds so that no byte outlives its tag's period
+    for (int b = 0; b < 3; ++b)
+      AV_HIP(hipMemsetAsync(reinterpret_cast<uint8_t*>(e->pref[b]) + e->rflag_off, 0, (size_t)e->N, e->stream));
+    ref_invalidate(e);
+  }
   if (refr) {
     p.ref_node = (uint32_t)e->ref_node;
     p.ps_shift = (uint32_t)__builtin_ctz(e->PS * 4u);
     p.rflag_off = (uint32_t)e->rflag_off;
+
     p.rflag_out = reinterpret_cast<uint8_t*>(e->pref[nb]) + e->rflag_off;
     p.rflag_in = e->rflag_ok[e->cur] ? reinterpret_cast<const uint8_t*>(e->pref[e->cur]) + e->rflag_off : nullptr;
   }
@@ -532,8 +558,13 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
       int rc = push_own_rows(e, nb);
       if (rc != AV_OK) return rc;
     }
-    int rc = peer_barrier(e);
-    if (rc != AV_OK) return rc;
+    if (p.arrive_n) {  // the arrival was stored by the round kernel: wait only
+      AV_HIP(avk::launch_peer_wait(e->peer_arrive, (uint32_t)e->peer_world, (uint32_t)e->peer_rank, p.arrive_seq,
+                                   e->barrier_err, e->barrier_timeout_ms, e->stream));
+    } else {
+      int rc = peer_barrier(e);
+      if (rc != AV_OK) return rc;
+    }
   }
   if (e->comm) {
     const size_t count = (size_t)e->NL * e->PS;
@@ -665,8 +696,11 @@ int av_destroy(av_engine* e) {
   if (e->arrive) (void)hipFree(e->arrive);
   if (e->barrier_err_host) (void)hipHostFree(const_cast<uint32_t*>(e->barrier_err_host));
   if (e->fetch_scratch) (void)hipFree(e->fetch_scratch);
+  if (e->dropin_host) (void)hipHostFree(e->dropin_host);
   if (e->digest) (void)hipFree(e->digest);
   if (e->push_tbl) (void)hipFree(e->push_tbl);
+  if (e->arrive_tbl) (void)hipFree(e->arrive_tbl);
+  if (e->wave_done) (void)hipFree(e->wave_done);
   if (e->marker) (void)hipEventDestroy(e->marker);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->kpend, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->readd, e->died_out, e->nopoll,
@@ -779,6 +813,7 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->finalized, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
   (void)hipMemsetAsync(e->finalized, 0, avk::kLogShards * 8, e->stream);
   if ((he = dev_alloc(&e->scratch_count, 1)) != hipSuccess) return hip_fail(he, "alloc counters");
+
   (void)hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
   (void)hipMemsetAsync(e->applied, 0, avk::kLogShards * 8, e->stream);
@@ -923,76 +958,68 @@ int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uin
   return AV_OK;
 }
 
+extern "C++" {
 namespace {
-// Batches of at least this many votes are grouped by lane on the device
-// (radix sort + run-length encode, log_ops.hip launch_group_votes) instead of
-// a host sort: the host sort of 32M (lane, vote) pairs took ~1 s.
-constexpr size_t kDeviceGroupVotes = 1u << 16;
+// Host work of the drop-in path (packing the caller's votes, expanding the
+// statuses) split over threads for large batches: the box's CPU share
+// (OMP_NUM_THREADS, else up to 16 hardware threads).
+int host_threads() {
+  static const int n = [] {
+    int t = 0;
+    if (const char* s = std::getenv("OMP_NUM_THREADS")) t = std::atoi(s);
+    if (t <= 0) t = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+    return std::max(1, std::min(t, 64));
+  }();
+  return n;
+}
 
-int register_votes_device(av_engine* e, const std::vector<std::pair<uint32_t, uint32_t>>& lv, const int64_t* targets,
-                          const uint32_t* errs, int64_t n, int32_t* status_out) {
-  const uint32_t m = (uint32_t)lv.size();
-  std::vector<uint32_t> host(3 * (size_t)m);  // keys | vote index | packed vote
-  for (uint32_t i = 0; i < m; ++i) {
-    const uint32_t v = lv[i].second;
-    const int64_t tl = targets[v] - e->t0;
-    const uint32_t err = errs[v];
-    host[i] = lv[i].first;
-    host[m + i] = v;
-    host[2 * (size_t)m + i] = (uint32_t)(tl & 31) | ((err == 0u ? 1u : 0u) << 5) | (((int32_t)err >= 0 ? 1u : 0u) << 6);
+template <class F>
+void parallel_chunks(int64_t n, int64_t min_chunk, F f) {
+  const int t = (int)std::max<int64_t>(1, std::min<int64_t>(host_threads(), n / std::max<int64_t>(1, min_chunk)));
+  if (t <= 1) {
+    f(0, (int64_t)0, n);
+    return;
   }
-  const uint64_t lanes_total = (uint64_t)e->NL * e->BL;
-  int key_bits = 1;
-  while (key_bits < 32 && (1ull << key_bits) < lanes_total) ++key_bits;
-  size_t tb = 0;
-  AV_HIP(avk::launch_group_votes(nullptr, &tb, nullptr, nullptr, nullptr, m, key_bits, nullptr, nullptr, nullptr, nullptr,
-                                 nullptr, nullptr, nullptr, nullptr, e->stream));
-  // keys vidx info keys_s perm perm_s lanes counts(m+1) offs(m+1) nruns entries(2m) status(n) temp
-  const size_t words = 7 * (size_t)m + 2 * ((size_t)m + 1) + 1 + 2 * (size_t)m + (size_t)n;
-  void* buf = nullptr;
-  int rc = engine_scratch(e, words * 4 + tb + 256, &buf);
-  if (rc != AV_OK) return rc;
-  auto* w = static_cast<uint32_t*>(buf);
-  uint32_t *keys = w, *vidx = keys + m, *info = vidx + m, *keys_s = info + m, *perm = keys_s + m, *perm_s = perm + m,
-           *lanes = perm_s + m, *counts = lanes + m, *offs = counts + m + 1, *nruns = offs + m + 1, *ent = nruns + 1;
-  auto* dstat = reinterpret_cast<int32_t*>(ent + 2 * (size_t)m);
-  void* temp = reinterpret_cast<void*>(((uintptr_t)(dstat + n) + 255) & ~(uintptr_t)255);
-  AV_HIP(hipMemcpyAsync(keys, host.data(), host.size() * 4, hipMemcpyHostToDevice, e->stream));
-  AV_HIP(avk::launch_group_votes(temp, &tb, keys, vidx, info, m, key_bits, keys_s, perm, perm_s, lanes, counts, offs,
-                                 nruns, ent, e->stream));
-  AV_HIP(hipMemsetAsync(dstat, 0xFF, (size_t)n * 4, e->stream));
-  uint32_t nb = 0;
-  AV_HIP(hipMemcpyAsync(&nb, nruns, 4, hipMemcpyDeviceToHost, e->stream));
-  AV_HIP(hipStreamSynchronize(e->stream));
-  avk::DropInParams p{};
-  p.planes = e->planes;
-  p.pref = e->pref[e->cur];
-  p.valid = e->valid;
-  p.byz = e->byz;
-  p.blocks = lanes;
-  p.offs = offs;
-  p.entries = ent;
-  p.status_out = dstat;
-  p.n_blocks = nb;
-  p.n0 = (uint32_t)e->n0;
-  p.BL = e->BL;
-  p.PS = e->PS;
-  p.round = (uint32_t)e->round;
-  p.pub_mode = (uint32_t)e->pub_mode;
-  AV_HIP(avk::launch_register_votes(p, e->stream));
-  AV_HIP(hipMemcpyAsync(status_out, dstat, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
-  AV_HIP(hipStreamSynchronize(e->stream));
+  std::vector<std::thread> th;
+  th.reserve(t);
+  for (int i = 0; i < t; ++i) th.emplace_back([&, i] { f(i, n * i / t, n * (i + 1) / t); });
+  for (auto& x : th) x.join();
+}
+
+// Pinned host staging of the drop-in path, grown on demand and kept by the engine.
+int dropin_staging(av_engine* e, size_t bytes) {
+  if (bytes <= e->dropin_host_bytes) return AV_OK;
+  if (e->dropin_host) AV_HIP(hipHostFree(e->dropin_host));
+  e->dropin_host = nullptr;
+  e->dropin_host_bytes = 0;
+  const size_t want = std::max(bytes, (size_t)1 << 20);
+  AV_HIP(hipHostMalloc(&e->dropin_host, want, hipHostMallocDefault));
+  e->dropin_host_bytes = want;
   return AV_OK;
 }
 }  // namespace
+}  // extern "C++"
 
 int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const uint32_t* errs, int64_t n,
                       int32_t* status_out) {
-  if (e) ref_invalidate(e);
   const int64_t offs[2] = {0, n};
   return av_register_votes_batch(e, 1, &node, offs, targets, errs, status_out);
 }
 
+// Many Responses in one call (processor.go:61-122 for each, in order). The
+// host packs each vote into one u32 (target's local index, unknown-hash, yes
+// and considered bits: dropin_word) in pinned memory, in parallel, and checks
+// on the way whether every Response has strictly ascending targets (a poll
+// set's order, rule R1). Then:
+//  * fast path (it holds): one workgroup per node applies the node's
+//    Responses in call order, each lane's run of votes where it lies
+//    (k_dropin_resp), no grouping step;
+//  * otherwise: lane keys on the device, stable radix sort of (lane, vote
+//    position) and run-length encoding (launch_group_votes), then
+//    k_register_votes over the runs.
+// Statuses come back as one byte per vote and are widened on the host.
+// Copies: 4 B per vote each way plus 1 B back (the caller's int64 hashes and
+// u32 errs are never copied as such).
 int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, const int64_t* offsets,
                             const int64_t* targets, const uint32_t* errs, int32_t* status_out) {
   if (e) ref_invalidate(e);
@@ -1003,6 +1030,7 @@ int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, 
   }
   AV_CHECK(n_resp >= 0 && (n_resp == 0 || (nodes && offsets)), AV_ERR_INVALID_ARG, "null argument");
   if (n_resp == 0) return AV_OK;
+  AV_CHECK(n_resp < (1ll << 31), AV_ERR_INVALID_ARG, "too many Responses in one call");
   AV_CHECK(offsets[0] == 0, AV_ERR_INVALID_ARG, "offsets[0] must be 0");
   for (int64_t i = 0; i < n_resp; ++i) {
     AV_CHECK(offsets[i + 1] >= offsets[i], AV_ERR_INVALID_ARG, "offsets must not decrease");
@@ -1011,89 +1039,143 @@ int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, 
   const int64_t n = offsets[n_resp];
   AV_CHECK(n == 0 || (targets && errs && status_out), AV_ERR_INVALID_ARG, "null argument");
   AV_CHECK(n < (1ll << 31), AV_ERR_INVALID_ARG, "too many votes in one call");
+  AV_CHECK(e->t1 - e->t0 <= (int64_t)avk::kDropTl + 1, AV_ERR_UNSUPPORTED, "drop-in votes need <= 4M local targets");
   {
     int rc = materialize_votes(e);
     if (rc != AV_OK) return rc;
   }
-  for (int64_t i = 0; i < n; ++i) status_out[i] = -1;
   e->fresh = false;
-  // every vote of every Response applies to its (node, 32-target block) lane
-  // in Response order, then vote order: group the votes by lane, keeping that
-  // order (the global vote index grows with it)
-  std::vector<std::pair<uint32_t, uint32_t>> lv;  // (lane, vote index)
-  lv.reserve((size_t)n);
-  std::vector<int32_t> per_node_votes;
+  // at most one confidence step per vote: bound by the most votes one node gets; the Responses
+  // grouped by node, in call order inside a group (fast path)
   int64_t max_node_votes = 0;
+  std::vector<uint32_t> order((size_t)n_resp), grp_off;
   {
-    std::vector<int64_t> cnt;
-    for (int64_t i = 0; i < n_resp; ++i) {
-      const uint32_t nl = (uint32_t)(nodes[i] - e->n0);
-      for (int64_t v = offsets[i]; v < offsets[i + 1]; ++v) {
-        if (!local_target(e, targets[v])) continue;  // unknown hash (processor.go:95-99)
-        lv.emplace_back(nl * e->BL + (uint32_t)((targets[v] - e->t0) >> 5), (uint32_t)v);
-        if ((int32_t)errs[v] < 0) e->c_monotone = false;  // neutral vote shifts in consider = 0
-      }
-    }
-    // at most one confidence step per vote: bound by the most votes one node gets
-    std::vector<std::pair<uint32_t, int64_t>> nn;
-    for (int64_t i = 0; i < n_resp; ++i) nn.emplace_back((uint32_t)(nodes[i] - e->n0), offsets[i + 1] - offsets[i]);
-    std::sort(nn.begin(), nn.end());
+    std::vector<std::pair<int64_t, uint32_t>> nn((size_t)n_resp);
+    for (int64_t i = 0; i < n_resp; ++i) nn[(size_t)i] = {nodes[i], (uint32_t)i};
+    std::sort(nn.begin(), nn.end());  // (node, Response index): call order inside a node
     for (size_t i = 0; i < nn.size();) {
       int64_t c = 0;
       size_t j = i;
-      for (; j < nn.size() && nn[j].first == nn[i].first; ++j) c += nn[j].second;
+      grp_off.push_back((uint32_t)i);
+      for (; j < nn.size() && nn[j].first == nn[i].first; ++j) {
+        c += offsets[nn[j].second + 1] - offsets[nn[j].second];
+        order[j] = nn[j].second;
+      }
       max_node_votes = std::max(max_node_votes, c);
       i = j;
     }
+    grp_off.push_back((uint32_t)n_resp);
   }
+  const uint32_t n_groups = (uint32_t)grp_off.size() - 1u;
   e->count_bound = (int)std::min<int64_t>(127, e->count_bound + max_node_votes);
-  if (lv.empty()) return AV_OK;
-  if (lv.size() >= kDeviceGroupVotes) return register_votes_device(e, lv, targets, errs, n, status_out);
-  std::sort(lv.begin(), lv.end());
-  std::vector<uint32_t> lanes, offs, entries(2 * lv.size());
-  for (size_t i = 0; i < lv.size(); ++i) {
-    if (i == 0 || lv[i].first != lv[i - 1].first) {
-      lanes.push_back(lv[i].first);
-      offs.push_back((uint32_t)i);
-    }
-    const uint32_t v = lv[i].second;
-    const int64_t tl = targets[v] - e->t0;
-    const uint32_t err = errs[v];
-    entries[2 * i] = v;
-    entries[2 * i + 1] = (uint32_t)(tl & 31) | ((err == 0u ? 1u : 0u) << 5) | (((int32_t)err >= 0 ? 1u : 0u) << 6);
+  if (n == 0) return AV_OK;
+  // ---- pack (pinned): votes, then the Response table
+  const size_t tab_words = 2 * (size_t)n_resp + 1 + (size_t)n_resp + n_groups + 1;  // off, node, order, grp_off
+  const size_t hb = (size_t)n * 5 + tab_words * 4 + 64;
+  {
+    int rc = dropin_staging(e, hb);
+    if (rc != AV_OK) return rc;
   }
-  offs.push_back((uint32_t)lv.size());
-  const size_t nb = lanes.size();
-  const size_t words = nb + (nb + 1) + entries.size() + (size_t)n;
+  auto* hpack = static_cast<uint32_t*>(e->dropin_host);
+  auto* hoff = hpack + n;
+  auto* hnode = hoff + n_resp + 1;
+  auto* horder = hnode + n_resp;
+  auto* hgrp = horder + n_resp;
+  auto* hstat = reinterpret_cast<int8_t*>(hgrp + n_groups + 1);
+  for (int64_t i = 0; i <= n_resp; ++i) hoff[i] = (uint32_t)offsets[i];
+  for (int64_t i = 0; i < n_resp; ++i) hnode[i] = (uint32_t)(nodes[i] - e->n0);
+  std::memcpy(horder, order.data(), (size_t)n_resp * 4);
+  std::memcpy(hgrp, grp_off.data(), ((size_t)n_groups + 1) * 4);
+  std::vector<uint8_t> asc_t(64, 1), neutral_t(64, 0);
+  const int64_t T0 = e->t0, T1 = e->t1;
+  parallel_chunks(n_resp, std::max<int64_t>(1, n_resp * (1 << 18) / std::max<int64_t>(1, n)),
+                  [&](int t, int64_t r0, int64_t r1) {
+    bool asc = true, neutral = false;
+    for (int64_t r = r0; r < r1; ++r) {
+      for (int64_t v = offsets[r]; v < offsets[r + 1]; ++v) {
+        const int64_t tg = targets[v];
+        const uint32_t err = errs[v];
+        hpack[v] = avk::dropin_word(tg - T0, tg >= T0 && tg < T1, err);
+        neutral |= (int32_t)err < 0;
+        if (v > offsets[r]) asc &= tg > targets[v - 1];
+      }
+    }
+    asc_t[t] = asc;
+    neutral_t[t] = neutral;
+  });
+  bool ascending = true;
+  for (int t = 0; t < 64; ++t) {
+    ascending &= asc_t[t] != 0;
+    if (neutral_t[t]) e->c_monotone = false;  // a neutral vote shifts in consider = 0
+  }
+  const bool fast = ascending && e->dropin_fast;
+  // ---- device: packed votes + Response table + byte statuses (+ grouping scratch)
+  size_t tb = 0;
+  int key_bits = 1;
+  const uint32_t m = (uint32_t)n;
+  if (!fast) {
+    const uint64_t keys_total = (uint64_t)e->L + 1;  // L = unknown targets
+    while (key_bits < 32 && (1ull << key_bits) < keys_total) ++key_bits;
+    AV_HIP(avk::launch_group_votes(nullptr, &tb, nullptr, nullptr, nullptr, m, key_bits, nullptr, nullptr, nullptr,
+                                   nullptr, nullptr, nullptr, nullptr, nullptr, e->stream));
+  }
+  // packed | off | node | status bytes || keys vidx info keys_s perm perm_s lanes counts(m+1) offs(m+1) nruns
+  // entries(2m) temp
+  const size_t head_words = (size_t)m + tab_words + ((size_t)m + 3) / 4;
+  const size_t grp_words = fast ? 0 : 7 * (size_t)m + 2 * ((size_t)m + 1) + 1 + 2 * (size_t)m;
   void* buf = nullptr;
-  int rc = engine_scratch(e, words * 4 + 64, &buf);
+  int rc = engine_scratch(e, (head_words + grp_words) * 4 + tb + 512, &buf);
   if (rc != AV_OK) return rc;
-  auto* dlanes = static_cast<uint32_t*>(buf);
-  auto* doffs = dlanes + nb;
-  auto* dent = doffs + nb + 1;
-  auto* dstat = reinterpret_cast<int32_t*>(dent + entries.size());
-  AV_HIP(hipMemcpyAsync(dlanes, lanes.data(), nb * 4, hipMemcpyHostToDevice, e->stream));
-  AV_HIP(hipMemcpyAsync(doffs, offs.data(), (nb + 1) * 4, hipMemcpyHostToDevice, e->stream));
-  AV_HIP(hipMemcpyAsync(dent, entries.data(), entries.size() * 4, hipMemcpyHostToDevice, e->stream));
-  AV_HIP(hipMemsetAsync(dstat, 0xFF, (size_t)n * 4, e->stream));
+  auto* w = static_cast<uint32_t*>(buf);
+  uint32_t *dpack = w, *doff = dpack + m, *dnode = doff + n_resp + 1, *dorder = dnode + n_resp,
+           *dgrp = dorder + n_resp;
+  auto* dstat = reinterpret_cast<int8_t*>(dgrp + n_groups + 1);
+  AV_HIP(hipMemcpyAsync(dpack, hpack, ((size_t)m + tab_words) * 4, hipMemcpyHostToDevice, e->stream));
+  AV_HIP(hipMemsetAsync(dstat, 0xFF, (size_t)m, e->stream));
   avk::DropInParams p{};
   p.planes = e->planes;
   p.pref = e->pref[e->cur];
   p.valid = e->valid;
   p.byz = e->byz;
-  p.blocks = dlanes;
-  p.offs = doffs;
-  p.entries = dent;
   p.status_out = dstat;
-  p.n_blocks = (uint32_t)nb;
   p.n0 = (uint32_t)e->n0;
   p.BL = e->BL;
   p.PS = e->PS;
+  p.L = e->L;
   p.round = (uint32_t)e->round;
   p.pub_mode = (uint32_t)e->pub_mode;
-  AV_HIP(avk::launch_register_votes(p, e->stream));
-  AV_HIP(hipMemcpyAsync(status_out, dstat, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
+  p.packed = dpack;
+  p.resp_off = doff;
+  p.resp_node = dnode;
+  p.n_resp = (uint32_t)n_resp;
+  p.order = dorder;
+  p.grp_off = dgrp;
+  p.n_groups = n_groups;
+  if (fast) {
+    AV_HIP(avk::launch_dropin_resp(p, e->stream));
+  } else {
+    uint32_t* g0 = w + head_words;
+    uint32_t *keys = g0, *vidx = keys + m, *info = vidx + m, *keys_s = info + m, *perm = keys_s + m,
+             *perm_s = perm + m, *lanes = perm_s + m, *counts = lanes + m, *offs = counts + m + 1,
+             *nruns = offs + m + 1, *ent = nruns + 1;
+    void* temp = reinterpret_cast<void*>(((uintptr_t)(ent + 2 * (size_t)m) + 255) & ~(uintptr_t)255);
+    AV_HIP(avk::launch_dropin_keys(p, keys, vidx, info, e->stream));
+    AV_HIP(avk::launch_group_votes(temp, &tb, keys, vidx, info, m, key_bits, keys_s, perm, perm_s, lanes, counts, offs,
+                                   nruns, ent, e->stream));
+    uint32_t nb = 0;
+    AV_HIP(hipMemcpyAsync(&nb, nruns, 4, hipMemcpyDeviceToHost, e->stream));
+    AV_HIP(hipStreamSynchronize(e->stream));
+    p.blocks = lanes;
+    p.offs = offs;
+    p.entries = ent;
+    p.n_blocks = nb;
+    AV_HIP(avk::launch_register_votes(p, e->stream));
+  }
+  AV_HIP(hipMemcpyAsync(hstat, dstat, (size_t)m, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
+  parallel_chunks(n, 1 << 20, [&](int, int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) status_out[i] = hstat[i];
+  });
   return AV_OK;
 }
 
@@ -1680,6 +1762,10 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     }
   } else if (n == "settled_fast") {
     e->settled_fast = value != 0;
+  } else if (n == "fold_arrival") {  // 0: the separate barrier kernel stores the arrival too (A/B)
+    e->fold_arrival = value != 0;
+  } else if (n == "dropin_fast") {
+    e->dropin_fast = value != 0;
   } else if (n == "settled_lean") {
     e->settled_lean = value != 0;
   } else if (n == "wave_runs") {
@@ -1911,6 +1997,12 @@ int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handl
     }
     AV_HIP(dev_alloc(&e->push_tbl, (size_t)3 * avk::kMaxPeers));
     AV_HIP(hipMemcpy(e->push_tbl, tbl, sizeof(tbl), hipMemcpyHostToDevice));
+    uint32_t* arr[avk::kMaxPeers + 1] = {};
+    for (int r = 0; r < world; ++r) arr[r] = e->peer_arrive.p[r];
+    AV_HIP(dev_alloc(&e->arrive_tbl, (size_t)avk::kMaxPeers + 1));
+    AV_HIP(hipMemcpy(e->arrive_tbl, arr, sizeof(arr), hipMemcpyHostToDevice));
+    AV_HIP(dev_alloc(&e->wave_done, 2));
+    AV_HIP(hipMemset(e->wave_done, 0, 8));
   }
   e->peer_world = world;
   e->peer_rank = rank;

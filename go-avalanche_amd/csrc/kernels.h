@@ -130,6 +130,13 @@ struct RoundParams {
   // device table, read only by lanes that push).
   uint32_t push_n;
   uint32_t* const* push_dst;
+  // Arrival folded into the round (k_round_sweep's last wave; launch_peer_wait then only waits):
+  // every wave counts itself in wave_done[arrive_seq & 1] once its stores (the pushes included) are
+  // acknowledged; the last one stores arrive_seq into slot arrive_rank of every rank's arrival array
+  // (arrive_dst[i], system scope) and resets the other counter. arrive_n = 0: no fold.
+  uint32_t* const* arrive_dst;
+  uint32_t arrive_n, arrive_rank, arrive_seq;
+  uint32_t* wave_done;
   // Deferred count planes (`kl`, k = 8, warm sim rounds in which no record can
   // finalize): a tile all of whose polled records agreed with
   // their accepted bit on all 8 votes gains exactly +8 on every polled count
@@ -156,6 +163,7 @@ struct RoundParams {
   const uint8_t* rflag_in;
   uint8_t* rflag_out;
   uint32_t rflag_off;        // byte offset of the flag bytes in every snapshot buffer (peer pushes)
+
   // fresh: the round right after av_init_records: every record is a
   // NewVoteRecord (votes = consider = 0, count 0, vote.go:33-35), so the
   // kernel reads only the A plane; the live mask of a block is its existing
@@ -247,6 +255,9 @@ hipError_t launch_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, u
 // Gives up after ~timeout_ms and sets *err (later barriers then return at once).
 hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
                                uint32_t timeout_ms, hipStream_t s);
+// The waiting half alone (the round kernel stored this rank's arrival: RoundParams::arrive_*).
+hipError_t launch_peer_wait(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
+                            uint32_t timeout_ms, hipStream_t s);
 
 struct InitParams {
   uint32_t* planes;
@@ -266,14 +277,39 @@ struct DropInParams {
   uint32_t* pref;          // current published snapshot row for the node
   const uint32_t* valid;
   const uint32_t* byz;
-  const uint32_t* blocks;  // touched lanes (local node * BL + block), each once
+  const uint32_t* blocks;  // touched lanes (local node * BL + block), each once; >= L: votes for unknown targets
   const uint32_t* offs;    // [n_blocks + 1] into entries
   const uint32_t* entries; // pairs (pos, meta = bit | yes<<5 | considered<<6)
-  int32_t* status_out;     // per vote position, -1 = no update
-  uint32_t n_blocks, n0, BL, PS, round;
+  int8_t* status_out;      // per vote position, -1 = no update
+  uint32_t n_blocks, n0, BL, PS, round, L;
   uint32_t pub_mode;
+  // av_register_votes_batch's Responses (k_dropin_resp / k_dropin_keys): packed votes (dropin_word),
+  // Response r = votes [resp_off[r], resp_off[r + 1]) of local node resp_node[r]
+  const uint32_t* packed;
+  const uint32_t* resp_off;
+  const uint32_t* resp_node;
+  uint32_t n_resp;
+  // fast path: the Responses grouped by node (order = Response indices, stable by node; group i =
+  // order[grp_off[i] .. grp_off[i + 1]))
+  const uint32_t* order;
+  const uint32_t* grp_off;
+  uint32_t n_groups;
 };
+// A drop-in vote as the host packs it: the target's local index, "unknown hash" (outside this
+// engine's targets: skipped, processor.go:95-99), err == 0 (yes) and int32(err) >= 0 (considered),
+// vote.go:55-56.
+constexpr uint32_t kDropUnknown = 1u << 29, kDropYes = 1u << 30, kDropCons = 1u << 31, kDropTl = (1u << 22) - 1u;
+__host__ __device__ inline uint32_t dropin_word(int64_t tl, bool local, uint32_t err) {
+  return (local ? (uint32_t)tl & kDropTl : kDropUnknown) | (err == 0u ? kDropYes : 0u) |
+         ((int32_t)err >= 0 ? kDropCons : 0u);
+}
 hipError_t launch_register_votes(const DropInParams& p, hipStream_t s);
+// Fast path of a batch whose Responses each have strictly ascending targets: one workgroup per node
+// (its Responses in order), the first vote of each (node, block) run applies the run.
+hipError_t launch_dropin_resp(const DropInParams& p, hipStream_t s);
+// General path: per vote, the lane key (L for unknown targets), its index and the packed vote for
+// launch_group_votes.
+hipError_t launch_dropin_keys(const DropInParams& p, uint32_t* keys, uint32_t* vidx, uint32_t* info, hipStream_t s);
 
 struct AddParams {
   uint32_t* planes;

@@ -279,6 +279,7 @@ __global__ void k_register_votes(const DropInParams p) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n_blocks) return;
   const uint32_t g = p.blocks[i];  // lane: local node * BL + block
+  if (g >= p.L) return;            // the run of votes for unknown targets: no update (status -1)
   const uint32_t nl = g / p.BL, b = g - nl * p.BL;
   const uint32_t node = p.n0 + nl;
   St s;
@@ -295,7 +296,7 @@ __global__ void k_register_votes(const DropInParams p) {
     died |= fin;
     int32_t st = -1;
     if (E & m) st = (fin & m) ? ((s.A & m) ? 3 : 0) : ((s.A & m) ? 2 : 1);
-    p.status_out[pos] = st;
+    p.status_out[pos] = (int8_t)st;
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -305,6 +306,94 @@ __global__ void k_register_votes(const DropInParams p) {
   store_state(p.planes, g, s);
   p.pref[(size_t)node * p.PS + b] =
       is_byz(p.byz, node) ? byz_pattern(p.round) : publish_word(s.A, s.K[7], p.pub_mode);
+}
+
+// av_register_votes_batch, fast path: every Response's targets strictly
+// ascending. A Response's votes for one (node, 32-target block) lane are then
+// consecutive and in order, and the run's first vote is the one whose
+// predecessor is in another block: one thread per run applies it (<= 32
+// votes) exactly as k_register_votes does, with no sort. One workgroup per
+// node (grid-stride over nodes): its Responses apply one after the other
+// (processor.go:61-122 per Response, in call order). A Response is walked in
+// chunks of kDropChunk votes: the chunk's run heads are collected in LDS, then
+// the workgroup's threads take one run each (a run may reach into the next
+// chunk; its head is in this one).
+constexpr uint32_t kDropChunk = 4096;
+
+__device__ __forceinline__ void dropin_run(const DropInParams& p, uint32_t v, uint32_t o1, uint32_t nl, uint32_t node) {
+  const uint32_t blk = (p.packed[v] & kDropTl) >> 5;
+  const uint32_t g = nl * p.BL + blk;
+  St s;
+  load_state(p.planes, g, s);
+  const uint32_t vmask = p.valid[blk];
+  uint32_t died = 0;
+  for (uint32_t u = v; u < o1; ++u) {
+    const uint32_t x = p.packed[u];
+    if ((x & kDropUnknown) || ((x & kDropTl) >> 5) != blk) break;
+    const uint32_t m = 1u << (x & 31u);
+    const uint32_t part = ~s.K[7] & vmask & m;  // skip deleted (:95-99) and invalid (:101-103)
+    uint32_t E, fin;
+    vote_step<true>(s, (x & kDropYes) ? m : 0u, (x & kDropCons) ? m : 0u, part, E, fin);
+    died |= fin;
+    int32_t st = -1;
+    if (E & m) st = (fin & m) ? ((s.A & m) ? 3 : 0) : ((s.A & m) ? 2 : 1);
+    p.status_out[u] = (int8_t)st;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    s.V[q] &= ~died;
+    s.C[q] |= died;
+  }
+  store_state(p.planes, g, s);
+  p.pref[(size_t)node * p.PS + blk] = is_byz(p.byz, node) ? byz_pattern(p.round) : publish_word(s.A, s.K[7], p.pub_mode);
+}
+
+__global__ __launch_bounds__(256) void k_dropin_resp(const DropInParams p) {
+  __shared__ uint32_t heads[kDropChunk];
+  __shared__ uint32_t nheads;
+  for (uint32_t gi = blockIdx.x; gi < p.n_groups; gi += gridDim.x) {
+    for (uint32_t k = p.grp_off[gi]; k < p.grp_off[gi + 1]; ++k) {
+      const uint32_t r = p.order[k];
+      const uint32_t o0 = p.resp_off[r], o1 = p.resp_off[r + 1];
+      const uint32_t nl = p.resp_node[r], node = p.n0 + nl;
+      for (uint32_t c0 = o0; c0 < o1; c0 += kDropChunk) {
+        const uint32_t c1 = min(o1, c0 + kDropChunk);
+        if (threadIdx.x == 0) nheads = 0u;
+        __syncthreads();
+        for (uint32_t v = c0 + threadIdx.x; v < c1; v += blockDim.x) {
+          const uint32_t w = p.packed[v];
+          if (w & kDropUnknown) continue;
+          if (v > o0) {
+            const uint32_t q = p.packed[v - 1u];
+            if (!(q & kDropUnknown) && ((q ^ w) & kDropTl) >> 5 == 0u) continue;  // inside a run
+          }
+          heads[atomicAdd(&nheads, 1u)] = v;
+        }
+        __syncthreads();
+        const uint32_t nh = nheads;
+        for (uint32_t h = threadIdx.x; h < nh; h += blockDim.x) dropin_run(p, heads[h], o1, nl, node);
+        __syncthreads();  // heads reused; the node's next Response sees this one's records
+      }
+    }
+  }
+}
+
+// General path: one workgroup per Response writes each vote's lane key (L for
+// an unknown target), its index and its packed (bit | yes << 5 | considered << 6)
+// for the stable radix grouping (log_ops.hip launch_group_votes).
+__global__ __launch_bounds__(256) void k_dropin_keys(const DropInParams p, uint32_t* keys, uint32_t* vidx,
+                                                     uint32_t* info) {
+  for (uint32_t r = blockIdx.x; r < p.n_resp; r += gridDim.x) {
+    const uint32_t o0 = p.resp_off[r], o1 = p.resp_off[r + 1];
+    const uint32_t nl = p.resp_node[r];
+    for (uint32_t v = o0 + threadIdx.x; v < o1; v += blockDim.x) {
+      const uint32_t w = p.packed[v];
+      const uint32_t tl = w & kDropTl;
+      keys[v] = (w & kDropUnknown) ? p.L : nl * p.BL + (tl >> 5);
+      vidx[v] = v;
+      info[v] = (tl & 31u) | ((w & kDropYes) ? 1u << 5 : 0u) | ((w & kDropCons) ? 1u << 6 : 0u);
+    }
+  }
 }
 
 // AddTargetToReconcile (processor.go:45-58) for a list of targets of one
@@ -752,6 +841,18 @@ hipError_t launch_register_votes(const DropInParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+hipError_t launch_dropin_resp(const DropInParams& p, hipStream_t s) {
+  if (!p.n_resp) return hipSuccess;
+  hipLaunchKernelGGL(k_dropin_resp, dim3(std::min<uint32_t>(p.n_groups, 65535u)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_dropin_keys(const DropInParams& p, uint32_t* keys, uint32_t* vidx, uint32_t* info, hipStream_t s) {
+  if (!p.n_resp) return hipSuccess;
+  hipLaunchKernelGGL(k_dropin_keys, dim3(std::min<uint32_t>(p.n_resp, 65535u)), dim3(256), 0, s, p, keys, vidx, info);
+  return hipGetLastError();
+}
+
 hipError_t launch_add_targets(const AddParams& p, hipStream_t s) {
   if (!p.n) return hipSuccess;
   hipLaunchKernelGGL(k_add_targets, dim3(1), dim3(64), 0, s, p);
@@ -803,13 +904,14 @@ __global__ __launch_bounds__(256) void k_push_rows(const uint32_t* src, PeerPtrs
 // waiting; the host refuses further rounds and results (engine.cpp
 // peer_failed, AV_ERR_PEER).
 __global__ __launch_bounds__(64) void k_peer_barrier(PeerPtrs arrive, const uint32_t* own, uint32_t world,
-                                                     uint32_t rank, uint32_t seq, uint32_t* err, uint64_t ticks) {
+                                                     uint32_t rank, uint32_t seq, uint32_t* err, uint64_t ticks,
+                                                     uint32_t store) {
   const uint32_t i = threadIdx.x;
   uint32_t* mine = arrive.p[0];  // lane i's rank-i array, selected with static indices
 #pragma unroll
   for (int r = 1; r <= kMaxPeers; ++r)
     if ((uint32_t)r == i) mine = arrive.p[r];
-  if (i < world) __hip_atomic_store(mine + rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (store && i < world) __hip_atomic_store(mine + rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   const bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
   if (i >= world || failed) return;
   const uint32_t* slot = own + i;  // own == arrive.p[rank]
@@ -887,7 +989,19 @@ hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, u
   if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
   if (e != hipSuccess) return e;
   const uint64_t ticks = (uint64_t)timeout_ms * (uint64_t)(khz > 0 ? khz : 100000);
-  hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, s, arrive, arrive.p[rank], world, rank, seq, err, ticks);
+  hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, s, arrive, arrive.p[rank], world, rank, seq, err, ticks, 1u);
+  return hipGetLastError();
+}
+
+hipError_t launch_peer_wait(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
+                            uint32_t timeout_ms, hipStream_t s) {
+  if (world > (uint32_t)kMaxPeers + 1u || rank >= world) return hipErrorInvalidValue;
+  int dev = 0, khz = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess) return e;
+  const uint64_t ticks = (uint64_t)timeout_ms * (uint64_t)(khz > 0 ? khz : 100000);
+  hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, s, arrive, arrive.p[rank], world, rank, seq, err, ticks, 0u);
   return hipGetLastError();
 }
 

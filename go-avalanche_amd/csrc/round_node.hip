@@ -241,7 +241,10 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
   const uint32_t bc = active ? b : p.BL - 1u;  // inactive lanes read a valid lane, never store
   const uint32_t g = nl * p.BL + bc;
   const uint32_t node = p.n0 + nl;
-  const bool early = b < kMaxPoll / 32u;  // wave-uniform
+  // wave-uniform; waves 0-1 always (kMaxPoll / 32 = 128 lanes): wave 0 is always heavy, which the
+  // round loop's barriers rely on
+  const bool early = b < kMaxPoll / 32u;
+  static_assert(kMaxPoll / 32u >= 64u, "wave 0 must be early (heavy)");
 
   uint32_t* const tp = p.planes + (size_t)(g >> 6) * (kPlanes * 64u);
   const uint32_t tl = g & 63u;
@@ -321,7 +324,10 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
   }
   uint32_t done = R, applied = 0u, upd = 0u, emitted = 0u, pubs = 0u;
   for (uint32_t r = 0; r < R; ++r) {
-    // a polled record with count >= 120 may finalize (and leave the poll set) this round
+    // a polled record with count >= 120 may finalize (and leave the poll set) this round.
+    // Only the heavy waves reach this barrier: the light ones ended above. CDNA's s_barrier counts
+    // the waves of the workgroup that have not ended, and wave 0 (lanes 0-63, early) is always
+    // heavy, so the workgroup's barrier is never empty (see the comment on `early`).
     if (r >= J) {
       const uint32_t nearfin = heavy ? polled & Kp[6] & Kp[5] & Kp[4] & Kp[3] : 0u;
       if (__syncthreads_or(nearfin != 0u)) {  // workgroup-uniform

@@ -369,14 +369,19 @@ __device__ __forceinline__ uint32_t emit_updates_lds(const RoundParams& p, uint3
 // rflag_out): every lane of the node published REF's word. BL divides 64, so
 // the node's lanes are the aligned BL-lane segment of this wave that holds
 // the lane; the node's block-0 lane stores the byte (and pushes it to the
-// peers' replicas when it changed, as the published words).
+// peers' replicas when it changed, as the published words). The byte is the
+// snapshot's tag (ref_tag) when the row equals the reference row, else 0; a
+// reader trusts only its own snapshot's tag, so flags are written by settled
+// tiles only and every other byte (older snapshots' tags, 0) reads as "gather".
+__device__ __forceinline__ uint8_t ref_tag(uint32_t snapshot_round) { return (uint8_t)(0x80u | (snapshot_round & 0x7Fu)); }
+
 __device__ __forceinline__ void ref_flag_store(const RoundParams& p, uint32_t lane, bool active, uint32_t b,
                                                uint32_t node, uint32_t pub, uint32_t ref) {
   const uint64_t eq = __ballot(!active || pub == ref);
   const uint32_t s0 = lane - b;  // the node's first lane (active lanes only)
   const uint64_t seg = (p.BL >= 64u ? ~0ull : ((1ull << p.BL) - 1ull)) << (s0 & 63u);
   if (active && b == 0u) {
-    const uint8_t f = (eq & seg) == seg ? 1u : 0u;
+    const uint8_t f = (eq & seg) == seg ? ref_tag(p.round + 1u) : 0u;  // pref_out = snapshot round + 1
     if (p.push_n && p.rflag_out[node] != f) {
       for (uint32_t r = 0; r < p.push_n; ++r)
         __hip_atomic_store(reinterpret_cast<uint8_t*>(p.push_dst[r]) + p.rflag_off + node, f, __ATOMIC_RELAXED,
@@ -609,7 +614,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
   }
-  if (REF && p.rflag_out) {  // reference-row flag of the row just published (kernels.h)
+  if (REF && p.rflag_out && settled) {  // reference-row flag of the row a settled tile just published
     ref_flag_store(p, lane, active, b, node, is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A,
                    p.pref_in[p.ref_node * p.PS + (active ? b : 0u)]);
     if (active) acc.lane_bytes += 4u + (b == 0u ? 1u : 0u);
@@ -701,7 +706,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
     const uint32_t rw = p.pref_prev[p.ref_node * p.PS + b];
     uint32_t fl = 1u;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fl &= p.rflag_in[rows[j] >> p.ps_shift];
+    for (int j = 0; j < 8; ++j) fl &= p.rflag_in[rows[j] >> p.ps_shift] == ref_tag(p.round) ? 1u : 0u;
     rbytes = 4u + (b == 0u ? 8u : 0u);
     if (fl) {
       dis = all = rw;
@@ -779,8 +784,12 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
   const uint32_t aoff = (1536u + lane) * 4u;
   // reference words of this lane's block: the snapshot being written is flagged against rin, the
   // flags of the snapshot being read were written against rprev
-  const uint32_t rin = REF ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
-  const uint32_t rprev = REF && p.rflag_in ? at_byte(p.pref_prev, p.ref_node * p.PS * 4u + bo) : 0u;
+  // flags are read until the first candidate tile with an unflagged peer: from there on the run
+  // gathers (a sparse flag set, e.g. the round after the first settled one, would cost the 8 flag
+  // loads on top of the gathers at every tile)
+  bool rd = REF && p.rflag_in;
+  const uint32_t rprev = rd ? at_byte(p.pref_prev, p.ref_node * p.PS * 4u + bo) : 0u;
+  const uint32_t rin = REF && p.rflag_out ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
   uint32_t done = 0u;
   uint32_t applied = 0u, bytes = 0u, reread = 0u;  // per lane
   for (uint32_t i = 0; i < ntiles; ++i) {
@@ -806,13 +815,18 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     }
     uint32_t dis = 0u, all = ~0u;
     bool gather = true;
-    if (REF && p.rflag_in) {
+    bool rdt = false;  // this tile read the flags
+    if (rd) {
       uint32_t fl = 1u;
+      const uint8_t tag = ref_tag(p.round);  // pref_in = snapshot round
 #pragma unroll
-      for (int j = 0; j < 8; ++j) fl &= p.rflag_in[rows[j] >> p.ps_shift];
-      if (fl) {
+      for (int j = 0; j < 8; ++j) fl &= p.rflag_in[rows[j] >> p.ps_shift] == tag ? 1u : 0u;
+      rdt = true;
+      if (__ballot(active && !fl) == 0ull) {
         dis = all = rprev;
         gather = false;
+      } else {
+        rd = false;
       }
     }
     if (gather) {
@@ -844,7 +858,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     // settled_tile's accounting: 40 B per active lane (+ 4 B push read), 28 of the 32 gathered re-read;
     // reference rows: the 8 flag bytes per node instead of the 32 B of votes, the flag byte written
     bytes += active ? 40u + (p.push_n ? 4u : 0u) - (gather ? 0u : 32u) +
-                          (REF && p.rflag_in ? (b == 0u ? 8u : 0u) : 0u) + (REF && p.rflag_out ? (b == 0u ? 1u : 0u) : 0u)
+                          (rdt ? (b == 0u ? 8u : 0u) : 0u) + (REF && p.rflag_out ? (b == 0u ? 1u : 0u) : 0u)
                     : 0u;
     reread += active && gather ? 28u : 0u;
   }
@@ -991,6 +1005,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     if (by) atomicAdd(&p.bytes[shard], by);
     if (rr) atomicAdd(&p.bytes[kLogShards + shard], rr);
     if (acc.updates) atomicAdd(&p.upd_count[shard], acc.updates);
+  }
+  if (p.arrive_n) {
+    // peer exchange: this rank's arrival, stored by the round's last wave once every wave's stores
+    // (its pushes into the peers' replicas: system-scope, written through) are acknowledged, so the
+    // barrier kernel behind the round only waits (one launch gap off the exchange's critical path)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t last = 0u;
+    if (lane == 0)
+      last = __hip_atomic_fetch_add(&p.wave_done[p.arrive_seq & 1u], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                     nwaves - 1u
+                 ? 1u
+                 : 0u;
+    if (__builtin_amdgcn_readfirstlane((int)last)) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+      if (lane < p.arrive_n)
+        __hip_atomic_store(p.arrive_dst[lane] + p.arrive_rank, p.arrive_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lane == 0) __hip_atomic_store(&p.wave_done[(p.arrive_seq + 1u) & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

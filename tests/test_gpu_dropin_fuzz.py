@@ -157,3 +157,58 @@ def test_register_votes_batch_device_grouping(oracle):
         eng.run_rounds(1)
         exp_u, _ = sim.run_round()
         assert np.array_equal(eng.fetch_updates(), exp_u)
+
+
+@pytest.mark.parametrize("seed,n_resp,unsorted", [(5, 200, False), (6, 290, False), (7, 250, True)],
+                         ids=["fast", "fast_many", "one_unsorted"])
+def test_register_votes_batch_fast_path(oracle, seed, n_resp, unsorted):
+    """The batch fast path (engine.cpp av_register_votes_batch: each
+    Response's targets strictly ascending — a poll set's order, rule R1 — so
+    k_dropin_resp applies each lane's run in place, one workgroup per node,
+    its Responses in call order, no grouping) == the oracle's RegisterVotes
+    per Response, and == the same engine forced onto the sort-grouped path
+    (option dropin_fast = 0). Nodes repeat across the batch. unsorted: one
+    Response out of order sends the whole batch down the general path."""
+    rng = np.random.default_rng(seed)
+    n, m = 300, 1000
+    engs = []
+    for fast in (1, 0):
+        e = avhip.Engine(n, m, k=8, seed=seed)
+        e.set_option("dropin_fast", fast)
+        e.init_records(avhip.INIT_BERNOULLI, int(0.6 * 2**32))
+        e.set_valid(11, False)
+        engs.append(e)
+    sim = oracle.Sim(n, m, 8, seed=seed, init_mode=3, init_param=int(0.6 * 2**32))
+    sim.set_valid(11, False)
+    for _ in range(15):  # counts near 120: batches finalize records
+        for e in engs:
+            e.run_rounds(1)
+        sim.run_round()
+    for e in engs:
+        e.discard_updates()
+    for batch in range(3):
+        nodes = np.concatenate([rng.permutation(n)[:n_resp // 2], rng.integers(0, n, n_resp - n_resp // 2)])
+        parts = []
+        for _ in range(n_resp):
+            k = int(rng.integers(0, 700))
+            parts.append(np.sort(rng.choice(np.arange(-3, m + 3), size=k, replace=False)))
+        if unsorted:
+            parts[n_resp // 2] = parts[n_resp // 2][::-1].copy()
+        offsets = np.concatenate([[0], np.cumsum([len(q) for q in parts])])
+        targets = np.concatenate(parts).astype(np.int64)
+        errs = rng.choice(ERRS, size=targets.size)
+        got = [e.register_votes_batch(nodes, offsets, targets, errs) for e in engs]
+        assert np.array_equal(got[0], got[1]), batch
+        for i in range(n_resp):
+            a, b = int(offsets[i]), int(offsets[i + 1])
+            exp = sim.register_votes(int(nodes[i]), targets[a:b], errs[a:b])
+            have = [(int(targets[v]), int(got[0][v])) for v in range(a, b) if got[0][v] >= 0]
+            assert have == exp, (batch, i)
+        check(engs[0], sim, f"fast batch {batch}")
+        assert np.array_equal(engs[0].read_records(), engs[1].read_records())
+    for e in engs:
+        e.run_rounds(1)
+    exp_u, _ = sim.run_round()
+    for e in engs:
+        assert np.array_equal(e.fetch_updates(), exp_u)
+        e.close()

@@ -41,10 +41,13 @@ def main():
         e.register_votes(i % n, t, rng.choice(errs_pool, votes))
     dt = (time.perf_counter() - t0) / reps
     out["single"] = {"us_per_call": dt * 1e6, "votes_per_call": votes, "votes_per_s": votes / dt}
-    for n_resp in (64, 1000, 8000):
+    # poll-set order (ascending targets: the fast path) and shuffled targets (sort-grouped path)
+    for n_resp, shuffled in ((64, False), (1000, False), (8000, False), (8000, True)):
         nodes = np.arange(n_resp, dtype=np.int64) % n
         offsets = np.arange(n_resp + 1, dtype=np.int64) * votes
         targets = np.tile(t, n_resp)
+        if shuffled:
+            targets = np.concatenate([rng.permutation(t) for _ in range(n_resp)])
         errs = rng.choice(errs_pool, targets.size)
         e.register_votes_batch(nodes, offsets, targets, errs)
         r = 5
@@ -52,7 +55,7 @@ def main():
         for _ in range(r):
             e.register_votes_batch(nodes, offsets, targets, errs)
         dt = (time.perf_counter() - t0) / r
-        out[f"batch_{n_resp}"] = {"us_per_call": dt * 1e6, "responses": n_resp, "votes_per_call": int(targets.size),
+        out[f"batch_{n_resp}" + ("_shuffled" if shuffled else "")] = {"us_per_call": dt * 1e6, "responses": n_resp, "votes_per_call": int(targets.size),
                                   "us_per_response": dt * 1e6 / n_resp, "votes_per_s": targets.size / dt}
     print(json.dumps(out, indent=1))
     if args.json:

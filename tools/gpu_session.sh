@@ -144,6 +144,7 @@ for s in "$@"; do
     probe_ref2) step probe_ref2 600 bash -c 'for w in c4 c5; do for o in "ref_rows=1" "ref_rows=0"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     reftests) step reftests 900 python -u -m pytest tests/test_gpu_ref_rows.py tests/test_gpu_virtual_votes.py tests/test_gpu_fresh.py tests/test_gpu_count_lazy.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     fullc5) step fullc5 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread -k "c5" ;;
+    dropintests) step dropintests 600 python -u -m pytest tests/test_gpu_dropin_fuzz.py tests/test_gpu_example.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
