@@ -161,6 +161,7 @@ struct av_engine {
   uint32_t* replay = nullptr;
   int64_t replay_cap_rounds = 0, replay_first = 0, replay_ready = 0;
   int replay_fuse = 16;  // option "replay_fuse": replay rounds per k_replay_node launch (capped engines; <= 1: off)
+  bool replay_fast = true;  // option "replay_fast": k_replay_fast for nodes whose poll set is their first 128 lanes
   // timing
   bool timing = false;
   bool round_marker = false;  // option "round_marker" (diagnostics)
@@ -592,6 +593,7 @@ int launch_replay_fused(av_engine* e, const uint32_t* replay0, int32_t R) {
   avk::RoundParams p = round_params(e, replay0);
   p.node_flags = e->node_flags;
   p.fuse_rounds = (uint32_t)R;
+  p.replay_fast = e->replay_fast && e->BL >= avk::kMaxPoll / 32 ? 1u : 0u;
   p.replay_stride = per;
   p.ring_next = (uint32_t)av_engine::nxt(e->cur);
   for (int i = 0; i < 3; ++i) p.pref_ring[i] = e->pref[i];
@@ -1762,6 +1764,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     }
   } else if (n == "settled_fast") {
     e->settled_fast = value != 0;
+  } else if (n == "replay_fast") {
+    e->replay_fast = value != 0;
   } else if (n == "fold_arrival") {  // 0: the separate barrier kernel stores the arrival too (A/B)
     e->fold_arrival = value != 0;
   } else if (n == "dropin_fast") {

@@ -76,6 +76,7 @@ struct RoundParams {
   // preference snapshots and the index of the one the launch's first round writes
   uint32_t fuse_rounds;
   uint32_t ring_next;
+  uint32_t replay_fast;  // k_replay_fast takes the nodes whose first 128 lanes are all live and valid
   uint64_t replay_stride;
   uint32_t* pref_ring[3];
   unsigned long long* applied;  // [kLogShards] regsiterVote applications

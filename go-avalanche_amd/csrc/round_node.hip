@@ -265,6 +265,19 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
   }
   const uint32_t P0 = ~k1[3] & vmask;  // live and IsValid (processor.go:95-103)
   const uint32_t polled = cap_select(P0, lane, wave, wsum, 0u);
+  // k_replay_fast ran this launch's rounds for nodes whose first 128 lanes hold 4096 live, valid
+  // records (the poll set is exactly those): only their other lanes' published words are left here
+  const bool fast_node = p.replay_fast && p.BL >= kMaxPoll / 32u && wsum[0][0] + wsum[0][1] == kMaxPoll;
+  if (fast_node) {  // workgroup-uniform; no barrier follows for this workgroup
+    if (!early) {   // records unchanged through the launch: publish the last three rounds
+      const uint32_t R = p.fuse_rounds, r0 = R > 3u ? R - 3u : 0u;
+      const bool byz = is_byz(p.byz, node);
+      for (uint32_t r = r0; r < R; ++r)
+        if (active) p.pref_ring[(p.ring_next + r) % 3u][node * p.PS + b] = byz ? byz_pattern(p.round + r + 1u) : A;
+      count_stats(p, blockIdx.x * (blockDim.x >> 6) + wave, lane, 0u, active, 20u + 4u + 4u * (R - r0), 0u, 0u, 0u);
+    }
+    return;
+  }
   const bool heavy = early || __ballot(polled != 0u) != 0ull;  // wave-uniform
   if (!early && heavy) {
     v0 = pld4<NT>(grp);
@@ -402,6 +415,141 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
   count_stats(p, wave_id, lane, applied, active, lane_bytes, emitted, upd, 0u);
 }
 
+// Fused replay rounds for a node whose first 128 lanes (4096 targets) hold
+// 4096 live, valid records: the poll set (processor.go:165-167) is exactly
+// those records until one of them is deleted, which only the exact pass does,
+// so the node's other lanes take no vote in the launch (k_replay_node
+// publishes their words). One 128-thread workgroup per node, lane b = block
+// b: every record of every lane is polled, so the vote and consider registers
+// shift without masks. Few waves (2 per node) and a large register budget:
+// the next round's replayed votes are loaded while this round is computed.
+// Same round loop, hand-off to the exact pass (count >= 120), StatusUpdates,
+// published words and counters as k_replay_node.
+template <int K, bool NT>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_replay_fast(const RoundParams p) {
+  __shared__ uint32_t wmax[2];
+  const uint32_t nl = blockIdx.x;
+  const uint32_t b = threadIdx.x;  // < 128 <= BL
+  const uint32_t lane = b & 63u, wave = b >> 6;
+  const uint32_t g = nl * p.BL + b;
+  const uint32_t node = p.n0 + nl;
+  uint32_t* const tp = p.planes + (size_t)(g >> 6) * (kPlanes * 64u);
+  const uint32_t tl = g & 63u;
+  u32x4* const grp = reinterpret_cast<u32x4*>(tp) + tl;
+  const u32x4 k1 = pld4<NT>(grp + 192);
+  const uint32_t vmask = p.valid[b];
+  // eligibility: every record of lanes 0..127 live and valid
+  const bool all = __syncthreads_and((~k1[3] & vmask) == ~0u) != 0;
+  if (!all) return;  // workgroup-uniform: k_replay_node runs the node
+  uint32_t A = pld<NT>(tp + 1536u + tl);
+  const u32x4 v0 = pld4<NT>(grp), v1 = pld4<NT>(grp + 64), k0 = pld4<NT>(grp + 128);
+  uint32_t V[8], C[8], Kp[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    V[i] = v0[i];
+    V[4 + i] = v1[i];
+    Kp[i] = k0[i];
+    Kp[4 + i] = k1[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
+  const uint32_t wave_id = blockIdx.x * 2u + wave;
+  const uint32_t prow = node * p.PS + b;
+  const bool byz = is_byz(p.byz, node);
+  const uint32_t R = p.fuse_rounds;
+  // largest count of the node (bit by bit from the top, as k_replay_node): no record can reach 120
+  // before round J, so those rounds need no workgroup check
+  uint32_t hi = 0u;
+  {
+    uint32_t m = ~0u;
+#pragma unroll
+    for (int q = 6; q >= 0; --q) {
+      const uint32_t t = m & Kp[q];
+      if (t) {
+        m = t;
+        hi |= 1u << q;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) hi = max(hi, (uint32_t)__shfl_xor((int)hi, o, 64));
+  if (lane == 0) wmax[wave] = hi;
+  __syncthreads();
+  const uint32_t maxc = max(wmax[0], wmax[1]);
+  const uint32_t J = maxc >= 120u ? 0u : (120u - maxc + (uint32_t)K - 1u) / (uint32_t)K;
+  uint32_t done = R, applied = 0u, upd = 0u, emitted = 0u, pubs = 0u;
+  uint32_t w[K], cw[K];
+  replay_load<K>(p.replay, g, w, cw);
+  for (uint32_t r = 0; r < R; ++r) {
+    if (r >= J) {  // a record with count >= 120 may finalize (and leave the poll set) this round
+      const uint32_t nearfin = Kp[6] & Kp[5] & Kp[4] & Kp[3];
+      if (__syncthreads_or(nearfin != 0u)) {  // workgroup-uniform
+        done = r;
+        break;
+      }
+    }
+    uint32_t nw[K], ncw[K];
+    const bool more = r + 1u < R;
+    if (more) replay_load<K>(p.replay + (size_t)(r + 1u) * p.replay_stride, g, nw, ncw);
+    uint32_t ys[7 + K], ns[7 + K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t yw = w[j] & cw[j];  // err == 0 implies considered (vote.go:55-56)
+      ys[7 + j] = yw;
+      ns[7 + j] = ~yw & cw[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      ys[i] = V[6 - i] & C[6 - i];
+      ns[i] = ~V[6 - i] & C[6 - i];
+    }
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {  // every record shifts in the K votes
+      V[i] = i < K ? ys[6 + K - i] : V[i - K];
+      C[i] = i < K ? cw[K - 1 - i] : C[i - K];
+    }
+    uint32_t E[K], alive = ~0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u, ap = 0u;
+    const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
+    round_slots<K, false>(ys, ns, low3, 0u, false, alive, A, E, c, F, ap);
+    applied += (uint32_t)K * 32u;
+    uint32_t cy = 0u;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const uint32_t ci = i < 4 ? c[i] : 0u;
+      const uint32_t t = Kp[i] ^ ci;
+      const uint32_t si = t ^ cy;
+      cy = (t & cy) | (Kp[i] & ci);
+      Kp[i] = (F & ci) | (~F & si);
+    }
+    if (r + 3u >= R) {  // the last three rounds fill the three snapshot buffers
+      p.pref_ring[(p.ring_next + r) % 3u][prow] = byz ? byz_pattern(p.round + r + 1u) : A;
+      ++pubs;
+    }
+    emitted += emit_updates_flat<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, 0u, upd, p.round_rel + r);
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        w[j] = nw[j];
+        cw[j] = ncw[j];
+      }
+    }
+  }
+  if (done < R && b == 0) p.node_flags[nl] = done + 1u;  // the exact pass takes rounds done..R-1
+  if (done > 0u) {
+    pst4<NT>(grp, u32x4{V[0], V[1], V[2], V[3]});
+    pst4<NT>(grp + 64, u32x4{V[4], V[5], V[6], V[7]});
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pst<NT>(tp + 1024u + (uint32_t)i * 64u + tl, C[i]);
+    pst4<NT>(grp + 128, u32x4{Kp[0], Kp[1], Kp[2], Kp[3]});
+    pst4<NT>(grp + 192, u32x4{Kp[4], Kp[5], Kp[6], Kp[7]});
+    pst<NT>(tp + 1536u + tl, A);
+  }
+  // bytes: 25 planes read once and written once (if a round ran), 8 B per replayed vote word pair
+  // per round, the published words
+  const uint32_t lane_bytes = kPlanes * 4u + 8u * K * done + 4u * pubs + (done > 0u ? kPlanes * 4u : 0u);
+  count_stats(p, wave_id, lane, applied, true, lane_bytes, emitted, upd, 0u);
+}
+
 template <int K, int MAXT>
 hipError_t launch_replay_t(const RoundParams& p, uint32_t bt, hipStream_t s) {
   if (p.plane_nt)
@@ -413,6 +561,14 @@ hipError_t launch_replay_t(const RoundParams& p, uint32_t bt, hipStream_t s) {
 
 template <int K>
 hipError_t launch_replay_k(const RoundParams& p, hipStream_t s) {
+  if (p.replay_fast) {  // nodes with 4096 live valid records in their first 128 lanes first
+    if (p.plane_nt)
+      hipLaunchKernelGGL((k_replay_fast<K, true>), dim3(p.NL), dim3(128), 0, s, p);
+    else
+      hipLaunchKernelGGL((k_replay_fast<K, false>), dim3(p.NL), dim3(128), 0, s, p);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   const uint32_t bt = ((p.BL + 63u) / 64u) * 64u;
   return bt <= 512u ? launch_replay_t<K, 512>(p, bt, s) : launch_replay_t<K, 1024>(p, bt, s);
 }

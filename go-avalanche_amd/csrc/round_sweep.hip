@@ -72,6 +72,9 @@ struct WaveDraw {
   const uint32_t* sd;  // the draw, parked in LDS (round_slots.h park_draw)
   unsigned long long bad;
   uint32_t nlA, t0, nn;
+  // REF: producer lane q's 4 candidates all carry pref_in's reference-row tag (bit q): a node's 8
+  // peers are flagged iff both of its producer lanes' bits are set
+  unsigned long long flagok;
   uint32_t meta;  // lane i: tile t0 + i's vstale << 8 | kpend & (kPendAllLive | 0xFF)
   bool pair, ok;
 };
@@ -765,9 +768,10 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
 //
 // REF (reference rows, kernels.h rflag_*): a tile whose 8 peers' rows are all
 // flagged equal to the reference row takes the reference word (one hoisted
-// load per run) for all 8 votes instead of gathering them; the flag bytes
-// (1 MB at C4) are L2-resident where the rows (128 MB) are not. Every settled
-// tile writes its nodes' flags for the row it published.
+// load per run) for all 8 votes instead of gathering them. The run's flags are
+// read in the prologue next to the draw (4 byte loads per producer lane, from
+// 1 MB at C4: L2-resident where the 128 MB of rows are not) and kept as one
+// ballot. Every settled tile writes its nodes' flags for the row it published.
 template <int POL, bool REF>
 __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t lane, uint32_t tile_end,
                                                 const WaveDraw& wd, SweepAcc& acc) {
@@ -783,11 +787,8 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
   const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
   const uint32_t aoff = (1536u + lane) * 4u;
   // reference words of this lane's block: the snapshot being written is flagged against rin, the
-  // flags of the snapshot being read were written against rprev
-  // flags are read until the first candidate tile with an unflagged peer: from there on the run
-  // gathers (a sparse flag set, e.g. the round after the first settled one, would cost the 8 flag
-  // loads on top of the gathers at every tile)
-  bool rd = REF && p.rflag_in;
+  // flags of the snapshot being read (prefetched for the run's nodes: wd.flagok) against rprev
+  const bool rd = REF && p.rflag_in && wd.flagok != 0ull;
   const uint32_t rprev = rd ? at_byte(p.pref_prev, p.ref_node * p.PS * 4u + bo) : 0u;
   const uint32_t rin = REF && p.rflag_out ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
   uint32_t done = 0u;
@@ -815,18 +816,12 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     }
     uint32_t dis = 0u, all = ~0u;
     bool gather = true;
-    bool rdt = false;  // this tile read the flags
     if (rd) {
-      uint32_t fl = 1u;
-      const uint8_t tag = ref_tag(p.round);  // pref_in = snapshot round
-#pragma unroll
-      for (int j = 0; j < 8; ++j) fl &= p.rflag_in[rows[j] >> p.ps_shift] == tag ? 1u : 0u;
-      rdt = true;
+      const uint32_t base = rel * 2u + (wd.pair ? 32u : 0u);  // the node's producer lanes
+      const bool fl = ((wd.flagok >> base) & 3ull) == 3ull;
       if (__ballot(active && !fl) == 0ull) {
         dis = all = rprev;
         gather = false;
-      } else {
-        rd = false;
       }
     }
     if (gather) {
@@ -858,7 +853,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     // settled_tile's accounting: 40 B per active lane (+ 4 B push read), 28 of the 32 gathered re-read;
     // reference rows: the 8 flag bytes per node instead of the 32 B of votes, the flag byte written
     bytes += active ? 40u + (p.push_n ? 4u : 0u) - (gather ? 0u : 32u) +
-                          (rdt ? (b == 0u ? 8u : 0u) : 0u) + (REF && p.rflag_out ? (b == 0u ? 1u : 0u) : 0u)
+                          (REF && p.rflag_out ? (b == 0u ? 1u : 0u) : 0u)
                     : 0u;
     reread += active && gather ? 28u : 0u;
   }
@@ -879,8 +874,16 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
 // the node's own row: timing diagnostics only, results invalid), kModeWarmPipe
 // (kModeWarm for a resident grid: the next tile's loads are issued before the
 // current tile is computed; 93 VGPRs, 5 waves per SIMD).
+// A/B build knobs (Makefile variant libraries): the warm modes' waves per SIMD and their StatusUpdate
+// emission (0: per-lane walk, emit_updates_flat; 1: staged through LDS, emit_updates_lds)
+#ifndef AVK_WARM_WPE
+#define AVK_WARM_WPE 5
+#endif
+#ifndef AVK_WARM_LE
+#define AVK_WARM_LE 0
+#endif
 template <int K, int MODE, int POL, bool REF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeReplay || MODE == kModeWarm || MODE == kModeFresh ? 6 : 7))) void k_round_sweep(const RoundParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeWarm ? AVK_WARM_WPE : MODE == kModeReplay || MODE == kModeFresh ? 6 : 7))) void k_round_sweep(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave0 = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * 4u;
@@ -907,6 +910,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     wd.pair = false;
     wd.nlA = 0u;
     wd.nn = 0u;
+    wd.flagok = 0ull;
     wd.t0 = 0u;
     wd.meta = 0u;
     wd.bad = 0ull;
@@ -938,6 +942,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           wd.bad = d.bad;
           wd.sd = s_draw[threadIdx.x >> 6];
           if (wd.ok) park_draw(d, s_draw[threadIdx.x >> 6], lane, p.PS * 4u);
+          wd.flagok = 0ull;
+          if constexpr (REF) {
+            if (wd.ok && p.rflag_in && p.klazy) {  // the run's peer flags in 4 loads (settled_run)
+              const uint8_t tag = ref_tag(p.round);
+              uint32_t ok = 1u;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) ok &= p.rflag_in[d.prod[i]] == tag ? 1u : 0u;
+              wd.flagok = __ballot(ok != 0u);
+            }
+          }
         }
       }
     }
@@ -962,7 +976,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         }
         TileIn<K, false, true> in;
         load_tile<K, false, true, POL, false, true>(p, tile, lane, in, &wd);
-        process_tile<K, false, true, POL, true, false, REF>(p, tile, lane, in, 0u, acc, es);
+        process_tile<K, false, true, POL, true, AVK_WARM_LE != 0, REF>(p, tile, lane, in, 0u, acc, es);
       } else if constexpr (MODE == kModeFresh) {
         TileIn<K, false, false> in;
         load_tile<K, false, false, POL, false, true, true>(p, tile, lane, in);

@@ -16,6 +16,20 @@ BYZ20 = int(0.2 * 2**32)
 P80 = int(0.8 * 2**32)
 
 
+@pytest.fixture(params=[1, 0], ids=["fast", "nofast"], autouse=True)
+def replay_fast(request, monkeypatch):
+    """Every test runs with k_replay_fast (nodes whose poll set is their first
+    128 lanes, round_node.hip) on and off (option replay_fast)."""
+    orig = avhip.Engine.__init__
+
+    def init(self, *a, **kw):
+        orig(self, *a, **kw)
+        self.set_option("replay_fast", request.param)
+
+    monkeypatch.setattr(avhip.Engine, "__init__", init)
+    return request.param
+
+
 def rows(u):
     return [tuple(int(v) for v in r) for r in np.asarray(u).tolist()]
 

@@ -36,9 +36,9 @@ import os
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROUND_KERNELS = ("k_round_sweep", "k_round_node", "k_replay_node", "k_round_fast", "k_round_capped", "k_peer_table")
-# launched before the round kernel of the same round (counted with the next primary dispatch)
-PRE = ("k_peer_table",)
+ROUND_KERNELS = ("k_round_sweep", "k_round_node", "k_replay_node", "k_round_fast", "k_round_capped", "k_replay_fast")
+# launched before the round kernel of the same launch (counted with the next primary dispatch)
+PRE = ("k_replay_fast",)
 # the kernel a launch of the bench's roofline pass is counted by (k_round_capped also runs as the
 # exact pass behind k_round_node / k_replay_node)
 PRIMARY = ("k_round_sweep", "k_round_node", "k_replay_node", "k_round_fast")
