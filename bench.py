@@ -453,12 +453,14 @@ def load_pmc(wl, window, world):
 
 
 # round kinds of a fresh sim network at k = 8 (engine: launch_one_round): round 0 reads only A
-# (fresh), rounds 1-3 carry the convergence storm, 4-14 may defer count planes (klazy; a tile that
-# stays unanimous takes the settled path), 15 applies the deferred steps (kconsume)
+# (fresh), rounds 1-3 carry the convergence storm, 4-15 may defer count planes (klazy; a tile that
+# stays unanimous takes the settled path: no count can reach 120 before round 16, the first 6 votes
+# of a fresh record never step it), 16 applies the deferred steps (kconsume, outside the all-live
+# epoch)
 def round_kind(r, replay):
     if replay:
         return "replay (fused rounds per launch)"
-    return "fresh" if r == 0 else "storm" if r <= 3 else "klazy" if r <= 14 else "kconsume"
+    return "fresh" if r == 0 else "storm" if r <= 3 else "klazy" if r <= 15 else "kconsume"
 
 
 def binding(fr):

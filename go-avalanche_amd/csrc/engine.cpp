@@ -80,6 +80,11 @@ struct av_engine {
   int64_t ref_node = -1;  // first honest node (chosen at the first round that can use it); -2: none
   size_t rflag_off = 0;   // byte offset of the flags in a snapshot buffer
   bool rflag_ok[3] = {false, false, false};
+  // option "uniform_rows" (default on; kernels.h uni_*): every snapshot buffer carries one mismatch
+  // slot per rank at word uni_off; uni_ok[b]: buffer b was written by a sweep round that tagged them
+  bool uni_rows = true;
+  size_t uni_off = 0;
+  bool uni_ok[3] = {false, false, false};
 
   int cur = 0;
   static int nxt(int c) { return c == 2 ? 0 : c + 1; }
@@ -101,6 +106,9 @@ struct av_engine {
   uint32_t* log_count = nullptr;
   uint64_t* dlog = nullptr;          // dense lane records (kernels.h dense_words(k) u64 each)
   uint32_t* dlog_count = nullptr;
+  uint64_t* mlog = nullptr;          // medium lane records (kernels.h kMedMax: 2 u64 each)
+  uint32_t* mlog_count = nullptr;
+  uint32_t mlog_cap = 0;
   uint32_t* upd_count = nullptr;     // StatusUpdates emitted per shard (singles + dense bits)
   uint32_t dlog_cap = 0;
   uint32_t* log_overflow = nullptr;
@@ -196,6 +204,7 @@ struct av_engine {
   // responder variant (option "responder", kernels.h pub_mode) and the nodes
   // that no longer poll (av_set_polling); both run the first-generation kernel
   uint32_t dense_min = 0;  // option "dense_min" (kernels.h dense records; default dense_min(k))
+  bool emit_med = true;    // option "emit_med": medium records in the k = 8 sweep rounds (kernels.h kMedMax)
   int32_t pub_mode = 0;
   uint32_t* readd = nullptr;     // [L] pub_mode 2: re-add marks
   uint32_t* died_out = nullptr;  // [L] pub_mode 2: records deleted this round
@@ -256,7 +265,10 @@ struct Scratch {
 // Anything but a reference-row sweep round that writes a snapshot buffer
 // (drop-in votes, adds, writes, init, validity/publish-rule refreshes, peer
 // and RCCL set-up, other round kernels) leaves its flags stale.
-void ref_invalidate(av_engine* e) { e->rflag_ok[0] = e->rflag_ok[1] = e->rflag_ok[2] = false; }
+void ref_invalidate(av_engine* e) {
+  e->rflag_ok[0] = e->rflag_ok[1] = e->rflag_ok[2] = false;
+  e->uni_ok[0] = e->uni_ok[1] = e->uni_ok[2] = false;
+}
 
 avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   avk::RoundParams p{};
@@ -274,6 +286,10 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.dlog_count = e->dlog_count;
   p.upd_count = e->upd_count;
   p.dlog_cap = e->dlog_cap;
+  p.mlog = e->mlog;
+  p.mlog_count = e->mlog_count;
+  p.mlog_cap = e->mlog_cap;
+  p.med = e->emit_med ? 1u : 0u;
   p.log_overflow = e->log_overflow;
   p.applied = e->applied;
   p.bytes = e->bytes;
@@ -520,6 +536,24 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     p.rflag_out = reinterpret_cast<uint8_t*>(e->pref[nb]) + e->rflag_off;
     p.rflag_in = e->rflag_ok[e->cur] ? reinterpret_cast<const uint8_t*>(e->pref[e->cur]) + e->rflag_off : nullptr;
   }
+  // uniform rows: sweep rounds at k = 8 tag the snapshot they write; a round whose input snapshot
+  // is known uniform tests settled tiles with no peer draw and no gather (kernels.h uni_*)
+  // (a node-sharded engine sees every row only through the peer exchange, whose pushes carry the slots)
+  bool uni = e->uni_rows && sweep && e->k == 8 && !replay && !e->comm && !e->ablate_gather &&
+             (e->NL == (uint32_t)e->N || e->peer_world > 1);
+  if (uni) {
+    int rc = ref_pick(e);
+    if (rc != AV_OK) return rc;
+    uni = e->ref_node >= 0;
+  }
+  if (uni) {
+    p.ref_node = (uint32_t)e->ref_node;
+    p.uni_off = (uint32_t)e->uni_off;
+    p.uni_world = (uint32_t)std::max(1, e->peer_world);
+    p.uni_rank = (uint32_t)std::max(0, e->peer_rank);
+    p.uni_out = e->pref[nb] + e->uni_off;
+    p.uni_in = e->uni_ok[e->cur] ? e->pref[e->cur] + e->uni_off : nullptr;
+  }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (e->timing) {
     AV_HIP(hipEventCreate(&ev0));
@@ -543,6 +577,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   e->count_bound = std::min(127, e->count_bound + e->k);
   e->fresh = false;
   e->rflag_ok[nb] = refr && refw;
+  e->uni_ok[nb] = uni;
   if (replay)
     e->warm_all = false;
   else if (e->c_monotone && e->k >= 8 && !e->capped && all_valid)
@@ -706,7 +741,7 @@ int av_destroy(av_engine* e) {
   if (e->marker) (void)hipEventDestroy(e->marker);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->kpend, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->readd, e->died_out, e->nopoll,
-                  e->dlog, e->dlog_count, e->upd_count,
+                  e->dlog, e->dlog_count, e->upd_count, e->mlog, e->mlog_count,
                   e->applied, e->bytes, e->finalized, e->scratch_count, e->replay};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -779,7 +814,9 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->planes, plane_words)) != hipSuccess) return hip_fail(he, "alloc planes");
   // whole 2-MiB units: each snapshot buffer is an allocation of its own (IPC export, av_peer_handles)
   e->rflag_off = (pref_words * 4 + 255) / 256 * 256;
-  const size_t pref_alloc = ((e->rflag_off + (size_t)e->N + (2u << 20) - 1) / (2u << 20)) * (2u << 20) / 4;
+  e->uni_off = (e->rflag_off + (size_t)e->N + 255) / 256 * 256 / 4;  // uniform-rows slots (kernels.h)
+  const size_t pref_alloc =
+      ((e->uni_off * 4 + (avk::kMaxPeers + 1) * 4 + (2u << 20) - 1) / (2u << 20)) * (2u << 20) / 4;
   e->pref_alloc_words = pref_alloc;
   if ((he = dev_alloc(&e->pref[0], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
   if ((he = dev_alloc(&e->pref[1], pref_alloc)) != hipSuccess) return hip_fail(he, "alloc pref");
@@ -800,6 +837,11 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->dlog, (size_t)e->dlog_cap * e->log_shards * dw)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->dlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->upd_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  // a medium record holds >= 2 updates: log_cap / 2 records per shard
+  e->mlog_cap = std::max<uint32_t>(e->log_cap / 2, 16);
+  if ((he = dev_alloc(&e->mlog, (size_t)e->mlog_cap * e->log_shards * 2)) != hipSuccess) return hip_fail(he, "alloc log");
+  if ((he = dev_alloc(&e->mlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  (void)hipMemsetAsync(e->mlog_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->dlog_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->upd_count, 0, avk::kLogShards * 4, e->stream);
   if ((he = dev_alloc(&e->log_overflow, 1)) != hipSuccess) return hip_fail(he, "alloc log");
@@ -849,7 +891,10 @@ int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
   if (e) ref_invalidate(e);
   AV_ENTER(e);
   e->warm_all = false;
-  e->count_bound = 0;  // every record starts at count 0 (NewVoteRecord, vote.go:33-35)
+  // every record starts at count 0 with no considered vote (NewVoteRecord, vote.go:33-35), and a
+  // count step needs > 6 considered votes in the 8-vote window (vote.go:58-61): the first 6 votes
+  // of a fresh record cannot step it, so after v votes every count is <= v - 6
+  e->count_bound = -6;
   if (e->v_stale) {  // every plane is rewritten
     AV_HIP(hipMemsetAsync(e->vstale, 0, (size_t)(e->Lpad / 64) * 4, e->stream));
     e->v_stale = false;
@@ -1457,6 +1502,7 @@ int av_log_base_round(av_engine* e, int64_t* out) {
 int clear_log(av_engine* e) {
   AV_HIP(hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream));
   AV_HIP(hipMemsetAsync(e->dlog_count, 0, avk::kLogShards * 4, e->stream));
+  AV_HIP(hipMemsetAsync(e->mlog_count, 0, avk::kLogShards * 4, e->stream));
   AV_HIP(hipMemsetAsync(e->upd_count, 0, avk::kLogShards * 4, e->stream));
   AV_HIP(hipMemsetAsync(e->log_overflow, 0, 4, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
@@ -1489,24 +1535,29 @@ int av_update_log_overflowed(av_engine* e, int32_t* out) {
 
 // Pending log state: per-shard counters copied to the host.
 struct LogCounts {
-  std::vector<uint32_t> singles, dense, upd;
+  std::vector<uint32_t> singles, dense, med, upd;
   uint32_t ovf = 0;
-  int64_t total = 0, n_singles = 0, n_records = 0;
-  std::vector<uint64_t> soff, doff;
+  int64_t total = 0, n_singles = 0, n_records = 0, n_med = 0;
+  std::vector<uint64_t> soff, doff, moff;
 };
 
 int read_log_counts(av_engine* e, LogCounts& c) {
   c.singles.assign(avk::kLogShards, 0);
   c.dense.assign(avk::kLogShards, 0);
   c.upd.assign(avk::kLogShards, 0);
+  c.med.assign(avk::kLogShards, 0);
   AV_HIP(hipMemcpyAsync(c.singles.data(), e->log_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipMemcpyAsync(c.dense.data(), e->dlog_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpyAsync(c.med.data(), e->mlog_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipMemcpyAsync(c.upd.data(), e->upd_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipMemcpyAsync(&c.ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
   c.soff.assign(avk::kLogShards, 0);
   c.doff.assign(avk::kLogShards, 0);
+  c.moff.assign(avk::kLogShards, 0);
   for (uint32_t i = 0; i < avk::kLogShards; ++i) {
+    c.moff[i] = (uint64_t)c.n_med;
+    c.n_med += std::min<uint32_t>(c.med[i], e->mlog_cap);
     c.total += c.upd[i];
     c.soff[i] = (uint64_t)c.n_singles;
     c.n_singles += std::min<uint32_t>(c.singles[i], e->log_cap);
@@ -1523,7 +1574,7 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
   LogCounts c;
   int rc = read_log_counts(e, c);
   if (rc != AV_OK) return rc;
-  const int64_t total = c.total, singles = c.n_singles, records = c.n_records;
+  const int64_t total = c.total, singles = c.n_singles, records = c.n_records, meds = c.n_med;
   *n_out = total;
   if (c.ovf) {
     rc = clear_log(e);
@@ -1533,11 +1584,13 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
   }
   AV_CHECK(total <= cap, AV_ERR_OVERFLOW, "cap too small: %lld updates pending", (long long)total);
   if (total > 0) {
-    // device: singles and expanded dense records side by side, radix-sorted
-    // into the canonical (round, node, slot, target) order, then one copy out
+    // device: singles and expanded medium and dense records side by side,
+    // radix-sorted into the canonical (round, node, slot, target) order, then
+    // one copy out
     const uint32_t K = (uint32_t)e->k, dw = avk::dense_words(K);
+    const int64_t nrec = std::max(records, meds);
     size_t scan_bytes = 0, sort_bytes = 0;
-    AV_HIP(avk::launch_dense_expand(nullptr, (uint64_t)records, K, nullptr, nullptr, nullptr, &scan_bytes, nullptr,
+    AV_HIP(avk::launch_dense_expand(nullptr, (uint64_t)nrec, K, nullptr, nullptr, nullptr, &scan_bytes, nullptr,
                                     e->stream));
     // sort on the key bits that vary: [2, 52 + width of the largest round_rel)
     // (status bits need no ordering: (round, node, slot, target) is unique)
@@ -1547,8 +1600,8 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
     AV_HIP(avk::launch_sort_updates(nullptr, &sort_bytes, nullptr, nullptr, (uint64_t)total, 2, end_bit, e->stream));
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t b_words = up((size_t)total * 8), b_rec = up((size_t)records * dw * 8),
-                 b_cnt = up((size_t)records * 8 + 8), b_off = up(2 * avk::kLogShards * 8);
-    const size_t bytes = 2 * b_words + b_rec + 2 * b_cnt + b_off + up(scan_bytes) + up(sort_bytes);
+                 b_med = up((size_t)meds * 16), b_cnt = up((size_t)nrec * 8 + 8), b_off = up(3 * avk::kLogShards * 8);
+    const size_t bytes = 2 * b_words + b_rec + b_med + 2 * b_cnt + b_off + up(scan_bytes) + up(sort_bytes);
     void* base = nullptr;
     rc = engine_scratch(e, bytes, &base);
     if (rc != AV_OK) return rc;
@@ -1559,35 +1612,51 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
     q += b_words;
     auto* recs = reinterpret_cast<uint64_t*>(q);
     q += b_rec;
+    auto* mrecs = reinterpret_cast<uint64_t*>(q);
+    q += b_med;
     auto* cnt = reinterpret_cast<uint64_t*>(q);
     q += b_cnt;
     auto* offs = reinterpret_cast<uint64_t*>(q);
     q += b_cnt;
     auto* soff = reinterpret_cast<uint64_t*>(q);
     auto* doff = soff + avk::kLogShards;
+    auto* moff = doff + avk::kLogShards;
     q += b_off;
     void* scan_tmp = q;
     q += up(scan_bytes);
     void* sort_tmp = q;
     AV_HIP(hipMemcpyAsync(soff, c.soff.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
     AV_HIP(hipMemcpyAsync(doff, c.doff.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
+    AV_HIP(hipMemcpyAsync(moff, c.moff.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
     AV_HIP(avk::launch_compact_log(e->log, e->log_count, soff, e->log_cap, e->log_shards, 1, words, e->stream));
+    // expand one record kind (dense: k, medium: kMedKind) at words + at; returns the updates it held
+    auto expand = [&](const uint64_t* src, int64_t n, uint32_t kind, int64_t at, int64_t* got) -> int {
+      *got = 0;
+      if (!n) return AV_OK;
+      size_t sb = scan_bytes;
+      AV_HIP(avk::launch_dense_expand(src, (uint64_t)n, kind, cnt, offs, scan_tmp, &sb, words + at, e->stream));
+      uint64_t last[2] = {0, 0};
+      AV_HIP(hipMemcpyAsync(&last[0], offs + n - 1, 8, hipMemcpyDeviceToHost, e->stream));
+      AV_HIP(hipMemcpyAsync(&last[1], cnt + n - 1, 8, hipMemcpyDeviceToHost, e->stream));
+      AV_HIP(hipStreamSynchronize(e->stream));
+      *got = (int64_t)(last[0] + last[1]);
+      return AV_OK;
+    };
+    int64_t n_med = 0, n_dense = 0;
+    if (meds) {
+      AV_HIP(avk::launch_compact_log(e->mlog, e->mlog_count, moff, e->mlog_cap, e->log_shards, 2, mrecs, e->stream));
+      rc = expand(mrecs, meds, avk::kMedKind, singles, &n_med);
+      if (rc != AV_OK) return rc;
+      AV_CHECK(singles + n_med <= total, AV_ERR_HIP, "StatusUpdate log inconsistent (medium records)");
+    }
     if (records) {
       AV_HIP(avk::launch_compact_log(e->dlog, e->dlog_count, doff, e->dlog_cap, e->log_shards, dw, recs, e->stream));
-      AV_HIP(avk::launch_dense_expand(recs, (uint64_t)records, K, cnt, offs, scan_tmp, &scan_bytes, words + singles,
-                                      e->stream));
-      // the expansion must produce exactly the counted updates
-      uint64_t last[2] = {0, 0};
-      AV_HIP(hipMemcpyAsync(&last[0], offs + records - 1, 8, hipMemcpyDeviceToHost, e->stream));
-      AV_HIP(hipMemcpyAsync(&last[1], cnt + records - 1, 8, hipMemcpyDeviceToHost, e->stream));
-      AV_HIP(hipStreamSynchronize(e->stream));
-      AV_CHECK((int64_t)(singles + last[0] + last[1]) == total, AV_ERR_HIP,
-               "StatusUpdate log inconsistent (%lld of %lld)", (long long)(singles + last[0] + last[1]),
-               (long long)total);
-    } else {
-      AV_CHECK(singles == total, AV_ERR_HIP, "StatusUpdate log inconsistent (%lld of %lld)", (long long)singles,
-               (long long)total);
+      rc = expand(recs, records, K, singles + n_med, &n_dense);
+      if (rc != AV_OK) return rc;
     }
+    // the expansion must produce exactly the counted updates
+    AV_CHECK(singles + n_med + n_dense == total, AV_ERR_HIP, "StatusUpdate log inconsistent (%lld of %lld)",
+             (long long)(singles + n_med + n_dense), (long long)total);
     AV_HIP(avk::launch_sort_updates(sort_tmp, &sort_bytes, words, sorted, (uint64_t)total, 2, end_bit, e->stream));
     AV_HIP(hipMemcpyAsync(out, sorted, (size_t)total * 8, hipMemcpyDeviceToHost, e->stream));
     AV_HIP(hipStreamSynchronize(e->stream));
@@ -1604,8 +1673,8 @@ int av_updates_digest_range(av_engine* e, int64_t n0, int64_t n1, uint64_t out[3
   uint32_t ovf = 0;
   AV_HIP(hipMemcpyAsync(&ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
   if (!e->digest) AV_HIP(dev_alloc(&e->digest, 3));
-  AV_HIP(avk::launch_log_digest(e->log, e->log_count, e->log_cap, e->dlog, e->dlog_count, e->dlog_cap,
-                                e->log_shards, (uint32_t)e->k, (uint32_t)n0, (uint32_t)n1, e->digest, e->stream));
+  AV_HIP(avk::launch_log_digest(e->log, e->log_count, e->log_cap, e->dlog, e->dlog_count, e->dlog_cap, e->mlog,
+                                e->mlog_count, e->mlog_cap, e->log_shards, (uint32_t)e->k, (uint32_t)n0, (uint32_t)n1, e->digest, e->stream));
   unsigned long long d[3] = {0, 0, 0};
   AV_HIP(hipMemcpyAsync(d, e->digest, sizeof(d), hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
@@ -1737,6 +1806,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->plane_nt = value != 0;
   } else if (n == "ablate_emit") {
     e->ablate_emit = (int)std::max<int64_t>(0, std::min<int64_t>(2, value));
+  } else if (n == "uniform_rows") {  // A/B: uniform-row settled tests (kernels.h uni_*)
+    e->uni_rows = value != 0;
+    ref_invalidate(e);
   } else if (n == "ref_rows") {  // reference-row flags in converged sweep rounds (kernels.h)
     e->ref_rows = value != 0;
   } else if (n == "replay_fuse") {  // replay rounds per fused launch on capped engines (<= 1: one launch per round)
@@ -1813,6 +1885,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     rc = refresh_pref(e);  // republish the current snapshot under the new rule
     if (rc != AV_OK) return rc;
     AV_HIP(hipStreamSynchronize(e->stream));
+  } else if (n == "emit_med") {  // A/B: medium lane records (kernels.h kMedMax) in the k = 8 sweep rounds
+    e->emit_med = value != 0;
   } else if (n == "dense_min") {  // tuning (A/B): fewer updates per dense record; the dense log may fill sooner
     AV_CHECK(value >= 1 && value <= 32 * (int64_t)e->k + 1, AV_ERR_INVALID_ARG, "bad dense_min");
     e->dense_min = (uint32_t)value;

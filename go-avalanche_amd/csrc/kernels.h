@@ -63,7 +63,9 @@ struct RoundParams {
   uint32_t* log_count;       // [kLogShards] singles reserved per shard
   uint64_t* dlog;            // [kLogShards][dlog_cap][dense_words(k)] dense lane records
   uint32_t* dlog_count;      // [kLogShards] dense records reserved per shard
-  uint32_t* upd_count;       // [kLogShards] StatusUpdates emitted (singles + dense bits)
+  uint32_t* upd_count;       // [kLogShards] StatusUpdates emitted (singles + medium + dense)
+  uint64_t* mlog;            // [kLogShards][mlog_cap][2] medium lane records (med_field)
+  uint32_t* mlog_count;      // [kLogShards] medium records reserved per shard
   uint32_t* log_overflow;    // [1]
   uint32_t* node_flags;      // [NL] capped path: nodes left to the exact pass (nullptr: none)
   // exact pass (k_round_capped behind k_round_node / k_replay_node): node_flags[nl] = 1 + the first
@@ -86,6 +88,7 @@ struct RoundParams {
   uint64_t seed;
   uint32_t log_cap;          // entries per shard
   uint32_t dlog_cap;         // dense records per shard
+  uint32_t mlog_cap;         // medium records per shard
   uint32_t log_shards;       // shards in use (<= kLogShards; min(waves, kLogShards))
   uint32_t n_nodes;          // N (global)
   uint32_t n0;               // first local node (global id)
@@ -165,6 +168,18 @@ struct RoundParams {
   uint8_t* rflag_out;
   uint32_t rflag_off;        // byte offset of the flag bytes in every snapshot buffer (peer pushes)
 
+  // Uniform rows (k_round_sweep, k = 8). Every snapshot buffer holds, uni_off words
+  // in, one mismatch slot per rank. A wave that publishes into pref_out a word differing from
+  // ref_node's word in pref_in stores the tag p.round + 1 into its rank's slot of pref_out (and of
+  // every peer replica): uni_out = pref_out + uni_off. uni_in = pref_in + uni_off (nullptr: pref_in
+  // was not written by such a round): if none of its uni_world slots holds p.round, every row of
+  // pref_in equals ref_node's row of pref_prev, so every gathered vote word is that row's word and a
+  // settled-candidate tile is tested with no peer draw and no gather (settled_run_uni). A stale slot
+  // can only read as a mismatch (tags are unique per round), never hide one.
+  uint32_t* uni_out;
+  const uint32_t* uni_in;
+  uint32_t uni_world, uni_rank, uni_off;
+
   // fresh: the round right after av_init_records: every record is a
   // NewVoteRecord (votes = consider = 0, count 0, vote.go:33-35), so the
   // kernel reads only the A plane; the live mask of a block is its existing
@@ -189,6 +204,10 @@ struct RoundParams {
   uint32_t* died_out;
   const uint32_t* nopoll;
   uint32_t dense_min;  // a lane with >= dense_min updates logs one dense record (default dense_min(k))
+  // medium lane records (k_round_sweep, k = 8; emit_updates_med): a lane with 2..kMedMax updates
+  // logs one 16-B record instead of 8 B per update, a lane with more a dense record; every lane
+  // then stores at most one entry, at its rank among the wave's lanes of that kind
+  uint32_t med;
 };
 constexpr uint32_t kPendAllLive = 0x80000000u;
 constexpr uint32_t kVStale = 1u, kVUniform = 2u, kVMask = 3u, kCAll = 4u;
@@ -211,6 +230,19 @@ inline void bl_divider(uint32_t d, uint32_t& magic, uint32_t& sh1, uint32_t& sh2
 // is at most that of the singles: 8 * count >= 8 * dense_words(k).
 __host__ __device__ constexpr uint32_t dense_words(uint32_t k) { return (k + 5u) / 2u; }  // u64 words
 __host__ __device__ constexpr uint32_t dense_min(uint32_t k) { return dense_words(k); }   // updates
+
+// A lane with 2..kMedMax StatusUpdates in one round (k <= 8) logs one medium
+// record of two u64: the key (pack_update with the block's first target, slot
+// 0, status 0) and a payload: bits [3:0] = n updates, then n 10-bit fields at
+// bit 4 + 10 i, each (slot << 7 | bit << 2 | status) = the update's offset
+// from the key (expanded word = key + (slot << 24) + (bit << 2) + status).
+constexpr uint32_t kMedMax = 6;
+__host__ __device__ constexpr uint32_t med_field(uint32_t slot, uint32_t bit, uint32_t status) {
+  return (slot << 7) | (bit << 2) | status;
+}
+__host__ __device__ inline uint64_t med_word(uint64_t key, uint32_t f) {
+  return key + ((uint64_t)(f >> 7) << 24) + ((uint64_t)((f >> 2) & 31u) << 2) + (f & 3u);
+}
 
 // Update-log entry (one StatusUpdate, avalanche.go:59-62):
 //   [63:52] round - log_base | [51:28] node | [27:24] slot | [23:2] target | [1:0] status
@@ -337,12 +369,16 @@ hipError_t launch_read_records_virtual(const RoundParams& p, uint32_t nl0, uint3
 // Digest {count, sum, xor} of splitmix64(packed word) over every pending update
 // of nodes [node0, node1).
 hipError_t launch_log_digest(const uint64_t* log, const uint32_t* counts, uint32_t cap, const uint64_t* dlog,
-                             const uint32_t* dcounts, uint32_t dcap, uint32_t shards, uint32_t k, uint32_t node0,
-                             uint32_t node1, unsigned long long* out, hipStream_t s);
+                             const uint32_t* dcounts, uint32_t dcap, const uint64_t* mlog, const uint32_t* mcounts,
+                             uint32_t mcap, uint32_t shards, uint32_t k, uint32_t node0, uint32_t node1,
+                             unsigned long long* out, hipStream_t s);
 // Expand n compacted dense records into packed words at out (scratch: n u64
 // counts + n u64 offsets; temp == nullptr: *temp_bytes = the scan's scratch size).
 hipError_t launch_dense_expand(const uint64_t* recs, uint64_t n, uint32_t k, uint64_t* counts_scratch,
                                uint64_t* offsets, void* temp, size_t* temp_bytes, uint64_t* out, hipStream_t s);
+// The same for n compacted medium records (k = 0 selects the medium form in launch_dense_expand's
+// kernels: 2 u64 per record, n updates in the payload's low 4 bits).
+constexpr uint32_t kMedKind = 0u;
 // Radix sort of packed update words on bits [begin_bit, end_bit) (temp ==
 // nullptr: size query).
 hipError_t launch_sort_updates(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,

@@ -60,6 +60,25 @@ __device__ __forceinline__ void for_each_dense(const uint32_t* w, uint32_t K, F&
   }
 }
 
+// Medium record (kernels.h kMedMax): w = {key, payload}.
+template <typename F>
+__device__ __forceinline__ void for_each_med(const uint64_t* w, F&& f) {
+  const uint64_t key = w[0], pl = w[1];
+  const uint32_t n = (uint32_t)(pl & 15u);
+  for (uint32_t i = 0; i < n && i < kMedMax; ++i) f(med_word(key, (uint32_t)(pl >> (4u + 10u * i)) & 1023u));
+}
+
+// u64 words of one record: dense (k >= 1) or medium (kMedKind)
+__host__ __device__ constexpr uint32_t rec_words(uint32_t K) { return K == kMedKind ? 2u : dense_words(K); }
+
+template <typename F>
+__device__ __forceinline__ void for_each_rec(const uint64_t* rec, uint32_t K, F&& f) {
+  if (K == kMedKind)
+    for_each_med(rec, f);
+  else
+    for_each_dense(reinterpret_cast<const uint32_t*>(rec), K, f);
+}
+
 __device__ __forceinline__ bool in_nodes(uint64_t w, uint32_t node0, uint32_t node1) {
   const uint32_t node = (uint32_t)(w >> 28) & 0xFFFFFFu;
   return node >= node0 && node < node1;
@@ -69,6 +88,7 @@ __device__ __forceinline__ bool in_nodes(uint64_t w, uint32_t node0, uint32_t no
 // the x-blocks stride over the shard's singles, then over its dense records.
 __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const uint32_t* counts, uint32_t cap,
                                                     const uint64_t* dlog, const uint32_t* dcounts, uint32_t dcap,
+                                                    const uint64_t* mlog, const uint32_t* mcounts, uint32_t mcap,
                                                     uint32_t K, uint32_t node0, uint32_t node1,
                                                     unsigned long long* out) {
   const uint32_t shard = blockIdx.y;
@@ -98,6 +118,17 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
       ++c;
     });
   }
+  const uint32_t nm = mlog ? min(mcounts[shard], mcap) : 0u;
+  const uint64_t* msrc = mlog + (size_t)shard * mcap * 2u;
+  for (uint32_t i = t; i < nm; i += stride) {
+    if (!in_nodes(msrc[2u * i], node0, node1)) continue;
+    for_each_med(msrc + 2u * i, [&](uint64_t wd) {
+      const uint64_t h = mix64(wd);
+      s += h;
+      x ^= h;
+      ++c;
+    });
+  }
   c = wave_add64(c);
   s = wave_add64(s);
   x = wave_xor64(x);
@@ -108,10 +139,14 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
   }
 }
 
-// Updates held by each dense record (popcount of its E_j).
+// Updates held by each dense record (popcount of its E_j) or medium record (its n).
 __global__ __launch_bounds__(256) void k_dense_counts(const uint64_t* recs, uint64_t n, uint32_t K, uint64_t* cnt) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (K == kMedKind) {
+    cnt[i] = min((uint32_t)(recs[2u * i + 1u] & 15u), kMedMax);
+    return;
+  }
   const uint32_t* w = reinterpret_cast<const uint32_t*>(recs + i * dense_words(K));
   uint32_t c = 0;
   for (uint32_t j = 0; j < K; ++j) c += (uint32_t)__popc(w[2 + j]);
@@ -124,18 +159,19 @@ __global__ __launch_bounds__(256) void k_dense_expand(const uint64_t* recs, uint
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint64_t* dst = out + off[i];
-  for_each_dense(reinterpret_cast<const uint32_t*>(recs + i * dense_words(K)), K, [&](uint64_t wd) { *dst++ = wd; });
+  for_each_rec(recs + i * rec_words(K), K, [&](uint64_t wd) { *dst++ = wd; });
 }
 
 }  // namespace
 
 hipError_t launch_log_digest(const uint64_t* log, const uint32_t* counts, uint32_t cap, const uint64_t* dlog,
-                             const uint32_t* dcounts, uint32_t dcap, uint32_t shards, uint32_t k, uint32_t node0,
-                             uint32_t node1, unsigned long long* out, hipStream_t s) {
+                             const uint32_t* dcounts, uint32_t dcap, const uint64_t* mlog, const uint32_t* mcounts,
+                             uint32_t mcap, uint32_t shards, uint32_t k, uint32_t node0, uint32_t node1,
+                             unsigned long long* out, hipStream_t s) {
   hipError_t e = hipMemsetAsync(out, 0, 3 * sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_log_digest, dim3(16, shards), dim3(256), 0, s, log, counts, cap, dlog, dcounts, dcap, k, node0,
-                     node1, out);
+  hipLaunchKernelGGL(k_log_digest, dim3(16, shards), dim3(256), 0, s, log, counts, cap, dlog, dcounts, dcap, mlog,
+                     mcounts, mcap, k, node0, node1, out);
   return hipGetLastError();
 }
 

@@ -527,6 +527,116 @@ __device__ __forceinline__ uint32_t emit_updates_flat(const RoundParams& p, uint
   return 8u * st_s + 8u * DW * st_d;
 }
 
+// StatusUpdate emission with medium records (p.med, k <= 8): every lane with
+// updates stores exactly one entry — a single packed word (1 update), a
+// medium record (2..kMedMax: key + 10 bits per update, kernels.h) or a dense
+// record (more) — at its rank among the wave's lanes of that kind, so each
+// kind is one contiguous run per wave written by one store instruction (the
+// dense record: three dwordx4). No per-update store loop: a medium lane folds
+// its updates into the payload in registers. Statuses as emit_updates_flat (A
+// after slot j = A_final, flipped back for the first of a record's two
+// updates; vote.go:77-91). Returns the bytes stored (wave-uniform).
+template <int K>
+__device__ __forceinline__ uint32_t emit_updates_med(const RoundParams& p, uint32_t wave_id, uint32_t lane,
+                                                     uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
+                                                     uint32_t A_final, uint32_t died, uint32_t& updates,
+                                                     uint32_t round_rel) {
+  static_assert(K <= 8, "slot fits 3 bits of a medium field; two updates per record per round at most");
+  uint32_t any = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) any |= E[j];
+  if (__ballot(any != 0u) == 0ull) return 0u;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int j = 0; j < K; ++j) cnt += (uint32_t)__popc(E[j]);
+  const uint32_t dmin = max(p.dense_min, kMedMax + 1u);
+  const bool dense = cnt >= dmin, med = !dense && cnt >= 2u, single = cnt == 1u;
+  const uint64_t dl = __ballot(dense), ml = __ballot(med), sl = __ballot(single);
+  const uint32_t tot_d = (uint32_t)__popcll(dl), tot_m = (uint32_t)__popcll(ml), tot_s = (uint32_t)__popcll(sl);
+  updates += wave_sum(cnt);
+  if (p.ablate_emit == 1u) return 0u;  // diagnostics: the cost of the round without its log stores
+  const uint32_t shard = wave_id % p.log_shards;
+  uint32_t base = 0, mbase = 0, dbase = 0;
+  if (lane == 0) {
+    if (tot_s) base = atomicAdd(&p.log_count[shard], tot_s);
+    if (tot_m) mbase = atomicAdd(&p.mlog_count[shard], tot_m);
+    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard], tot_d);
+  }
+  base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+  mbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)mbase);
+  dbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)dbase);
+  const uint32_t st_d = dbase >= p.dlog_cap ? 0u : min(tot_d, p.dlog_cap - dbase);
+  const uint32_t st_m = mbase >= p.mlog_cap ? 0u : min(tot_m, p.mlog_cap - mbase);
+  const uint32_t st_s = base >= p.log_cap ? 0u : min(tot_s, p.log_cap - base);
+  const bool ovf = st_d < tot_d || st_m < tot_m || st_s < tot_s;
+  const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u);
+  const uint64_t mine = dense ? dl : med ? ml : sl;
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+  if (dense) {
+    if (rank < st_d) {
+      constexpr uint32_t DW = dense_words(K);
+      uint32_t w[2 * DW];
+      w[0] = (uint32_t)key;
+      w[1] = (uint32_t)(key >> 32);
+#pragma unroll
+      for (int j = 0; j < K; ++j) w[2 + j] = E[j];
+      w[2 + K] = A_final;
+      w[3 + K] = died;
+#pragma unroll
+      for (uint32_t i = 4 + K; i < 2 * DW; ++i) w[i] = 0u;
+      uint64_t* const rec = p.dlog + ((size_t)shard * p.dlog_cap + dbase + rank) * DW;
+      if constexpr (DW % 2u == 0u) {  // 16-B aligned records (k = 8: 48 B, three dwordx4)
+#pragma unroll
+        for (uint32_t i = 0; i < DW / 2u; ++i)
+          reinterpret_cast<u32x4*>(rec)[i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < DW; ++i) rec[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+      }
+    }
+  } else if (cnt) {
+    // T: records with two updates this round; walk the updates in slot order
+    uint32_t seen = 0u, T = 0u, nz = 0u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      T |= seen & E[j];
+      seen |= E[j];
+      nz |= (E[j] != 0u ? 1u : 0u) << j;
+    }
+    uint32_t S = 0u, j = 0u, cur = 0u;
+    uint64_t pl = cnt;  // payload: n, then one field per update
+#pragma unroll
+    for (uint32_t r = 0; r < kMedMax; ++r) {
+      if (r < cnt) {
+        if (cur == 0u) {  // next slot with updates
+          j = (uint32_t)__ffs(nz) - 1u;
+          nz &= nz - 1u;
+          cur = E[0];
+#pragma unroll
+          for (int q = 1; q < K; ++q) cur = j == (uint32_t)q ? E[q] : cur;
+        }
+        const uint32_t bit = (uint32_t)__ffs(cur) - 1u;
+        cur &= cur - 1u;
+        const uint32_t m = 1u << bit;
+        const uint32_t a = ((A_final ^ (T & ~S)) >> bit) & 1u;  // A after slot j (vote.go:77-91)
+        S |= m;
+        const uint32_t st = (died & m) ? (a ? 3u : 0u) : (a ? 2u : 1u);
+        pl |= (uint64_t)med_field(j, bit, st) << (4u + 10u * r);
+      }
+    }
+    if (med) {
+      if (rank < st_m) {
+        u32x4* rec = reinterpret_cast<u32x4*>(p.mlog + ((size_t)shard * p.mlog_cap + mbase + rank) * 2u);
+        *rec = u32x4{(uint32_t)key, (uint32_t)(key >> 32), (uint32_t)pl, (uint32_t)(pl >> 32)};
+      }
+    } else if (rank < st_s) {
+      p.log[(size_t)shard * p.log_cap + base + rank] = med_word(key, (uint32_t)(pl >> 4) & 1023u);
+    }
+  }
+  if (__ballot(ovf) != 0ull) note_overflow(p, lane);
+  return 8u * st_s + 16u * st_m + 8u * dense_words(K) * st_d;
+}
+
 __device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied,
                                             bool active, uint32_t bytes_per_lane, uint32_t emitted_bytes,
                                             uint32_t updates, uint32_t died) {

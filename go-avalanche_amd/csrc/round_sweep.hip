@@ -43,6 +43,7 @@ struct SweepAcc {
   uint32_t applied = 0, died = 0, lane_bytes = 0;
   uint32_t reread = 0;  // per lane: gathered preference bytes beyond the one compulsory read of each word
   uint32_t emitted_bytes = 0, updates = 0;  // wave-uniform: StatusUpdate log bytes written, updates emitted
+  uint32_t umis = 0;  // per lane: some published word differed from ref_node's word of pref_in (p.uni_out)
 };
 
 enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3, kModeWarmPipe = 4, kModeFresh = 5 };
@@ -60,6 +61,7 @@ struct TileIn {
   uint32_t cflag;                // wave-uniform: vstale & kCAll (consider planes virtual, all-ones)
   uint32_t kw;                   // wave-uniform: kpend[tile] (kernels.h klazy); K planes not loaded if all-live
   uint32_t C[WARM ? 1 : 8];
+  uint32_t uref;                 // uniform rows (p.uni_out): ref_node's word of pref_in for the lane's block
   uint32_t w[K];                 // yes bits: err == 0 (vote.go:55)
   uint32_t cw[REPLAY ? K : 1];   // consider bits: int32(err) >= 0 (vote.go:56); sim votes: all-ones
 };
@@ -153,6 +155,9 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
   }
   in.vmask = x.active ? p.valid[x.b] : 0u;
   in.byzw = p.byz[x.node >> 5];
+  // loaded with the tile (an in-order vmcnt wait for it late in the step would also wait for the
+  // step's plane stores)
+  in.uref = p.uni_out ? p.pref_in[p.ref_node * p.PS + x.b] : 0u;
   if constexpr (REPLAY) {
     replay_load<K>(p.replay, x.gc, in.w, in.cw);
   } else {
@@ -600,6 +605,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     if (astore) st1<POL>(tr, tp + 1536u + lane, (1536u + lane) * 4u, A);
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^31
     const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
+    if (p.uni_out) acc.umis |= pub != in.uref ? 1u : 0u;  // uniform rows (kernels.h)
     if (p.push_n) {
       // peer-push exchange (kernels.h): the word being overwritten is what
       // every peer replica holds; push only a changed word
@@ -643,8 +649,11 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   }
   // LE (the fresh round, lighter on registers): log stores staged through LDS;
   // in the warm modes the staging's registers spill (measured slower)
+  // medium records (p.med, k = 8): one contiguous entry per lane with updates, no LDS staging
   uint32_t emitted;
-  if constexpr (LE)
+  if (K == 8 && p.med)
+    emitted = emit_updates_med<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, p.round_rel);
+  else if constexpr (LE)
     emitted = emit_updates_lds<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, es);
   else if constexpr (K == 8)
     emitted = emit_updates_flat<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, p.round_rel);
@@ -696,6 +705,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
       __builtin_amdgcn_make_buffer_rsrc(p.planes + (size_t)tile * (kPlanes * 64u), 0, kPlanes * 64 * 4, kRsrcWord3);
   const uint32_t A = __builtin_amdgcn_raw_buffer_load_b32(ta, (1536u + lane) * 4u, 0, POL > 0 ? 2 : 0);
   const uint32_t P0 = active ? at_byte(p.valid, b * 4u) : 0u;  // polled = live (kPendAllLive) and valid
+  const uint32_t uref = p.uni_out ? p.pref_in[p.ref_node * p.PS + b] : 0u;  // uniform rows (kernels.h)
   uint32_t rows[8];
   pick_parked(p, wd.sd, wd.bad, (nl - wd.nlA) * 2u + (wd.pair ? 32u : 0u), p.n0 + nl, p.round, p.PS * 4u, rows);
   const uint32_t bo = b * 4u;
@@ -727,6 +737,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   const uint32_t node = p.n0 + nl;
   const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
   if (active) {
+    if (p.uni_out) acc.umis |= pub != uref ? 1u : 0u;
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
     if (p.push_n) {  // peer-push exchange: as process_tile
       const uint32_t old = p.pref_out[prow];
@@ -790,8 +801,8 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
   // flags of the snapshot being read (prefetched for the run's nodes: wd.flagok) against rprev
   const bool rd = REF && p.rflag_in && wd.flagok != 0ull;
   const uint32_t rprev = rd ? at_byte(p.pref_prev, p.ref_node * p.PS * 4u + bo) : 0u;
-  const uint32_t rin = REF && p.rflag_out ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
-  uint32_t done = 0u;
+  const uint32_t rin = (REF && p.rflag_out) || p.uni_out ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
+  uint32_t done = 0u, umis = 0u;
   uint32_t applied = 0u, bytes = 0u, reread = 0u;  // per lane
   for (uint32_t i = 0; i < ntiles; ++i) {
     const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)wd.meta, (int)i);
@@ -837,6 +848,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     const uint32_t node = p.n0 + nl;
     const uint32_t pub = ((byzm >> rel) & 1ull) ? bpat : A;
     if (active) {
+      umis |= pub != rin ? 1u : 0u;
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
       if (p.push_n) {  // peer-push exchange: as process_tile
         const uint32_t old = p.pref_out[prow];
@@ -865,6 +877,84 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
   acc.applied += applied;
   acc.lane_bytes += bytes;
   acc.reread += reread;
+  if (p.uni_out) acc.umis |= umis;
+  return done;
+}
+
+// The settled candidates of a wave's run when every row of pref_in is ref_node's row of pref_prev
+// (uniform rows, kernels.h uni_in): each of a lane's 8 gathered votes would be that row's word
+// `refp`, whoever the peers are, so the settled test of settled_run needs no peer draw and no
+// gather: every polled record's accepted bit equals refp. Same outputs and accounting as
+// settled_run otherwise (the published word, the deferred +8 step); the votes' 32 B per lane are
+// not read. Bit i of the result = tile t0 + i settled; the other tiles take the draw and the
+// general path.
+constexpr uint32_t kUniRun = 8;  // longest run settled_run_uni takes (p.tpw <= 8 at k = 8)
+
+template <int POL>
+__device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32_t lane, uint32_t t0,
+                                                    uint32_t tile_end, uint32_t meta, uint32_t nlA, uint32_t nn,
+                                                    SweepAcc& acc) {
+  const uint32_t ntiles = tile_end - t0;
+  const uint32_t b = lane & (p.BL - 1u), bo = b * 4u;
+  const uint32_t vw = at_byte(p.valid, bo);
+  const uint32_t refp = at_byte(p.pref_prev, p.ref_node * p.PS * 4u + bo);  // every vote word this round
+  const uint32_t rin = p.uni_out ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
+  const unsigned long long byzm = __ballot(lane < nn && is_byz(p.byz, p.n0 + nlA + lane));
+  const uint32_t bpat = byz_pattern(p.round + 1u);
+  const __amdgpu_buffer_rsrc_t ta =
+      __builtin_amdgcn_make_buffer_rsrc(p.planes + (size_t)t0 * (kPlanes * 64u), 0, (int)(ntiles * kPlanes * 64u * 4u),
+                                        kRsrcWord3);
+  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
+  const uint32_t aoff = (1536u + lane) * 4u;
+  // the candidates' A planes are all loaded before the first test: up to kUniRun loads in flight
+  // per wave instead of one load latency per tile
+  uint32_t cand = 0u;
+  for (uint32_t i = 0; i < ntiles; ++i) {
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, (int)i);
+    if ((m & (kPendAllLive | (kVMask << 8))) == (kPendAllLive | (kVUniform << 8))) cand |= 1u << i;
+  }
+  uint32_t Av[kUniRun];
+#pragma unroll
+  for (uint32_t i = 0; i < kUniRun; ++i)
+    Av[i] = (cand >> i) & 1u ? __builtin_amdgcn_raw_buffer_load_b32(ta, aoff + i * (kPlanes * 64u * 4u), 0, POL > 0 ? 2 : 0)
+                             : 0u;
+  uint32_t done = 0u, applied = 0u, bytes = 0u, umis = 0u;
+#pragma unroll
+  for (uint32_t i = 0; i < kUniRun; ++i) {
+    if (!((cand >> i) & 1u)) continue;
+    const uint32_t tile = t0 + i;
+    const uint32_t A = Av[i];
+    const uint32_t g = tile * 64u + lane;
+    const bool active = g < p.L;
+    const uint32_t nl = (active ? g : p.L - 1u) >> p.bl_log2;
+    const uint32_t P0 = active ? vw : 0u;  // polled = live (kPendAllLive) and valid
+    if (__ballot((refp ^ A) & P0) != 0ull) continue;
+    const uint32_t node = p.n0 + nl;
+    const uint32_t pub = ((byzm >> (nl - nlA)) & 1ull) ? bpat : A;
+    if (active) {
+      umis |= pub != rin ? 1u : 0u;
+      const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
+      if (p.push_n) {  // peer-push exchange: as process_tile
+        const uint32_t old = p.pref_out[prow];
+        if (pub != old) {
+          for (uint32_t r = 0; r < p.push_n; ++r)
+            __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
+    }
+    done |= 1u << i;
+    applied += 8u * (uint32_t)__popc(P0);
+    // settled_run's accounting without the 32 B of gathered votes: A read, valid, published word
+    bytes += active ? 8u + (p.push_n ? 4u : 0u) : 0u;
+  }
+  if (lane < ntiles && ((done >> lane) & 1u)) {
+    p.kpend[t0 + lane] = ((meta & 0xFFu) + 1u) | kPendAllLive;
+    bytes += 8u;  // kpend read (prologue) + written
+  }
+  acc.applied += applied;
+  acc.lane_bytes += bytes;
+  if (p.uni_out) acc.umis |= umis;
   return done;
 }
 
@@ -891,6 +981,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   uint32_t* const es = s_emit[threadIdx.x >> 6];
   const uint32_t tiles = p.Lpad >> 6;
   SweepAcc acc;
+  // uniform rows (kernels.h): no rank's slot of pref_in carries this round's tag
+  bool uniform = p.uni_in != nullptr;
+  if (uniform)
+    for (uint32_t r = 0; r < p.uni_world; ++r) uniform = uniform && p.uni_in[r] != p.round;
   if constexpr (MODE == kModeWarmPipe) {
     // software-pipelined: tile t + nwaves's loads (state, peer draw, gathers)
     // are in flight while tile t is computed
@@ -915,6 +1009,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     wd.meta = 0u;
     wd.bad = 0ull;
     wd.sd = nullptr;
+    uint32_t uni_done = 0u;  // uniform rows: run tiles settled with no draw (settled_run_uni)
+    bool uni_ran = false;
     if constexpr (MODE == kModeWarm && K == 8) {
       if (p.tpw) {
         // a run of p.tpw consecutive tiles per wave; one Philox pass draws the
@@ -932,33 +1028,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           const uint32_t kw = (p.klazy || p.kconsume) && ti < tile_end ? p.kpend[ti] : 0u;
           wd.meta = (st << 8) | (kw & (kPendAllLive | 0xFFu));
           wd.t0 = tile;
-          const bool any_stale = __ballot((st & kVMask) == kVStale) != 0ull;
-          __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][256];
-          const PairDraw d = any_stale ? pair_draw(p, p.round, nlA, nn, lane) : single_draw(p, p.round, nlA, nn, lane);
           wd.nlA = nlA;
           wd.nn = nn;
-          wd.pair = any_stale;
-          wd.ok = !d.fallback;
-          wd.bad = d.bad;
-          wd.sd = s_draw[threadIdx.x >> 6];
-          if (wd.ok) park_draw(d, s_draw[threadIdx.x >> 6], lane, p.PS * 4u);
-          wd.flagok = 0ull;
-          if constexpr (REF) {
-            if (wd.ok && p.rflag_in && p.klazy) {  // the run's peer flags in 4 loads (settled_run)
-              const uint8_t tag = ref_tag(p.round);
-              uint32_t ok = 1u;
+          // uniform rows: the run's settled candidates first, with no draw; the draw only if a tile is left
+          const uint32_t all_tiles = (uint32_t)((1ull << (tile_end - tile)) - 1ull);
+          if (uniform && p.lean && p.settled_fast && p.klazy && p.vv && nn <= 64u && tile_end - tile <= kUniRun) {
+            uni_done = settled_run_uni<POL>(p, lane, tile, tile_end, wd.meta, nlA, nn, acc);
+            uni_ran = true;
+          }
+          const bool any_stale = __ballot((st & kVMask) == kVStale) != 0ull;
+          __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][256];
+          if (uni_done != all_tiles) {
+            const PairDraw d = any_stale ? pair_draw(p, p.round, nlA, nn, lane) : single_draw(p, p.round, nlA, nn, lane);
+            wd.pair = any_stale;
+            wd.ok = !d.fallback;
+            wd.bad = d.bad;
+            wd.sd = s_draw[threadIdx.x >> 6];
+            if (wd.ok) park_draw(d, s_draw[threadIdx.x >> 6], lane, p.PS * 4u);
+            wd.flagok = 0ull;
+            if constexpr (REF) {
+              if (wd.ok && p.rflag_in && p.klazy) {  // the run's peer flags in 4 loads (settled_run)
+                const uint8_t tag = ref_tag(p.round);
+                uint32_t ok = 1u;
 #pragma unroll
-              for (int i = 0; i < 4; ++i) ok &= p.rflag_in[d.prod[i]] == tag ? 1u : 0u;
-              wd.flagok = __ballot(ok != 0u);
+                for (int i = 0; i < 4; ++i) ok &= p.rflag_in[d.prod[i]] == tag ? 1u : 0u;
+                wd.flagok = __ballot(ok != 0u);
+              }
             }
           }
         }
       }
     }
-    uint32_t lean_done = 0u;  // run tiles the lean settled loop completed (bit i: tile wd.t0 + i)
-    bool lean_ran = false;    // the run's settled candidates were all tested by it
+    uint32_t lean_done = uni_done;  // run tiles the lean settled loop completed (bit i: tile wd.t0 + i)
+    bool lean_ran = uni_ran;        // the run's settled candidates were all tested by it
     if constexpr (MODE == kModeWarm && K == 8) {
-      if (wd.ok && wd.bad == 0ull && p.lean && p.settled_fast && p.klazy && p.vv && tile < tile_end) {
+      if (!uni_ran && wd.ok && wd.bad == 0ull && p.lean && p.settled_fast && p.klazy && p.vv && tile < tile_end) {
         lean_done = settled_run<POL, REF>(p, lane, tile_end, wd, acc);
         lean_ran = true;
       }
@@ -1019,6 +1123,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     if (by) atomicAdd(&p.bytes[shard], by);
     if (rr) atomicAdd(&p.bytes[kLogShards + shard], rr);
     if (acc.updates) atomicAdd(&p.upd_count[shard], acc.updates);
+  }
+  if (p.uni_out && __ballot(acc.umis != 0u) != 0ull && lane == 0) {
+    // some word this wave published differs from the reference row: tag the output snapshot's slot
+    // of this rank in every replica (read by the next round, after the barrier in a peer exchange)
+    const uint32_t tag = p.round + 1u;
+    p.uni_out[p.uni_rank] = tag;
+    for (uint32_t r = 0; r < p.push_n; ++r)
+      __hip_atomic_store(p.push_dst[r] + p.uni_off + p.uni_rank, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (p.arrive_n) {
     // peer exchange: this rank's arrival, stored by the round's last wave once every wave's stores

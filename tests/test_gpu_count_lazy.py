@@ -116,18 +116,23 @@ def test_count_lazy_bytes():
     so from round 2 the vote register is the A plane itself (kVUniform):
     nothing is regathered, 40 B (8 gathered words, the A read, the published
     word). Plus the tile's kpend word: read, and written when it changes
-    (every deferred round)."""
+    (every deferred round).
+    With uniform rows (option uniform_rows, default on; every published row
+    equals the reference row, so no vote is gathered) the settled round moves
+    8 B per lane: the A read and the published word."""
     n, m = 4000, 1000
-    e = avhip.Engine(n, m, k=8, seed=1, log_capacity=1 << 22)
-    e.init_records(avhip.INIT_ACCEPTED, 0)
-    lanes = e.layout_info()["lanes"]
-    tiles = (lanes + 63) // 64
-    e.run_rounds(1)  # round 0 fresh: A read, C/K/A/pref written, V virtual
-    b = e.alg_bytes()
-    e.run_rounds(1)
-    assert e.alg_bytes() - b == lanes * 100 + tiles * 8
-    b = e.alg_bytes()
-    e.run_rounds(1)
-    assert e.alg_bytes() - b == lanes * 40 + tiles * 8
-    assert e.updates_count() == 0
-    e.close()
+    for uni, settled in ((0, 40), (1, 8)):
+        e = avhip.Engine(n, m, k=8, seed=1, log_capacity=1 << 22)
+        e.set_option("uniform_rows", uni)
+        e.init_records(avhip.INIT_ACCEPTED, 0)
+        lanes = e.layout_info()["lanes"]
+        tiles = (lanes + 63) // 64
+        e.run_rounds(1)  # round 0 fresh: A read, C/K/A/pref written, V virtual
+        b = e.alg_bytes()
+        e.run_rounds(1)
+        assert e.alg_bytes() - b == lanes * 100 + tiles * 8
+        b = e.alg_bytes()
+        e.run_rounds(1)
+        assert e.alg_bytes() - b == lanes * settled + tiles * 8, uni
+        assert e.updates_count() == 0
+        e.close()

@@ -42,7 +42,7 @@ def test_fresh_round_vs_oracle(oracle, case):
 
 def test_fresh_and_kconsume_identical_to_stored_planes():
     """C4 shape at 1/50 scale through finalization: the fresh round 0 and the
-    consuming round 15 change nothing but the bytes moved; a re-initialised
+    consuming round 16 change nothing but the bytes moved; a re-initialised
     engine is fresh again."""
     n, m = 20_000, 1000
     out = []

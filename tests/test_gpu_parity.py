@@ -319,15 +319,23 @@ def dense_words(k):  # kernels.h dense_words: u64 words of a dense lane record
     return (k + 5) // 2
 
 
-def emitted_bytes(u, k=8):
-    """Log bytes the round kernels write for decoded updates `u`: a (round,
-    node, 32-target block) with >= dense_words(k) updates is one dense record
-    of dense_words(k) u64 words; other updates are 8-B single words."""
+MED_MAX = 6  # kernels.h kMedMax
+
+
+def emitted_bytes(u, k=8, med=False):
+    """Log bytes the round kernels write for decoded updates `u`, per (round,
+    node, 32-target block) with c updates. med=False (first-generation
+    kernels): c >= dense_words(k) is one dense record of dense_words(k) u64
+    words, else c single 8-B words. med=True (the k = 8 sweep,
+    round_common.h emit_updates_med): 1 update a single word, 2..MED_MAX one
+    16-B medium record, more a dense record."""
     if len(u) == 0:
         return 0
     key = np.stack([u[:, 0], u[:, 1], u[:, 3] // 32], axis=1)
     _, counts = np.unique(key, axis=0, return_counts=True)
     dw = dense_words(k)
+    if med:
+        return int(np.where(counts > MED_MAX, 8 * dw, np.where(counts >= 2, 16, 8 * counts)).sum())
     return int(np.where(counts >= dw, 8 * dw, 8 * counts).sum())
 
 
@@ -356,11 +364,12 @@ def test_c4_shape_properties():
         assert e.applied_votes() == n * m * k * 16
         u = e.fetch_updates()
         r0 = u[:, 0] == 0
-        assert b1 == lanes * cold_bytes + emitted_bytes(u[r0])
+        med = kernel == 2  # the sweep logs medium records (emit_updates_med)
+        assert b1 == lanes * cold_bytes + emitted_bytes(u[r0], med=med)
         if warm_bytes is not None:
-            assert b16 - b1 == lanes * warm_bytes + emitted_bytes(u[~r0])
+            assert b16 - b1 == lanes * warm_bytes + emitted_bytes(u[~r0], med=med)
         else:
-            assert lanes * 15 * 108 <= b16 - b1 - emitted_bytes(u[~r0]) <= lanes * 15 * 136
+            assert lanes * 15 * 108 <= b16 - b1 - emitted_bytes(u[~r0], med=med) <= lanes * 15 * 136
         assert not np.isin(u[:, 4], [avhip.STATUS_FINALIZED, avhip.STATUS_INVALID]).any()
         recs = e.read_records(0, n, 0, m)
         assert ((recs >> 17) < 128).all()

@@ -28,6 +28,7 @@ def rows(u):
                          ids=["bl32", "bl8", "bl32_byz", "bl2"])
 def test_ref_rows_vs_oracle(oracle, n, m, byz):
     eng = avhip.Engine(n, m, k=8, seed=91, byz_threshold=byz, log_capacity=1 << 24)
+    eng.set_option("uniform_rows", 0)  # uniform rows would take the settled tiles first
     eng.set_option("ref_rows", 1)
     eng.init_records(avhip.INIT_BERNOULLI, P80)
     sim = oracle.Sim(n, m, 8, seed=91, byz_threshold=byz, init_mode=avhip.INIT_BERNOULLI, init_param=P80, threads=T)
@@ -59,6 +60,7 @@ def test_ref_rows_on_off_identical_and_taken():
     out = []
     for on in (1, 0):
         eng = avhip.Engine(n, m, k=8, seed=5, log_capacity=1 << 26)
+        eng.set_option("uniform_rows", 0)  # (test_gpu_uniform_rows.py): the settled rounds would gather nothing
         eng.set_option("ref_rows", on)
         eng.init_records(avhip.INIT_BERNOULLI, P80)
         digests, settled_bytes = [], 0

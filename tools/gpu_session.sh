@@ -145,7 +145,10 @@ for s in "$@"; do
     reftests) step reftests 900 python -u -m pytest tests/test_gpu_ref_rows.py tests/test_gpu_virtual_votes.py tests/test_gpu_fresh.py tests/test_gpu_count_lazy.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     fullc5) step fullc5 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread -k "c5" ;;
     dropintests) step dropintests 600 python -u -m pytest tests/test_gpu_dropin_fuzz.py tests/test_gpu_example.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    abvar) step abvar 900 bash -c 'for v in base w6 w4 le5 le4; do for w in c4 c4pb; do for o in ref_rows=0 ref_rows=1; do echo "== $v $w $o"; if [ $v = base ]; then python tools/round_probe.py --workload $w --option $o; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w --option $o; fi; done; done; done' ;;
+    abvar) step abvar 900 bash -c 'for v in base w6 w4 le5 le4; do for w in c4 c4pb; do echo "== $v $w"; if [ $v = base ]; then python tools/round_probe.py --workload $w; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w; fi; done; done' ;;
+    abmed) step abmed 600 bash -c 'for w in c4 c4pb c3; do for o in emit_med=1 emit_med=0; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
+    abuni) step abuni 600 bash -c 'for w in c4 c5 c4p; do for o in uniform_rows=1 uniform_rows=0; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
+    unitests) step unitests 900 python -u -m pytest tests/test_gpu_uniform_rows.py tests/test_gpu_count_lazy.py tests/test_gpu_ref_rows.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     pmcall) for W in c4 c4pb c3; do WL=$W bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $?; done
             WL=c2 PMC_LAUNCHES=2 PMC_REPLAY=1 bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
