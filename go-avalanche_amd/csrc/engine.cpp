@@ -83,6 +83,7 @@ struct av_engine {
   // option "uniform_rows" (default on; kernels.h uni_*): every snapshot buffer carries one mismatch
   // slot per rank at word uni_off; uni_ok[b]: buffer b was written by a sweep round that tagged them
   bool uni_rows = true;
+  bool k_hi_virtual = true;  // option "k_hi_virtual": the K4..K7 group left unstored while counts are < 16 (kernels.h kHiVirt)
   size_t uni_off = 0;
   bool uni_ok[3] = {false, false, false};
 
@@ -490,6 +491,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   }
   p.klazy = klazy ? 1u : 0u;
   p.kconsume = kconsume ? 1u : 0u;
+  p.hivirt = e->k_hi_virtual && e->k == 8 ? 1u : 0u;
   if (klazy) e->k_pend = true;
   if (kconsume) e->k_pend = false;
   bool all_valid = true;
@@ -575,6 +577,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     e->count_bound = 127;
   }
   e->count_bound = std::min(127, e->count_bound + e->k);
+  if (fresh && p.hivirt) e->k_pend = true;  // the fresh round flags its tiles kHiVirt
   e->fresh = false;
   e->rflag_ok[nb] = refr && refw;
   e->uni_ok[nb] = uni;
@@ -1806,6 +1809,10 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->plane_nt = value != 0;
   } else if (n == "ablate_emit") {
     e->ablate_emit = (int)std::max<int64_t>(0, std::min<int64_t>(2, value));
+  } else if (n == "k_hi_virtual") {  // A/B: virtual K4..K7 group (kernels.h kHiVirt)
+    int rc = materialize_counts(e);
+    if (rc != AV_OK) return rc;
+    e->k_hi_virtual = value != 0;
   } else if (n == "uniform_rows") {  // A/B: uniform-row settled tests (kernels.h uni_*)
     e->uni_rows = value != 0;
     ref_invalidate(e);

@@ -186,6 +186,7 @@ struct RoundParams {
   // targets (tn = targets in this engine's range).
   uint32_t fresh;
   uint32_t tn;
+  uint32_t hivirt;  // k = 8 sweep rounds may leave the K4..K7 group unstored (kHiVirt)
   uint32_t tpw;     // kModeWarm, k = 8: run length of consecutive tiles per wave with one shared peer draw (0 = grid stride)
   uint32_t settled_fast;  // kModeWarm, k = 8: settled tiles skip process_tile (round_sweep.hip settled_fast)
   // kModeWarm, k = 8, BL dividing 64 (a lane's block is lane % BL): the settled candidates of a wave's
@@ -210,6 +211,17 @@ struct RoundParams {
   uint32_t med;
 };
 constexpr uint32_t kPendAllLive = 0x80000000u;
+// kpend bit 30 (kHiVirt, k = 8 sweep rounds while every count is < 16; option "k_hi_virtual"): the
+// tile's K4..K7 group is not stored: K4 = K5 = K6 = 0 on every record and K7 = the records past the
+// engine's last target (k_init_planes: every existing target's record live, none deleted since).
+// Set by the fresh round; kept by a warm round whose counts all stay < 16 with no deletion (or
+// that defers the tile's count planes); written back by the round that breaks it, kconsume and
+// k_kl_materialize (k_read_records_v reads it virtually).
+constexpr uint32_t kHiVirt = 0x40000000u;
+__host__ __device__ inline uint32_t real_mask(uint32_t tn, uint32_t b) {  // existing targets of local block b
+  const uint32_t rem = tn > b * 32u ? tn - b * 32u : 0u;
+  return rem >= 32u ? ~0u : ((1u << rem) - 1u);
+}
 constexpr uint32_t kVStale = 1u, kVUniform = 2u, kVMask = 3u, kCAll = 4u;
 
 // Division by the (runtime) block count BL without a hardware divide:

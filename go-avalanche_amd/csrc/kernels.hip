@@ -559,7 +559,12 @@ __global__ __launch_bounds__(256) void k_read_records_v(const RoundParams p, uin
     for (int q = 0; q < 8; ++q) s.V[q] = s.A;
   }
   if (p.klazy) {
-    const uint32_t pend = p.kpend[tile] & 0xFFu;
+    const uint32_t kw = p.kpend[tile];
+    if (kw & kHiVirt) {  // the K4..K7 group is virtual (kernels.h)
+      s.K[4] = s.K[5] = s.K[6] = 0u;
+      s.K[7] = ~real_mask(p.tn, b);
+    }
+    const uint32_t pend = kw & 0xFFu;
     if (pend) {  // + 8 * pend on the polled records: pend added to count bits 3..6
       const uint32_t P0 = ~s.K[7] & p.valid[b];
       uint32_t cy = 0u;

@@ -134,11 +134,14 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
       in.v1 = ld4<POL>(grp + 64);
     }
     if constexpr (VV) {
-      if (p.klazy || p.kconsume) in.kw = meta ? meta_of(*wd, tile) & (kPendAllLive | 0xFFu) : uni(p.kpend[tile]);
+      if (p.klazy || p.kconsume) in.kw = meta ? meta_of(*wd, tile) & (kPendAllLive | kHiVirt | 0xFFu) : uni(p.kpend[tile]);
     }
     if (!(in.kw & kPendAllLive) || !p.klazy) {
       in.k0 = ld4<POL>(grp + 128);
-      in.k1 = ld4<POL>(grp + 192);
+      if (in.kw & kHiVirt)  // the K4..K7 group is virtual (kernels.h kHiVirt)
+        in.k1 = u32x4{0u, 0u, 0u, ~real_mask(p.tn, x.b)};
+      else
+        in.k1 = ld4<POL>(grp + 192);
     } else {
       in.k0 = u32x4{0u, 0u, 0u, 0u};
       in.k1 = u32x4{0u, 0u, 0u, 0u};
@@ -554,7 +557,8 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
       if (!kdefer) {
         if (kunread) {  // late load: the tile leaves the deferred state
           k0 = ld4<POL>(reinterpret_cast<const u32x4*>(tp) + lane + 128);
-          k1 = ld4<POL>(reinterpret_cast<const u32x4*>(tp) + lane + 192);
+          k1 = in.kw & kHiVirt ? u32x4{0u, 0u, 0u, ~real_mask(p.tn, b)}
+                               : ld4<POL>(reinterpret_cast<const u32x4*>(tp) + lane + 192);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             Kp[i] = k0[i];
@@ -591,6 +595,11 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
 
   // klazy rounds: a tile whose A plane did not change does not rewrite it
   const bool astore = !klazy || __ballot(active && A != A_in) != 0ull;
+  // the K4..K7 group stays virtual (kernels.h kHiVirt) while every count is < 16 and nothing was
+  // deleted: set by the fresh round, kept by klazy rounds (deferred tiles leave K as it is)
+  bool hv = false;
+  if (K == 8 && p.hivirt && ((!WARM && p.fresh) || (klazy && (in.kw & kHiVirt))))
+    hv = kdefer || __ballot(active && ((Kp[4] | Kp[5] | Kp[6] | died) != 0u)) == 0ull;
   if (active) {
     if (!kdefer) {
       u32x4 o2, o3;
@@ -600,7 +609,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
         o3[i] = Kp[4 + i];
       }
       st4<POL>(tr, grp + 128, 2048u + lane * 16u, o2);
-      st4<POL>(tr, grp + 192, 3072u + lane * 16u, o3);
+      if (!hv) st4<POL>(tr, grp + 192, 3072u + lane * 16u, o3);
     }
     if (astore) st1<POL>(tr, tp + 1536u + lane, (1536u + lane) * 4u, A);
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^31
@@ -639,12 +648,18 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
       // live records == valid targets in every lane (no live-but-invalid record):
       // the next round need not read K to find the polled set
       const bool all_live = __ballot(active && live0 != vmask) == 0ull;
-      const uint32_t kw = (kdefer ? pend + 1u : 0u) | (all_live ? kPendAllLive : 0u);
+      const uint32_t kw = (kdefer ? pend + 1u : 0u) | (all_live ? kPendAllLive : 0u) | (hv ? kHiVirt : 0u);
       if (lane == 0 && kw != in.kw) p.kpend[tile] = kw;
       if (lane == 0) acc.lane_bytes += kw != in.kw ? 8u : 4u;  // kpend word read (+ written)
     } else if (kcons) {
       if (lane == 0 && in.kw) p.kpend[tile] = 0u;
       if (lane == 0) acc.lane_bytes += in.kw ? 8u : 4u;
+    }
+  }
+  if constexpr (!WARM && !REPLAY && K == 8) {  // the fresh round starts the tile's virtual K4..K7 group
+    if (hv && lane == 0) {
+      p.kpend[tile] = kHiVirt;
+      acc.lane_bytes += 4u;
     }
   }
   // LE (the fresh round, lighter on registers): log stores staged through LDS;
@@ -668,7 +683,9 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   // stale: 7 regathered words instead of the 8 V planes read; virt: V planes not written
   // push: + the 4-B read of the word being overwritten
   // kl: K planes neither read (kunread and deferred) nor written (deferred); A not rewritten
-  const uint32_t kbytes = (kunread && kdefer ? 32u : 0u) + (kdefer ? 32u : 0u);
+  const uint32_t kbytes = (kunread && kdefer ? 32u : 0u) + (kdefer ? 32u : 0u) +
+                          // virtual K4..K7 group (kHiVirt): not read (if K was read), not written
+                          (WARM && (in.kw & kHiVirt) && !(kunread && kdefer) ? 16u : 0u) + (hv && !kdefer ? 16u : 0u);
   // V read: 32 B stored, 28 B regathered (stale), 0 B uniform
   acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale == kVStale ? 4u : in.stale == kVUniform ? 32u : 0u) -
                                  (virt ? 32u : 0u) - (cvirt ? 32u : 0u) + (p.push_n ? 4u : 0u) -
@@ -750,7 +767,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
     st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
   }
   if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, p.pref_in[p.ref_node * p.PS + (active ? b : 0u)]);
-  if (lane == 0) p.kpend[tile] = ((kw & 0xFFu) + 1u) | kPendAllLive;
+  if (lane == 0) p.kpend[tile] = ((kw & 0xFFu) + 1u) | kPendAllLive | (kw & kHiVirt);
   acc.applied += 8u * (uint32_t)__popc(P0);
   // process_tile's accounting for this case: 17 plane words + 8 vote words +
   // valid read, minus V (uniform), V store (virtual), K read + store (deferred),
@@ -871,7 +888,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
   }
   // the settled tiles' pending count steps: +1 deferred +8 step each (lane i: tile t0 + i)
   if (lane < ntiles && ((done >> lane) & 1u)) {
-    p.kpend[t0 + lane] = ((wd.meta & 0xFFu) + 1u) | kPendAllLive;
+    p.kpend[t0 + lane] = ((wd.meta & 0xFFu) + 1u) | kPendAllLive | (wd.meta & kHiVirt);
     bytes += 8u;  // kpend read (prologue) + written
   }
   acc.applied += applied;
@@ -949,7 +966,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
     bytes += active ? 8u + (p.push_n ? 4u : 0u) : 0u;
   }
   if (lane < ntiles && ((done >> lane) & 1u)) {
-    p.kpend[t0 + lane] = ((meta & 0xFFu) + 1u) | kPendAllLive;
+    p.kpend[t0 + lane] = ((meta & 0xFFu) + 1u) | kPendAllLive | (meta & kHiVirt);
     bytes += 8u;  // kpend read (prologue) + written
   }
   acc.applied += applied;
@@ -1026,7 +1043,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           const uint32_t ti = tile + lane;
           const uint32_t st = p.vv && ti < tile_end ? p.vstale[ti] : 0u;
           const uint32_t kw = (p.klazy || p.kconsume) && ti < tile_end ? p.kpend[ti] : 0u;
-          wd.meta = (st << 8) | (kw & (kPendAllLive | 0xFFu));
+          wd.meta = (st << 8) | (kw & (kPendAllLive | kHiVirt | 0xFFu));
           wd.t0 = tile;
           wd.nlA = nlA;
           wd.nn = nn;
@@ -1074,7 +1091,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           if (lean_done && ((lean_done >> (tile - wd.t0)) & 1u)) continue;
           if (wd.ok && p.settled_fast && p.klazy && p.vv && !lean_ran) {
             const uint32_t m = meta_of(wd, tile);
-            if (((m >> 8) & kVMask) == kVUniform && (m & kPendAllLive) && settled_tile<POL, REF>(p, tile, lane, m & 0x800000FFu, wd, acc))
+            if (((m >> 8) & kVMask) == kVUniform && (m & kPendAllLive) &&
+                settled_tile<POL, REF>(p, tile, lane, m & (kPendAllLive | kHiVirt | 0xFFu), wd, acc))
               continue;
           }
         }
@@ -1261,9 +1279,10 @@ __global__ __launch_bounds__(256) void k_kl_materialize(const RoundParams p) {
   const uint32_t pend = kw & 0xFFu;
   if (kw == 0u) return;
   const LaneIdx x = lane_idx(p, tile, lane);
-  if (pend && x.active) {
+  if ((pend || (kw & kHiVirt)) && x.active) {
     u32x4* const grp = reinterpret_cast<u32x4*>(p.planes + (size_t)tile * (kPlanes * 64u)) + lane;
-    const u32x4 k0 = grp[128], k1 = grp[192];
+    const u32x4 k0 = grp[128];
+    const u32x4 k1 = kw & kHiVirt ? u32x4{0u, 0u, 0u, ~real_mask(p.tn, x.b)} : grp[192];  // kernels.h kHiVirt
     uint32_t Kp[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

@@ -119,20 +119,52 @@ def test_count_lazy_bytes():
     (every deferred round).
     With uniform rows (option uniform_rows, default on; every published row
     equals the reference row, so no vote is gathered) the settled round moves
-    8 B per lane: the A read and the published word."""
+    8 B per lane: the A read and the published word.
+    With the K4..K7 group virtual (option k_hi_virtual, default on: every
+    count < 16, kernels.h kHiVirt) round 1 reads 16 B less of K: 84 B."""
     n, m = 4000, 1000
-    for uni, settled in ((0, 40), (1, 8)):
+    for uni, hv, warm, settled in ((0, 0, 100, 40), (1, 0, 100, 8), (1, 1, 84, 8)):
         e = avhip.Engine(n, m, k=8, seed=1, log_capacity=1 << 22)
         e.set_option("uniform_rows", uni)
+        e.set_option("k_hi_virtual", hv)
         e.init_records(avhip.INIT_ACCEPTED, 0)
         lanes = e.layout_info()["lanes"]
         tiles = (lanes + 63) // 64
         e.run_rounds(1)  # round 0 fresh: A read, C/K/A/pref written, V virtual
         b = e.alg_bytes()
         e.run_rounds(1)
-        assert e.alg_bytes() - b == lanes * 100 + tiles * 8
+        assert e.alg_bytes() - b == lanes * warm + tiles * 8, (uni, hv)
         b = e.alg_bytes()
         e.run_rounds(1)
-        assert e.alg_bytes() - b == lanes * settled + tiles * 8, uni
+        assert e.alg_bytes() - b == lanes * settled + tiles * 8, (uni, hv)
         assert e.updates_count() == 0
         e.close()
+
+
+@pytest.mark.parametrize("init", [avhip.INIT_BERNOULLI, avhip.INIT_PAIRS])
+def test_k_hi_virtual_on_off_identical(init):
+    """C4 shape at 1/50 scale (and the conflicting-pairs form, whose storm
+    keeps counts low for longer): identical records, StatusUpdates and
+    counters with the virtual K4..K7 group on and off, through the storm, the
+    settled rounds, kconsume and finalization, with a mid-run read (virtual
+    read of flagged tiles) and a validity flip (write-back); fewer bytes on."""
+    n, m = 20_000, 1000
+    out = []
+    for hv in (0, 1):
+        e = avhip.Engine(n, m, k=8, seed=0xA7A1A9C4, log_capacity=1 << 27)
+        e.set_option("k_hi_virtual", hv)
+        e.init_records(init, P80)
+        e.run_rounds(2)
+        mid = e.read_records()
+        b2 = e.alg_bytes()
+        e.run_rounds(3)
+        e.set_valid(17, False)
+        e.run_rounds(2)
+        e.set_valid(17, True)
+        e.run_rounds(15)
+        out.append((mid, e.read_records(), e.fetch_updates(), e.applied_votes(), e.finalized_count(), b2))
+        e.close()
+    off, on = out
+    for a, b in zip(off[:5], on[:5]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    assert on[5] < off[5]

@@ -355,6 +355,7 @@ def test_c4_shape_properties():
         e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4)
         e.set_option("kernel", kernel)
         e.set_option("count_lazy", 0)  # per-lane bytes with stored count planes (test_gpu_count_lazy.py)
+        e.set_option("k_hi_virtual", 0)  # (the virtual K4..K7 group's bytes: test_gpu_count_lazy.py)
         e.init_records(avhip.INIT_BERNOULLI, P80)
         lanes = e.layout_info()["lanes"]
         e.run_rounds(1)  # round 0: consider planes fill up
