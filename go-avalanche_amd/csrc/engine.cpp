@@ -680,6 +680,8 @@ uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
     return (uint32_t)(bpc * cus);
   }
   // (by size: a run's nodes must fit the shared draw, 2 producer lanes each: 8 tiles need BL >= 16)
+  // (a run's nodes must fit the run's peer draw: 2 producer lanes per node and round, 64 lanes; runs
+  // of 16 tiles at BL >= 32 draw both rounds in two passes, option tiles_per_wave = 16)
   const uint64_t tpw = e->tiles_per_wave ? e->tiles_per_wave : (tiles >= (1u << 18) && e->BL >= 16 ? 8u : 4u);
   const uint64_t waves = (tiles + tpw - 1) / tpw;
   return (uint32_t)std::max<uint64_t>(1, (waves + 3) / 4);

@@ -71,8 +71,13 @@ struct TileIn {
 // draws (some tile of the run is kVStale), else round's only; `ok` = the
 // run's nodes fit the producer lanes (otherwise every tile draws its own).
 struct WaveDraw {
-  const uint32_t* sd;  // the draw, parked in LDS (round_slots.h park_draw)
-  unsigned long long bad;
+  // the draws parked in LDS (round_slots.h park_draw): node rel of the run has its 8 candidates at
+  // sdc + rel * 8 (this round) and sdp + rel * 8 (round - 1, if pair); badc / badp: the draws'
+  // repeated-candidate ballots, bit rel * 2 (and rel * 2 + 1) for node rel
+  const uint32_t* sdc;
+  const uint32_t* sdp;
+  unsigned long long badc, badp;
+  uint32_t fofs;  // REF: bit offset of this round's producer lanes in flagok (32 in the paired layout)
   uint32_t nlA, t0, nn;
   // REF: producer lane q's 4 candidates all carry pref_in's reference-row tag (bit q): a node's 8
   // peers are flagged iff both of its producer lanes' bits are set
@@ -177,14 +182,14 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
         const uint32_t base = (x.nl - wd->nlA) * 2u;
         if (in.stale == kVStale) {
           uint32_t pp[K];
-          pick_parked(p, wd->sd, wd->bad, base, x.node, p.round - 1u, rb, pp);
+          pick_parked(p, wd->sdp, wd->badp, base, x.node, p.round - 1u, rb, pp);
 #pragma unroll
           for (int i = 0; i < 4; ++i) in.v0[i] = at_byte(p.pref_prev, pp[7 - i] + bo);
 #pragma unroll
           for (int i = 0; i < 3; ++i) in.v1[i] = at_byte(p.pref_prev, pp[3 - i] + bo);
           in.v1[3] = 0u;
         }
-        pick_parked(p, wd->sd, wd->bad, base + (wd->pair ? 32u : 0u), x.node, p.round, rb, rows);
+        pick_parked(p, wd->sdc, wd->badc, base, x.node, p.round, rb, rows);
         drawn = have_rows = true;
       } else if (in.stale == kVStale) {
         // the vote register after last round's 8 sim votes is those votes:
@@ -724,7 +729,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   const uint32_t P0 = active ? at_byte(p.valid, b * 4u) : 0u;  // polled = live (kPendAllLive) and valid
   const uint32_t uref = p.uni_out ? p.pref_in[p.ref_node * p.PS + b] : 0u;  // uniform rows (kernels.h)
   uint32_t rows[8];
-  pick_parked(p, wd.sd, wd.bad, (nl - wd.nlA) * 2u + (wd.pair ? 32u : 0u), p.n0 + nl, p.round, p.PS * 4u, rows);
+  pick_parked(p, wd.sdc, wd.badc, (nl - wd.nlA) * 2u, p.n0 + nl, p.round, p.PS * 4u, rows);
   const uint32_t bo = b * 4u;
   uint32_t dis = 0u, all = ~0u;
   bool gather = true;
@@ -833,7 +838,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     const uint32_t rel = nl - wd.nlA;
     uint32_t rows[8];
     {
-      const uint32_t* q = wd.sd + (rel * 2u + (wd.pair ? 32u : 0u)) * 4u;
+      const uint32_t* q = wd.sdc + rel * 8u;
       const u32x4 lo = *reinterpret_cast<const u32x4*>(q);
       const u32x4 hi = *reinterpret_cast<const u32x4*>(q + 4);
 #pragma unroll
@@ -845,7 +850,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     uint32_t dis = 0u, all = ~0u;
     bool gather = true;
     if (rd) {
-      const uint32_t base = rel * 2u + (wd.pair ? 32u : 0u);  // the node's producer lanes
+      const uint32_t base = rel * 2u + wd.fofs;  // the node's producer lanes
       const bool fl = ((wd.flagok >> base) & 3ull) == 3ull;
       if (__ballot(active && !fl) == 0ull) {
         dis = all = rprev;
@@ -905,7 +910,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
 // settled_run otherwise (the published word, the deferred +8 step); the votes' 32 B per lane are
 // not read. Bit i of the result = tile t0 + i settled; the other tiles take the draw and the
 // general path.
-constexpr uint32_t kUniRun = 8;  // longest run settled_run_uni takes (p.tpw <= 8 at k = 8)
+constexpr uint32_t kUniRun = 16;  // longest run settled_run_uni takes (p.tpw <= 16)
 
 template <int POL>
 __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32_t lane, uint32_t t0,
@@ -1024,8 +1029,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     wd.flagok = 0ull;
     wd.t0 = 0u;
     wd.meta = 0u;
-    wd.bad = 0ull;
-    wd.sd = nullptr;
+    wd.badc = wd.badp = 0ull;
+    wd.sdc = wd.sdp = nullptr;
+    wd.fofs = 0u;
     uint32_t uni_done = 0u;  // uniform rows: run tiles settled with no draw (settled_run_uni)
     bool uni_ran = false;
     if constexpr (MODE == kModeWarm && K == 8) {
@@ -1054,22 +1060,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
             uni_ran = true;
           }
           const bool any_stale = __ballot((st & kVMask) == kVStale) != 0ull;
-          __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][256];
+          __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][512];
+          uint32_t* const sd = s_draw[threadIdx.x >> 6];
           if (uni_done != all_tiles) {
-            const PairDraw d = any_stale ? pair_draw(p, p.round, nlA, nn, lane) : single_draw(p, p.round, nlA, nn, lane);
             wd.pair = any_stale;
-            wd.ok = !d.fallback;
-            wd.bad = d.bad;
-            wd.sd = s_draw[threadIdx.x >> 6];
-            if (wd.ok) park_draw(d, s_draw[threadIdx.x >> 6], lane, p.PS * 4u);
             wd.flagok = 0ull;
-            if constexpr (REF) {
-              if (wd.ok && p.rflag_in && p.klazy) {  // the run's peer flags in 4 loads (settled_run)
-                const uint8_t tag = ref_tag(p.round);
-                uint32_t ok = 1u;
+            if (any_stale && nn * 2u > 32u) {
+              // both rounds' draws for up to 32 nodes: two passes over all 64 lanes, parked side by side
+              const PairDraw dp = single_draw(p, p.round - 1u, nlA, nn, lane);
+              const PairDraw dc = single_draw(p, p.round, nlA, nn, lane);
+              wd.ok = !dp.fallback && !dc.fallback;
+              if (wd.ok) {
+                park_draw(dp, sd, lane, p.PS * 4u);
+                park_draw(dc, sd + 256, lane, p.PS * 4u);
+              }
+              wd.sdp = sd;
+              wd.sdc = sd + 256;
+              wd.badp = dp.bad;
+              wd.badc = dc.bad;
+            } else {
+              // one pass: lanes 0-31 round - 1 and 32-63 this round (pair), or all 64 this round
+              const PairDraw d = any_stale ? pair_draw(p, p.round, nlA, nn, lane) : single_draw(p, p.round, nlA, nn, lane);
+              wd.ok = !d.fallback;
+              if (wd.ok) park_draw(d, sd, lane, p.PS * 4u);
+              wd.sdp = sd;
+              wd.sdc = any_stale ? sd + 128 : sd;
+              wd.badp = d.bad & 0xFFFFFFFFull;
+              wd.badc = any_stale ? d.bad >> 32 : d.bad;
+              wd.fofs = any_stale ? 32u : 0u;
+              if constexpr (REF) {
+                if (wd.ok && p.rflag_in && p.klazy) {  // the run's peer flags in 4 loads (settled_run)
+                  const uint8_t tag = ref_tag(p.round);
+                  uint32_t ok = 1u;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) ok &= p.rflag_in[d.prod[i]] == tag ? 1u : 0u;
-                wd.flagok = __ballot(ok != 0u);
+                  for (int i = 0; i < 4; ++i) ok &= p.rflag_in[d.prod[i]] == tag ? 1u : 0u;
+                  wd.flagok = __ballot(ok != 0u);
+                }
               }
             }
           }
@@ -1079,7 +1105,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     uint32_t lean_done = uni_done;  // run tiles the lean settled loop completed (bit i: tile wd.t0 + i)
     bool lean_ran = uni_ran;        // the run's settled candidates were all tested by it
     if constexpr (MODE == kModeWarm && K == 8) {
-      if (!uni_ran && wd.ok && wd.bad == 0ull && p.lean && p.settled_fast && p.klazy && p.vv && tile < tile_end) {
+      if (!uni_ran && wd.ok && wd.badc == 0ull && p.lean && p.settled_fast && p.klazy && p.vv && tile < tile_end) {
         lean_done = settled_run<POL, REF>(p, lane, tile_end, wd, acc);
         lean_ran = true;
       }

@@ -149,10 +149,11 @@ for s in "$@"; do
     abmed) step abmed 600 bash -c 'for w in c4 c4pb c3; do for o in emit_med=1 emit_med=0; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     abuni) step abuni 600 bash -c 'for w in c4 c5 c4p; do for o in uniform_rows=1 uniform_rows=0; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     unitests) step unitests 900 python -u -m pytest tests/test_gpu_uniform_rows.py tests/test_gpu_count_lazy.py tests/test_gpu_ref_rows.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    abtpw) step abtpw 600 bash -c 'for w in c4 c5; do for o in tiles_per_wave=4 tiles_per_wave=8 tiles_per_wave=16; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
+    abtpw) step abtpw 600 bash -c 'for w in c4 c4p; do for o in tiles_per_wave=16 tiles_per_wave=8; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     abub) step abub 600 bash -c 'for w in c4 c5 c3; do for o in uni_blocks=-1 uni_blocks=2560 uni_blocks=5120 uni_blocks=0; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     abhv) step abhv 600 bash -c 'for w in c4 c4pb c3; do for o in k_hi_virtual=1 k_hi_virtual=0; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     hvtests) step hvtests 900 python -u -m pytest tests/test_gpu_count_lazy.py tests/test_gpu_fresh.py tests/test_gpu_virtual_votes.py tests/test_gpu_uniform_rows.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    barrier) step barrier 300 bash -c 'python tools/barrier_cost.py --world 2 --json gpurun_out/barrier2.json && python tools/barrier_cost.py --world 4 --json gpurun_out/barrier4.json && python tools/barrier_cost.py --world 2 --nodes 131072 --json gpurun_out/barrier2_big.json' ;;
     pmcall) for W in c4 c4pb c3; do WL=$W bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $?; done
             WL=c2 PMC_LAUNCHES=2 PMC_REPLAY=1 bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
