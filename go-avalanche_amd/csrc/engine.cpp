@@ -83,6 +83,7 @@ struct av_engine {
   // option "uniform_rows" (default on; kernels.h uni_*): every snapshot buffer carries one mismatch
   // slot per rank at word uni_off; uni_ok[b]: buffer b was written by a sweep round that tagged them
   bool uni_rows = true;
+  uint32_t uni_merge = 1;  // option "uni_merge": runs per wave in a round with a uniform input (kernels.h)
   bool k_hi_virtual = true;  // option "k_hi_virtual": the K4..K7 group left unstored while counts are < 16 (kernels.h kHiVirt)
   size_t uni_off = 0;
   bool uni_ok[3] = {false, false, false};
@@ -205,7 +206,6 @@ struct av_engine {
   // responder variant (option "responder", kernels.h pub_mode) and the nodes
   // that no longer poll (av_set_polling); both run the first-generation kernel
   uint32_t dense_min = 0;  // option "dense_min" (kernels.h dense records; default dense_min(k))
-  bool emit_med = true;    // option "emit_med": medium records in the k = 8 sweep rounds (kernels.h kMedMax)
   int32_t pub_mode = 0;
   uint32_t* readd = nullptr;     // [L] pub_mode 2: re-add marks
   uint32_t* died_out = nullptr;  // [L] pub_mode 2: records deleted this round
@@ -290,7 +290,6 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.mlog = e->mlog;
   p.mlog_count = e->mlog_count;
   p.mlog_cap = e->mlog_cap;
-  p.med = e->emit_med ? 1u : 0u;
   p.log_overflow = e->log_overflow;
   p.applied = e->applied;
   p.bytes = e->bytes;
@@ -555,6 +554,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     p.uni_rank = (uint32_t)std::max(0, e->peer_rank);
     p.uni_out = e->pref[nb] + e->uni_off;
     p.uni_in = e->uni_ok[e->cur] ? e->pref[e->cur] + e->uni_off : nullptr;
+    p.uni_merge = e->uni_merge;
   }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (e->timing) {
@@ -1815,6 +1815,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     int rc = materialize_counts(e);
     if (rc != AV_OK) return rc;
     e->k_hi_virtual = value != 0;
+  } else if (n == "uni_merge") {  // tuning: runs per wave in a uniform-input round (1 = off)
+    AV_CHECK(value >= 1 && value <= 16, AV_ERR_INVALID_ARG, "bad uni_merge");
+    e->uni_merge = (uint32_t)value;
   } else if (n == "uniform_rows") {  // A/B: uniform-row settled tests (kernels.h uni_*)
     e->uni_rows = value != 0;
     ref_invalidate(e);
@@ -1894,8 +1897,6 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     rc = refresh_pref(e);  // republish the current snapshot under the new rule
     if (rc != AV_OK) return rc;
     AV_HIP(hipStreamSynchronize(e->stream));
-  } else if (n == "emit_med") {  // A/B: medium lane records (kernels.h kMedMax) in the k = 8 sweep rounds
-    e->emit_med = value != 0;
   } else if (n == "dense_min") {  // tuning (A/B): fewer updates per dense record; the dense log may fill sooner
     AV_CHECK(value >= 1 && value <= 32 * (int64_t)e->k + 1, AV_ERR_INVALID_ARG, "bad dense_min");
     e->dense_min = (uint32_t)value;

@@ -179,6 +179,7 @@ struct RoundParams {
   uint32_t* uni_out;
   const uint32_t* uni_in;
   uint32_t uni_world, uni_rank, uni_off;
+  uint32_t uni_merge;  // a round with a uniform input: every uni_merge-th wave takes uni_merge runs (1: off)
 
   // fresh: the round right after av_init_records: every record is a
   // NewVoteRecord (votes = consider = 0, count 0, vote.go:33-35), so the
@@ -205,10 +206,6 @@ struct RoundParams {
   uint32_t* died_out;
   const uint32_t* nopoll;
   uint32_t dense_min;  // a lane with >= dense_min updates logs one dense record (default dense_min(k))
-  // medium lane records (k_round_sweep, k = 8; emit_updates_med): a lane with 2..kMedMax updates
-  // logs one 16-B record instead of 8 B per update, a lane with more a dense record; every lane
-  // then stores at most one entry, at its rank among the wave's lanes of that kind
-  uint32_t med;
 };
 constexpr uint32_t kPendAllLive = 0x80000000u;
 // kpend bit 30 (kHiVirt, k = 8 sweep rounds while every count is < 16; option "k_hi_virtual"): the

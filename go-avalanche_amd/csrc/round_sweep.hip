@@ -219,166 +219,6 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
   }
 }
 
-// StatusUpdate emission of one tile, staged through the wave's LDS area so
-// that the log is written with whole-wave contiguous stores (emit_updates,
-// round_common.h, writes the same log: a dense record per lane with >=
-// dense_min updates, single packed words for the rest). The dense records of
-// the wave are assembled at consecutive LDS slots (rank among dense lanes)
-// and copied out 16 B per lane; each sparse lane writes its singles at its
-// exclusive prefix in LDS and the wave copies them out 8 B per lane. One
-// atomic per kind per wave reserves the wave's run in its log shard, as in
-// emit_updates. es: kEmitWords u32 of LDS for this wave.
-constexpr uint32_t kEmitWords = 768;  // 64 dense records of 12 words (k = 8) or 384 singles
-
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-template <int K>
-__device__ __forceinline__ uint32_t emit_updates_lds(const RoundParams& p, uint32_t wave_id, uint32_t lane,
-                                                     uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
-                                                     uint32_t A_final, uint32_t died, uint32_t& updates,
-                                                     uint32_t* es) {
-  uint32_t any = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) any |= E[j];
-  if (__ballot(any != 0u) == 0ull) return 0u;
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) cnt += (uint32_t)__popc(E[j]);
-  constexpr uint32_t DW = dense_words(K);  // u64 words per dense record
-  constexpr uint32_t RW = 2u * DW;         // u32 words per dense record
-  static_assert(64u * RW <= kEmitWords, "dense records of a wave must fit the LDS area");
-  const bool dense = cnt >= p.dense_min;
-  const uint64_t dl = __ballot(dense);
-  const uint32_t scnt = dense ? 0u : cnt;
-  const uint32_t incl = wave_incl_scan(scnt, lane);
-  const uint32_t tot_s = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  const uint32_t tot_d = (uint32_t)__popcll(dl);
-  updates += wave_sum(cnt);
-  if (p.ablate_emit == 1u) return 0u;  // diagnostics: the cost of the round without its log stores
-  const uint32_t shard = wave_id % p.log_shards;
-  uint32_t base = 0, dbase = 0;
-  if (p.ablate_emit == 2u) {  // diagnostics: stores at made-up positions, no reserving atomic (log invalid)
-    base = p.log_cap > 8192u ? (wave_id * 509u) % (p.log_cap - 4096u) : 0u;
-    dbase = p.dlog_cap > 128u ? (wave_id * 131u) % (p.dlog_cap - 64u) : 0u;
-  } else if (lane == 0) {
-    if (tot_s) base = atomicAdd(&p.log_count[shard], tot_s);
-    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard], tot_d);
-  }
-  base = (uint32_t)__shfl((int)base, 0, 64);
-  dbase = (uint32_t)__shfl((int)dbase, 0, 64);
-  const uint32_t st_d = dbase >= p.dlog_cap ? 0u : min(tot_d, p.dlog_cap - dbase);
-  const uint32_t st_s = base >= p.log_cap ? 0u : min(tot_s, p.log_cap - base);
-  bool ovf = st_d < tot_d || st_s < tot_s;
-  if (tot_d) {
-    if (dense) {
-      uint32_t* const r = es + __builtin_amdgcn_mbcnt_hi((uint32_t)(dl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dl, 0u)) * RW;
-      const uint64_t key = pack_update(p.round_rel, node, 0u, tbase, 0u);
-      r[0] = (uint32_t)key;
-      r[1] = (uint32_t)(key >> 32);
-#pragma unroll
-      for (int j = 0; j < K; ++j) r[2 + j] = E[j];
-      r[2 + K] = A_final;
-      r[3 + K] = died;
-    }
-    wave_lds_sync();
-    uint32_t* const dst = reinterpret_cast<uint32_t*>(p.dlog + ((size_t)shard * p.dlog_cap + dbase) * DW);
-    const uint32_t nw = st_d * RW;
-    if constexpr (RW % 4u == 0u) {
-      for (uint32_t i = lane * 4u; i < nw; i += 256u)
-        *reinterpret_cast<u32x4*>(dst + i) = *reinterpret_cast<const u32x4*>(es + i);
-    } else {
-      for (uint32_t i = lane * 2u; i < nw; i += 128u)
-        *reinterpret_cast<uint64_t*>(dst + i) = *reinterpret_cast<const uint64_t*>(es + i);
-    }
-    wave_lds_sync();
-  }
-  if (tot_s) {
-    uint64_t* const dst = p.log + (size_t)shard * p.log_cap + base;
-    if (tot_s * 2u <= kEmitWords) {
-      // this lane's singles at its exclusive prefix, then one contiguous copy
-      uint64_t* const s64 = reinterpret_cast<uint64_t*>(es);
-      uint32_t pos = incl - scnt;
-      if constexpr (K == 8) {
-        // one update per lane per iteration (emit_updates_flat)
-        uint32_t seen = 0u, T = 0u, nz = 0u;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          T |= seen & E[j];
-          seen |= E[j];
-          nz |= (E[j] != 0u ? 1u : 0u) << j;
-        }
-        if (dense) nz = 0u;
-        uint32_t S = 0u, j = 0u, cur = 0u;
-        const uint64_t hi = ((uint64_t)p.round_rel << 52) | ((uint64_t)node << 28);
-        for (uint32_t r = 0; r < 64u; ++r) {
-          const bool more = r < scnt;
-          if (__ballot(more) == 0ull) break;
-          if (more) {
-            if (cur == 0u) {
-              j = (uint32_t)__ffs(nz) - 1u;
-              nz &= nz - 1u;
-              cur = E[0];
-#pragma unroll
-              for (int q = 1; q < K; ++q) cur = j == (uint32_t)q ? E[q] : cur;
-            }
-            const uint32_t bit = (uint32_t)__ffs(cur) - 1u;
-            cur &= cur - 1u;
-            const uint32_t m = 1u << bit;
-            const uint32_t a = ((A_final ^ (T & ~S)) >> bit) & 1u;
-            S |= m;
-            const uint32_t st = (died & m) ? (a ? 3u : 0u) : (a ? 2u : 1u);
-            s64[pos++] = hi | ((uint64_t)j << 24) | ((uint64_t)(tbase + bit) << 2) | st;
-          }
-        }
-      } else {
-        uint32_t par = 0;
-#pragma unroll
-        for (int j = K - 1; j >= 0; --j) {  // A after slot j = A_final ^ parity(later flips)
-          const uint32_t Aj = A_final ^ par;
-          par ^= E[j];
-          uint32_t e = dense ? 0u : E[j];
-          while (e) {
-            const uint32_t bit = (uint32_t)__ffs(e) - 1u;
-            e &= e - 1u;
-            const uint32_t a = (Aj >> bit) & 1u;
-            const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
-            s64[pos++] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
-          }
-        }
-      }
-      wave_lds_sync();
-      for (uint32_t i = lane; i < st_s; i += 64u) dst[i] = s64[i];
-      wave_lds_sync();
-    } else {
-      // more singles than the LDS area holds (dense_min raised past its
-      // default): each lane stores its own entries directly
-      uint32_t pos = incl - scnt;
-      uint32_t par = 0;
-#pragma unroll
-      for (int j = K - 1; j >= 0; --j) {
-        const uint32_t Aj = A_final ^ par;
-        par ^= E[j];
-        uint32_t e = dense ? 0u : E[j];
-        while (e) {
-          const uint32_t bit = (uint32_t)__ffs(e) - 1u;
-          e &= e - 1u;
-          const uint32_t a = (Aj >> bit) & 1u;
-          const uint32_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);
-          if (pos < st_s) dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
-          ++pos;
-        }
-      }
-    }
-  }
-  if (__ballot(ovf) != 0ull) note_overflow(p, lane);
-  // bytes actually stored (wave-uniform): entries past a full shard were dropped
-  return 8u * st_s + 8u * DW * st_d;
-}
-
 // The round step of one loaded tile. WARM: consider planes all-ones (neither
 // loaded nor stored; sim votes only). POL: plane-stream cache policy.
 // Reference-row flag of the node whose lanes include this one (kernels.h
@@ -407,10 +247,9 @@ __device__ __forceinline__ void ref_flag_store(const RoundParams& p, uint32_t la
   }
 }
 
-template <int K, bool REPLAY, bool WARM, int POL, bool VVM = false, bool LE = false, bool REF = false>
+template <int K, bool REPLAY, bool WARM, int POL, bool VVM = false, bool REF = false>
 __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
-                                             const TileIn<K, REPLAY, WARM>& in, uint32_t extra_bytes, SweepAcc& acc,
-                                             uint32_t* es) {
+                                             const TileIn<K, REPLAY, WARM>& in, uint32_t extra_bytes, SweepAcc& acc) {
   const LaneIdx x = lane_idx(p, tile, lane);
   const bool active = x.active;
   const uint32_t b = x.b, node = x.node;
@@ -667,16 +506,10 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
       acc.lane_bytes += 4u;
     }
   }
-  // LE (the fresh round, lighter on registers): log stores staged through LDS;
-  // in the warm modes the staging's registers spill (measured slower)
-  // medium records (p.med, k = 8): one contiguous entry per lane with updates, no LDS staging
+  // k = 8: single words, medium and dense records, one contiguous entry per lane (round_common.h)
   uint32_t emitted;
-  if (K == 8 && p.med)
+  if constexpr (K == 8)
     emitted = emit_updates_med<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, p.round_rel);
-  else if constexpr (LE)
-    emitted = emit_updates_lds<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, es);
-  else if constexpr (K == 8)
-    emitted = emit_updates_flat<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, p.round_rel);
   else
     emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates);
 
@@ -986,21 +819,15 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
 // the node's own row: timing diagnostics only, results invalid), kModeWarmPipe
 // (kModeWarm for a resident grid: the next tile's loads are issued before the
 // current tile is computed; 93 VGPRs, 5 waves per SIMD).
-// A/B build knobs (Makefile variant libraries): the warm modes' waves per SIMD and their StatusUpdate
-// emission (0: per-lane walk, emit_updates_flat; 1: staged through LDS, emit_updates_lds)
+// A/B build knob (Makefile variant libraries): the warm modes' waves per SIMD
 #ifndef AVK_WARM_WPE
 #define AVK_WARM_WPE 5
-#endif
-#ifndef AVK_WARM_LE
-#define AVK_WARM_LE 0
 #endif
 template <int K, int MODE, int POL, bool REF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeWarm ? AVK_WARM_WPE : MODE == kModeReplay || MODE == kModeFresh ? 6 : 7))) void k_round_sweep(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave0 = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * 4u;
-  __shared__ __attribute__((aligned(16))) uint32_t s_emit[4][kEmitWords];  // emit_updates_lds staging
-  uint32_t* const es = s_emit[threadIdx.x >> 6];
   const uint32_t tiles = p.Lpad >> 6;
   SweepAcc acc;
   // uniform rows (kernels.h): no rank's slot of pref_in carries this round's tag
@@ -1016,7 +843,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     for (; tile < tiles; tile += nwaves) {
       const uint32_t next = tile + nwaves;
       if (next < tiles) load_tile<K, false, true, POL, false, true>(p, next, lane, nxt);
-      process_tile<K, false, true, POL, true>(p, tile, lane, cur, 0u, acc, es);
+      process_tile<K, false, true, POL, true>(p, tile, lane, cur, 0u, acc);
       cur = nxt;
     }
   } else {
@@ -1041,6 +868,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         tile = wave0 * p.tpw;
         tile_end = min(tile + p.tpw, tiles);
         stride = 1u;
+        if (uniform && p.uni_merge > 1u && p.lean && p.settled_fast && p.klazy && p.vv &&
+            p.tpw * p.uni_merge <= kUniRun) {
+          // uniform input: most tiles settle with no draw, and what is left per wave is its set-up,
+          // so every uni_merge-th wave takes its neighbours' runs too and the others end here
+          if (wave0 % p.uni_merge) tile = tile_end = tiles;
+          else tile_end = min(tile + p.tpw * p.uni_merge, tiles);
+        }
         if (tile < tiles) {
           const uint32_t nlA = uni(div_bl(p, tile * 64u));
           const uint32_t nlB = uni(div_bl(p, min(tile_end * 64u, p.L) - 1u));
@@ -1124,15 +958,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         }
         TileIn<K, false, true> in;
         load_tile<K, false, true, POL, false, true>(p, tile, lane, in, &wd);
-        process_tile<K, false, true, POL, true, AVK_WARM_LE != 0, REF>(p, tile, lane, in, 0u, acc, es);
+        process_tile<K, false, true, POL, true, REF>(p, tile, lane, in, 0u, acc);
       } else if constexpr (MODE == kModeFresh) {
         TileIn<K, false, false> in;
         load_tile<K, false, false, POL, false, true, true>(p, tile, lane, in);
-        process_tile<K, false, false, POL, true, true>(p, tile, lane, in, 0u, acc, es);
+        process_tile<K, false, false, POL, true>(p, tile, lane, in, 0u, acc);
       } else if constexpr (MODE == kModeReplay) {
         TileIn<K, true, false> in;
         load_tile<K, true, false, POL, false>(p, tile, lane, in);
-        process_tile<K, true, false, POL>(p, tile, lane, in, 0u, acc, es);
+        process_tile<K, true, false, POL>(p, tile, lane, in, 0u, acc);
       } else {
         bool warm = false;
         if (p.warm_skip) {
@@ -1144,11 +978,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         if (warm) {
           TileIn<K, false, true> in;
           load_tile<K, false, true, POL, AB>(p, tile, lane, in);
-          process_tile<K, false, true, POL>(p, tile, lane, in, 4u, acc, es);
+          process_tile<K, false, true, POL>(p, tile, lane, in, 4u, acc);
         } else {
           TileIn<K, false, false> in;
           load_tile<K, false, false, POL, AB>(p, tile, lane, in);
-          process_tile<K, false, false, POL>(p, tile, lane, in, 0u, acc, es);
+          process_tile<K, false, false, POL>(p, tile, lane, in, 0u, acc);
         }
       }
     }

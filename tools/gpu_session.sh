@@ -145,8 +145,6 @@ for s in "$@"; do
     reftests) step reftests 900 python -u -m pytest tests/test_gpu_ref_rows.py tests/test_gpu_virtual_votes.py tests/test_gpu_fresh.py tests/test_gpu_count_lazy.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     fullc5) step fullc5 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread -k "c5" ;;
     dropintests) step dropintests 600 python -u -m pytest tests/test_gpu_dropin_fuzz.py tests/test_gpu_example.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    abvar) step abvar 900 bash -c 'for v in base w6 w4 le5 le4; do for w in c4 c4pb; do echo "== $v $w"; if [ $v = base ]; then python tools/round_probe.py --workload $w; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w; fi; done; done' ;;
-    abmed) step abmed 600 bash -c 'for w in c4 c4pb c3; do for o in emit_med=1 emit_med=0; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     abuni) step abuni 600 bash -c 'for w in c4 c5 c4p; do for o in uniform_rows=1 uniform_rows=0; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     unitests) step unitests 900 python -u -m pytest tests/test_gpu_uniform_rows.py tests/test_gpu_count_lazy.py tests/test_gpu_ref_rows.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     abtpw) step abtpw 600 bash -c 'for w in c4 c4p; do for o in tiles_per_wave=16 tiles_per_wave=8; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
@@ -154,6 +152,8 @@ for s in "$@"; do
     abhv) step abhv 600 bash -c 'for w in c4 c4pb c3; do for o in k_hi_virtual=1 k_hi_virtual=0; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     hvtests) step hvtests 900 python -u -m pytest tests/test_gpu_count_lazy.py tests/test_gpu_fresh.py tests/test_gpu_virtual_votes.py tests/test_gpu_uniform_rows.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     barrier) step barrier 300 bash -c 'python tools/barrier_cost.py --world 2 --json gpurun_out/barrier2.json && python tools/barrier_cost.py --world 4 --json gpurun_out/barrier4.json && python tools/barrier_cost.py --world 2 --nodes 131072 --json gpurun_out/barrier2_big.json' ;;
+    evidence) for S in abtpw abuni abhv; do bash "$0" $S || exit $?; done ;;
+    abmerge) step abmerge 600 bash -c 'for w in c4 c5 c4p; do for o in uni_merge=2 uni_merge=1 uni_merge=4; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     pmcall) for W in c4 c4pb c3; do WL=$W bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $?; done
             WL=c2 PMC_LAUNCHES=2 PMC_REPLAY=1 bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
