@@ -201,7 +201,11 @@ struct av_engine {
   uint32_t** push_tbl = nullptr;                     // device [3][kMaxPeers]: peers' replicas of each buffer
   uint32_t** arrive_tbl = nullptr;                   // device [world]: every rank's arrival array
   uint32_t* wave_done = nullptr;                     // device [2]: waves of the round counted (kernels.h)
-  bool fold_arrival = true;                          // option "fold_arrival": the sweep stores the arrival
+  // option "fold_arrival" (default off): the sweep's last wave stores the arrival. Every wave then
+  // counts itself on one device-wide counter, and those same-address atomics serialize: 2 ranks of
+  // C4 on one GPU ran 5.5 ms per round folded against 0.58 ms with the barrier kernel storing the
+  // arrival (profiles/r03/barrier2_c4_fold_arrival=*.json)
+  bool fold_arrival = false;
 
   // responder variant (option "responder", kernels.h pub_mode) and the nodes
   // that no longer poll (av_set_polling); both run the first-generation kernel
@@ -681,8 +685,10 @@ uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
   }
   // (by size: a run's nodes must fit the shared draw, 2 producer lanes each: 8 tiles need BL >= 16)
   // (a run's nodes must fit the run's peer draw: 2 producer lanes per node and round, 64 lanes; runs
-  // of 16 tiles at BL >= 32 draw both rounds in two passes, option tiles_per_wave = 16)
-  const uint64_t tpw = e->tiles_per_wave ? e->tiles_per_wave : (tiles >= (1u << 18) && e->BL >= 16 ? 8u : 4u);
+  // of 16 tiles at BL >= 32 draw both rounds in two passes: C4 epoch 5.14 -> 4.95 ms, the settled
+  // rounds 0.112 -> 0.088 ms, storm rounds +2 %, profiles/r03/ab_tiles_per_wave.log)
+  const uint64_t tpw = e->tiles_per_wave ? e->tiles_per_wave
+                                         : (tiles >= (1u << 18) ? (e->BL >= 32 ? 16u : e->BL >= 16 ? 8u : 4u) : 4u);
   const uint64_t waves = (tiles + tpw - 1) / tpw;
   return (uint32_t)std::max<uint64_t>(1, (waves + 3) / 4);
 }

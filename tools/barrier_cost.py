@@ -48,6 +48,9 @@ def _rank(args, world, rank, d, q):
         per = args.nodes // world
         e = avhip.Engine(args.nodes, args.targets, k=8, seed=3, node_range=(rank * per, (rank + 1) * per), device=0,
                          log_capacity=1 << 24)
+        for o in args.option:
+            name, v = o.split("=")
+            e.set_option(name, int(v))
         e.init_records(avhip.INIT_BERNOULLI, P80)
         with open(os.path.join(d, f"h{rank}.tmp"), "wb") as f:
             f.write(e.peer_handles())
@@ -73,6 +76,7 @@ def main():
     ap.add_argument("--targets", type=int, default=1000)
     ap.add_argument("--warm", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=100)
+    ap.add_argument("--option", action="append", default=[], help="name=value engine option for the rank engines")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
     import avhip
@@ -99,7 +103,7 @@ def main():
             p.join(timeout=10)
             if p.is_alive():
                 p.kill()
-    out = {"world": args.world, "nodes": args.nodes, "targets": args.targets, "rounds": args.rounds,
+    out = {"options": args.option, "world": args.world, "nodes": args.nodes, "targets": args.targets, "rounds": args.rounds,
            "single_engine": {"ms_per_round": base_ms, "kernel_ms_per_launch": base_kms}, "ranks": res}
     ok = [v for v in res.values() if "ms_per_round" in v]
     if len(ok) == args.world:
