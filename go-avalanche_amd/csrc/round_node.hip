@@ -478,8 +478,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   const uint32_t maxc = max(wmax[0], wmax[1]);
   const uint32_t J = maxc >= 120u ? 0u : (120u - maxc + (uint32_t)K - 1u) / (uint32_t)K;
   uint32_t done = R, applied = 0u, upd = 0u, emitted = 0u, pubs = 0u;
-  uint32_t w[K], cw[K];
+  // the replayed votes are prefetched two rounds ahead (w: this round, w1: the next one): a round's
+  // compute is shorter than a load's latency with two waves per SIMD
+  uint32_t w[K], cw[K], w1[K], cw1[K];
   replay_load<K>(p.replay, g, w, cw);
+  if (R > 1u) replay_load<K>(p.replay + p.replay_stride, g, w1, cw1);
   for (uint32_t r = 0; r < R; ++r) {
     if (r >= J) {  // a record with count >= 120 may finalize (and leave the poll set) this round
       const uint32_t nearfin = Kp[6] & Kp[5] & Kp[4] & Kp[3];
@@ -489,8 +492,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       }
     }
     uint32_t nw[K], ncw[K];
-    const bool more = r + 1u < R;
-    if (more) replay_load<K>(p.replay + (size_t)(r + 1u) * p.replay_stride, g, nw, ncw);
+    const bool more = r + 2u < R;
+    if (more) replay_load<K>(p.replay + (size_t)(r + 2u) * p.replay_stride, g, nw, ncw);
     uint32_t ys[7 + K], ns[7 + K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -526,11 +529,13 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       ++pubs;
     }
     emitted += emit_updates_flat<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, 0u, upd, p.round_rel + r);
-    if (more) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        w[j] = nw[j];
-        cw[j] = ncw[j];
+    for (int j = 0; j < K; ++j) {
+      w[j] = w1[j];
+      cw[j] = cw1[j];
+      if (more) {
+        w1[j] = nw[j];
+        cw1[j] = ncw[j];
       }
     }
   }
