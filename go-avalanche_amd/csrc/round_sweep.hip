@@ -819,9 +819,11 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
 // the node's own row: timing diagnostics only, results invalid), kModeWarmPipe
 // (kModeWarm for a resident grid: the next tile's loads are issued before the
 // current tile is computed; 93 VGPRs, 5 waves per SIMD).
-// A/B build knob (Makefile variant libraries): the warm modes' waves per SIMD
+// A/B build knob (Makefile variant libraries): the warm modes' waves per SIMD. 6 (80 VGPRs, 7
+// spilled to scratch in cold paths) beat 5 (87 VGPRs): C4p / C4pb epochs -4 %, C4 storm rounds -2 to
+// -3 %; 7 (54 spilled) ran storm rounds 1.7x slower (profiles/r03/ab_waves_per_simd.log)
 #ifndef AVK_WARM_WPE
-#define AVK_WARM_WPE 5
+#define AVK_WARM_WPE 6
 #endif
 template <int K, int MODE, int POL, bool REF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeWarm ? AVK_WARM_WPE : MODE == kModeReplay || MODE == kModeFresh ? 6 : 7))) void k_round_sweep(const RoundParams p) {
