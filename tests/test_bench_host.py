@@ -1,0 +1,84 @@
+"""bench.py's host logic (no GPU): round kinds of the C4 epoch, the binding
+resource, the roofline built from a roofline pass's per-round rows, the PMC
+summary gate (source digest + window) and the CPU-count rule."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+bench = pytest.importorskip("bench")
+
+
+def test_round_kinds_follow_the_count_bound():
+    # round 0 fresh, 1-3 storm, 4-15 klazy (no count can reach 120 before round 16: the first 6
+    # votes of a fresh record never step it), 16 on kconsume
+    kinds = [bench.round_kind(r, False) for r in range(17)]
+    assert kinds[0] == "fresh" and set(kinds[1:4]) == {"storm"}
+    assert set(kinds[4:16]) == {"klazy"} and kinds[16] == "kconsume"
+    assert bench.round_kind(3, True).startswith("replay")
+
+
+def test_binding_picks_the_resource_or_latency():
+    assert bench.binding({"fabric": 0.8, "valu_issue": 0.3, "salu_issue": 0.2, "wait_any": 0.6}) == "fabric"
+    assert bench.binding({"fabric": 0.3, "valu_issue": 0.41, "salu_issue": 0.3, "wait_any": 0.55}) == "latency"
+    assert bench.binding({"fabric": 0.3, "valu_issue": 0.41, "salu_issue": 0.3, "wait_any": 0.2}) == "valu_issue"
+    assert bench.binding({"fabric": None, "hbm_compulsory": 0.7, "valu_issue": None, "salu_issue": None}) == \
+        "hbm_compulsory"
+
+
+def _r(per_round, lanes=1000):
+    kern = sum(p["kernel_ms"] for p in per_round)
+    n = len(per_round)
+    moved = sum(p["model_bytes"] for p in per_round)
+    return {"wl": "c4", "kavg_ms": kern / n, "moved_bytes": moved / n,
+            "reread_bytes": sum(p["reread_bytes"] for p in per_round) / n, "kernel": "k", "launches": n,
+            "kernel_ms_total": kern, "steps": n, "elapsed": kern * 1e-3 * 1.01, "rounds_per_launch": 1.0,
+            "s8d_bytes": 9.125e9, "per_round": per_round, "replay": False, "lanes": lanes}
+
+
+def test_roofline_is_model_bytes_over_kernel_time():
+    rows = [{"round": r, "kernel_ms": 0.1 if r >= 4 else 1.0, "launches": 1,
+             "model_bytes": 8e8 if r >= 4 else 4e9, "reread_bytes": 0 if r >= 4 else 1e9} for r in range(6)]
+    r = _r(rows)
+    out = bench.roofline(r, window=None)
+    t = r["kavg_ms"] * 1e-3
+    assert out["frac"] == pytest.approx(r["moved_bytes"] / t / 1e9 / bench.HBM_PEAK_GBS)
+    assert out["frac"] <= 1.0 and out["traffic"] is None
+    kinds = out["round_kinds"]
+    assert kinds["klazy"]["rounds"] == [4, 5] and kinds["storm"]["rounds"] == [1, 2, 3]
+    # 8e8 B in 0.1 ms = 8 TB/s: the klazy rows sit exactly at the peak
+    assert kinds["klazy"]["fracs"]["model"] == pytest.approx(1.0)
+    assert kinds["storm"]["fracs"]["hbm_compulsory"] == pytest.approx(3e9 / 1e-3 / 1e9 / bench.HBM_PEAK_GBS)
+    assert out["host_gap_ms_per_step"] > 0
+
+
+def test_pmc_summary_used_only_when_digest_and_window_match(tmp_path, monkeypatch):
+    monkeypatch.setattr(bench, "PMC_DIR", str(tmp_path))
+    good = {"src_sha": bench.src_digest(), "window": "5+20", "fabric_bytes_per_launch": 1.0}
+    (tmp_path / "pmc_c4.json").write_text(json.dumps(good))
+    assert bench.load_pmc("c4", "5+20", 1)["fabric_bytes_per_launch"] == 1.0
+    assert bench.load_pmc("c4", "0+5", 1) is None      # another window
+    assert bench.load_pmc("c4", "5+20", 2) is None     # multi-rank lines carry no single-GPU PMC
+    (tmp_path / "pmc_c4.json").write_text(json.dumps(dict(good, src_sha="0" * 16)))
+    assert bench.load_pmc("c4", "5+20", 1) is None     # other kernel sources
+
+
+def test_committed_pmc_summaries_are_well_formed():
+    d = os.path.join(ROOT, "profiles", "r03")
+    files = [f for f in os.listdir(d) if f.startswith("pmc_") and f.endswith(".json")] if os.path.isdir(d) else []
+    for f in files:
+        pm = json.load(open(os.path.join(d, f)))
+        assert pm["window"] == "5+20" and len(pm["src_sha"]) == 16
+        assert pm["fabric_bytes_per_launch"] > 0 and 0 < pm["issue"]["frac_valu"] < 1
+        assert all(src.startswith("profiles/r03/") for src in pm["source"].values())
+
+
+def test_cpu_baseline_threads_respect_the_quota():
+    hc = bench.host_cpus()
+    assert 1 <= hc["threads"] <= hc["affinity_cpus"]
+    if hc["cgroup_cpu_quota"]:
+        assert hc["threads"] <= max(1, round(hc["cgroup_cpu_quota"]))
