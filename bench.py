@@ -1,8 +1,12 @@
 #!/usr/bin/env python3
 """Throughput bench of the batched Avalanche vote-record update path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3|c5|c4p|c4pb]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+`python bench.py --gpus N` (N > 1) with no launcher around it starts its own N
+rank processes: a fresh `python -m torch.distributed.run` child (before any GPU
+call), whose rank 0 prints the line; the exit status is the child's.
 
 One *step* = one synchronous round of go-avalanche's poll loop for every
 simulated node: k peers sampled per node, k Responses
@@ -44,6 +48,8 @@ import argparse
 import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -97,7 +103,7 @@ class BenchFailure(SystemExit):
     pass
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -118,7 +124,32 @@ def parse():
                          "barrier/reductions (not a measurement)")
     ap.add_argument("--no-roofline-pass", action="store_true",
                     help="skip the HIP-event pass (rocprofv3 PMC runs: one window only)")
-    return ap.parse_args()
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="where the full per-round / per-workload detail goes (the line stays compact)")
+    return ap.parse_args(argv)
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_launch_cmd(argv, gpus, port):
+    """The command that runs this bench as `gpus` rank processes of one node
+    (torch.distributed.run, rendezvous on 127.0.0.1), with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(argv, gpus):
+    """`bench.py --gpus N` started without a launcher (WORLD_SIZE unset): run
+    the N ranks as ONE fresh child process (never exec: nothing here has
+    touched the GPU, and this process only waits), pass its output through and
+    return its exit status."""
+    cmd = rank_launch_cmd(argv, gpus, free_port())
+    print("bench: launching " + " ".join(cmd[1:7]) + f" ... ({gpus} ranks)", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
 
 
 def src_digest():
@@ -187,6 +218,7 @@ def cpu_baseline(wl, seed, budget_s):
     sim.close()
     return {"value": applied / dt, "unit": "vote-record updates/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus": hc,
+            "sample_short": f"oracle C restatement, {ns} x {m}, rounds 0..{rounds - 1}, {dt:.1f}s, {threads} threads",
             "sample": f"oracle/avalanche_oracle.c (C restatement of vote.go/processor.go, the parity oracle), "
                       f"{ns} nodes x {m} targets, k={k}, rounds 0..{rounds - 1} ({applied} regsiterVote "
                       f"applications, {dt:.1f}s, OpenMP over nodes, {threads} threads on {cpu_model()})"}
@@ -238,6 +270,8 @@ class Runner:
                 eng.close()
                 self.fallback = next(e for e in errs if e)
         self.info = eng.layout_info() if self.fallback is None else None
+        # tests (test_gpu_bench_protocol.py): called after every segment, before the log is emptied
+        self.on_segment = None
 
     def close(self):
         self.eng.close()
@@ -295,6 +329,8 @@ class Runner:
             if eng.log_overflowed():
                 raise BenchFailure(f"bench: StatusUpdate log overflowed in {self.wl} steps "
                                    f"{self.pos}..{self.pos + seg - 1}: updates were not stored; no number reported")
+            if self.on_segment is not None:
+                self.on_segment(self, self.pos, seg)
             emitted += eng.updates_count()
             applied += eng.applied_votes() - a0
             self.pos += seg
@@ -315,7 +351,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
     # the log holds every StatusUpdate of one timed segment (up to 16 rounds:
     # C4 ~2e8 in rounds 0-2, the conflicting C4p/C4pb ~1e9 over rounds 0-8);
-    # 16 B of device memory per entry (singles + dense records): 20 GB at 1M x 1000
+    # 24 B of device memory per entry at k = 8 (singles 8, medium records 8, dense
+    # records 8 B of capacity per update): 30 GB at 1M x 1000
     log_cap = min(int(1.25 * n * m) + (1 << 20), (1 << 31) - 1)
     run = Runner(wl, args, world, rank, local_rank, log_cap)
     if run.fallback is not None:
@@ -330,6 +367,15 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     # ---- warmup steps (untimed), then the timed steps
     run.goto(warmup)
     elapsed, applied, emitted, segs = run.steps(steps, timed=True)
+    # ---- the deferred state the timed rounds leave behind (pending count steps, stale vote
+    # planes) written back and timed on its own: outside the window, reported beside it
+    writeback_ms = None
+    if not replay:
+        eng.set_timing(True)
+        eng.materialize()
+        ms, nl = eng.kernel_stats()
+        eng.set_timing(False)
+        writeback_ms = ms if nl else 0.0
 
     # ---- roofline pass: the same steps again, every round's kernels bracketed
     # by HIP events on the engine's stream; sim rounds one step at a time so
@@ -364,6 +410,20 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         eng.set_timing(False)
         if applied2 != applied:
             raise BenchFailure(f"bench: roofline pass applied {applied2} votes, the timed pass {applied}")
+    # ---- exchange pass (one GPU, sim workloads): the same steps again with the changed published
+    # words counted per round (option count_changed), the input of the multi-GPU push model
+    changed = None
+    if world == 1 and not replay and not args.no_roofline_pass:
+        run.goto(warmup)
+        eng.set_option("count_changed", 1)
+        changed = []
+        for _ in range(steps):
+            rnd = run.pos % EPOCH
+            w0, g0 = eng.changed_words()
+            run.steps(1, timed=False)
+            w1, g1 = eng.changed_words()
+            changed.append({"round": rnd, "words": w1 - w0, "segments": g1 - g0})
+        eng.set_option("count_changed", 0)
     replicas = None
     if world > 1 and args.shard in ("peers", "nodes"):
         # every rank's replica of the published preferences must be the same:
@@ -413,6 +473,7 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         "lanes": info["lanes"] if info else None,
         "rounds_per_launch": steps / launches if launches else None,
         "first_round": warmup % EPOCH,
+        "writeback_ms": writeback_ms, "changed": changed,
     }
 
 
@@ -562,8 +623,48 @@ def roofline(r, window=None, world=1):
     return out
 
 
-def main():
-    args = parse()
+# xGMI between two MI355X of one node: 7 links per GPU, one per peer, ~153.6 GB/s per link both
+# directions together (MI355X_MICROARCH.md / the platform figure): 76.8 GB/s per direction
+XGMI_LINK_GBS = 76.8
+
+
+def exchange_model(changed, n, ps, ranks=(2, 4, 8)):
+    """The peer-push exchange at G ranks from the one-GPU exchange pass: rank r owns
+    1/G of the nodes, so it changes ~1/G of the round's published words and stores each changed
+    64-B row segment into each of its G - 1 peers' replicas, one peer per xGMI link (all links
+    busy at once): per-link bytes per round = segments / G * 64 B. Beside it the all-gather of
+    every rank's rows (what `--shard nodes` does with RCCL): (N / G) * row bytes per link."""
+    if not changed:
+        return None
+    out = {"link_GBs_per_direction": XGMI_LINK_GBS, "rounds": [c["round"] for c in changed],
+           "changed_words": [c["words"] for c in changed], "changed_segments": [c["segments"] for c in changed]}
+    for g in ranks:
+        push = [c["segments"] / g * 64.0 / (XGMI_LINK_GBS * 1e9) * 1e3 for c in changed]
+        out[f"g{g}"] = {"push_ms_per_round_mean": sum(push) / len(push), "push_ms_per_round_max": max(push),
+                        "push_bytes_per_link_max": max(c["segments"] for c in changed) / g * 64.0,
+                        "allgather_ms_per_round": n / g * ps * 4.0 / (XGMI_LINK_GBS * 1e9) * 1e3}
+    return out
+
+
+def compact_roofline(rf):
+    """The line's roofline: the contract's keys, the kernel and its launches, the binding resource and
+    per round kind (ms per launch, frac, binding). Everything else: the detail file."""
+    if rf is None:
+        return None
+    keep = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms_avg", "launches",
+            "frac_hbm_compulsory", "frac_s8d", "binding")
+    out = {k: rf[k] for k in keep if k in rf}
+    out["kinds"] = {name: {"ms": kd["kernel_ms_avg"], "frac": kd["fracs"]["model"], "binding": kd["binding"]}
+                    for name, kd in rf.get("round_kinds", {}).items()}
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: start the ranks as one fresh child process and wait
+        sys.exit(launch_ranks(argv, args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -579,6 +680,8 @@ def main():
     elif world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
+    window = f"{args.warmup}+{args.steps}"
+    detail = {"window": window, "n_gpus": world, "workloads": {}}
     try:
         r = measure(args.workload, args, world, rank, local_rank, args.steps, args.warmup)
         secondary = {}
@@ -591,25 +694,32 @@ def main():
                     secondary["xgmi_allgather"] = allgather_probe(world, local_rank)
                 except Exception as exc:
                     secondary["xgmi_allgather"] = {"error": repr(exc)[:200]}
-            others = ["c4p", "c4pb", "c3"] + (["c2"] if world == 1 else [])
+            others = ["c4p", "c4pb", "c3", "c5"] + (["c2"] if world == 1 else [])
             for wl in others:
                 if wl == args.workload:
                     continue
-                s = measure(wl, args, world, rank, local_rank, args.steps, args.warmup)
-                secondary[wl] = {"workload": s["desc"], "value": s["value"], "unit": "vote-record updates/s",
-                                 "ms_per_step": s["elapsed"] / args.steps * 1e3, "updates_emitted": int(s["emitted"]),
-                                 "rounds": f"steps {args.warmup}..{args.warmup + args.steps - 1} of 16-round epochs",
-                                 "roofline": roofline(s, f"{args.warmup}+{args.steps}", world)}
+                sr = measure(wl, args, world, rank, local_rank, args.steps, args.warmup)
+                rf = roofline(sr, window, world)
+                secondary[wl] = {"value": sr["value"], "ms_per_step": sr["elapsed"] / args.steps * 1e3,
+                                 "frac": rf["frac"] if rf else None, "binding": rf.get("binding") if rf else None}
+                if sr["writeback_ms"] is not None:
+                    secondary[wl]["writeback_ms"] = sr["writeback_ms"]
                 if world > 1:
-                    secondary[wl]["replicas_identical"] = s["replicas_identical"]
+                    secondary[wl]["replicas_identical"] = sr["replicas_identical"]
+                detail["workloads"][wl] = {"workload": sr["desc"], "value": sr["value"],
+                                           "ms_per_step": sr["elapsed"] / args.steps * 1e3,
+                                           "updates_emitted": int(sr["emitted"]), "roofline": rf,
+                                           "per_round": sr["per_round"], "writeback_ms": sr["writeback_ms"],
+                                           "exchange_model": exchange_model(sr["changed"], sr["n"],
+                                                                            avhip_pref_stride(sr))}
     except BenchFailure as ex:
         if rank == 0:
             print(str(ex), file=sys.stderr, flush=True)
         raise SystemExit(3)
 
     if rank == 0:
-        window = f"{args.warmup}+{args.steps}"
         first = r["first_round"]
+        rf = roofline(r, window, world)
         line = {
             "metric": "vote-record updates/sec (node·target·round) at 1/2/4/8 GPU; % HBM roofline",
             "value": r["value"],
@@ -626,17 +736,14 @@ def main():
             "config": {
                 "workload": r["desc"],
                 "n_nodes": r["n"], "n_targets": r["m"], "k": r["k"],
-                "rounds": f"steps {args.warmup}..{args.warmup + args.steps - 1} = round (step % 16) of 16-round "
-                          f"epochs (all records live; records re-initialised untimed at each epoch start); "
-                          f"timed rounds start at round {first}, {r['segments']} timed segment(s)",
+                "rounds": f"step p = round p % 16 of a fresh network (all records live), timed from round {first}, "
+                          f"{r['segments']} segment(s)",
                 "parallelism": (PARALLELISM[args.shard] + f" x{world}") if world > 1 else "single GPU",
-                "layout": "bit-sliced: 25 u32 planes per 32 records; tile of 64 lanes contiguous",
-                "capped_poll_path": r["info"]["capped"],
             },
-            "triples_per_s": r["value"] / r["k"],
             "updates_emitted": int(r["emitted"]),
-            "update_log_overflow": False,
-            "roofline": roofline(r, window, world),
+            "roofline": compact_roofline(rf),
+            "writeback_ms": r["writeback_ms"],
+            "detail": os.path.relpath(args.detail, ROOT),
         }
         if r["replicas_identical"] is not None:
             line["config"]["replicas_identical"] = r["replicas_identical"]
@@ -644,12 +751,30 @@ def main():
             line["config"]["shard_fallback"] = "peer exchange unavailable: " + args.shard_fallback
         if secondary:
             line["secondary"] = secondary
+        detail["workloads"][args.workload] = {"workload": r["desc"], "value": r["value"],
+                                              "ms_per_step": r["elapsed"] / args.steps * 1e3,
+                                              "updates_emitted": int(r["emitted"]), "roofline": rf,
+                                              "per_round": r["per_round"], "writeback_ms": r["writeback_ms"],
+                                              "exchange_model": exchange_model(r["changed"], r["n"],
+                                                                               avhip_pref_stride(r))}
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(args.workload, args.seed, args.cpu_seconds)
+            cb = cpu_baseline(args.workload, args.seed, args.cpu_seconds)
+            detail["cpu_baseline"] = cb
+            line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind")}
+            line["cpu_baseline"]["sample"] = cb["sample_short"]
+        os.makedirs(os.path.dirname(os.path.abspath(args.detail)), exist_ok=True)
+        with open(args.detail, "w") as f:
+            json.dump(detail, f, indent=1)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def avhip_pref_stride(r):
+    """Words per preference row (kernels.h pref_stride) of a measured workload."""
+    bl = r["info"]["local_blocks"] if r["info"] else (r["m"] + 31) // 32
+    return bl if bl <= 1 else ((bl + 31) // 32 * 32 if bl > 32 else 1 << (bl - 1).bit_length())
 
 
 if __name__ == "__main__":

@@ -199,13 +199,18 @@ struct av_engine {
   std::vector<void*> peer_opened;                    // IPC mappings to close
   avk::PeerPtrs peer_arrive{};
   uint32_t** push_tbl = nullptr;                     // device [3][kMaxPeers]: peers' replicas of each buffer
-  uint32_t** arrive_tbl = nullptr;                   // device [world]: every rank's arrival array
-  uint32_t* wave_done = nullptr;                     // device [2]: waves of the round counted (kernels.h)
-  // option "fold_arrival" (default off): the sweep's last wave stores the arrival. Every wave then
-  // counts itself on one device-wide counter, and those same-address atomics serialize: 2 ranks of
-  // C4 on one GPU ran 5.5 ms per round folded against 0.58 ms with the barrier kernel storing the
-  // arrival (profiles/r03/barrier2_c4_fold_arrival=*.json)
-  bool fold_arrival = false;
+  uint64_t barrier_ticks = 0;                        // barrier_timeout_ms in wall-clock ticks (peer_timeout_ticks)
+  // diagnostics option "solo_barrier": a one-rank barrier (the same 1-wave kernel, world 1) after every
+  // round of an engine without a peer exchange — the exchange's fixed cost per round without the
+  // pushes and without other ranks (tools/exchange_cost.py)
+  bool solo_barrier = false;
+  // changed published words (kernels.h RoundParams::changed): counted in every peer-push round and,
+  // with option "count_changed", in every sweep round
+  unsigned long long* changed = nullptr;
+  bool count_changed = false;
+  // the reference-row flag bytes of every buffer were cleared (or the engine created) at this round;
+  // a flag byte carries a 7-bit round tag, so they are cleared again before 128 rounds have passed
+  int64_t rflag_clear_round = 0;
 
   // responder variant (option "responder", kernels.h pub_mode) and the nodes
   // that no longer poll (av_set_polling); both run the first-generation kernel
@@ -382,8 +387,9 @@ int push_own_rows(av_engine* e, int b) {
 
 // Barrier across the peer ranks, on the engine stream (kernels.h).
 int peer_barrier(av_engine* e) {
-  AV_HIP(avk::launch_peer_barrier(e->peer_arrive, (uint32_t)e->peer_world, (uint32_t)e->peer_rank,
-                                  ++e->barrier_seq, e->barrier_err, e->barrier_timeout_ms, e->stream));
+  if (!e->barrier_ticks) AV_HIP(avk::peer_timeout_ticks(e->cfg.device, e->barrier_timeout_ms, &e->barrier_ticks));
+  AV_HIP(avk::launch_peer_barrier(e->peer_arrive, (uint32_t)std::max(1, e->peer_world), (uint32_t)e->peer_rank,
+                                  ++e->barrier_seq, e->barrier_err, e->barrier_ticks, e->stream));
   return AV_OK;
 }
 
@@ -511,14 +517,9 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   if (peer && sweep && !replay) {
     p.push_n = (uint32_t)e->peer_world - 1u;
     p.push_dst = e->push_tbl + (size_t)nb * avk::kMaxPeers;
-    if (e->fold_arrival) {  // the round kernel's last wave stores this rank's arrival
-      p.arrive_dst = e->arrive_tbl;
-      p.arrive_n = (uint32_t)e->peer_world;
-      p.arrive_rank = (uint32_t)e->peer_rank;
-      p.arrive_seq = ++e->barrier_seq;
-      p.wave_done = e->wave_done;
-    }
   }
+  p.count_changed = (p.push_n || e->count_changed) && sweep && !replay ? 1u : 0u;
+  p.changed = e->changed;
   // reference rows: sweep rounds at k = 8 with a node's lanes inside one wave
   bool refr = e->ref_rows && sweep && e->k == 8 && !replay && 64 % e->BL == 0 && !e->comm && !e->ablate_gather;
   if (refr) {
@@ -526,11 +527,13 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     if (rc != AV_OK) return rc;
     refr = e->ref_node >= 0;
   }
-  if (refr && ((e->round + 1) & 127) == 0) {
-    // flag bytes carry a 7-bit snapshot tag (round_sweep.hip ref_tag): clear every buffer's flags
-    // every 128 rounds so that no byte outlives its tag's period
+  if (refr && e->round - e->rflag_clear_round >= 120) {
+    // flag bytes carry a 7-bit snapshot tag (round_sweep.hip ref_tag): every buffer's flags are
+    // cleared before 128 rounds have passed since the last clear, whatever kind of round ran in
+    // between (replay, capped, non-refr), so no byte outlives its tag's period
     for (int b = 0; b < 3; ++b)
       AV_HIP(hipMemsetAsync(reinterpret_cast<uint8_t*>(e->pref[b]) + e->rflag_off, 0, (size_t)e->N, e->stream));
+    e->rflag_clear_round = e->round;
     ref_invalidate(e);
   }
   if (refr) {
@@ -601,13 +604,11 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
       int rc = push_own_rows(e, nb);
       if (rc != AV_OK) return rc;
     }
-    if (p.arrive_n) {  // the arrival was stored by the round kernel: wait only
-      AV_HIP(avk::launch_peer_wait(e->peer_arrive, (uint32_t)e->peer_world, (uint32_t)e->peer_rank, p.arrive_seq,
-                                   e->barrier_err, e->barrier_timeout_ms, e->stream));
-    } else {
-      int rc = peer_barrier(e);
-      if (rc != AV_OK) return rc;
-    }
+    int rc = peer_barrier(e);
+    if (rc != AV_OK) return rc;
+  } else if (e->solo_barrier) {
+    int rc = peer_barrier(e);
+    if (rc != AV_OK) return rc;
   }
   if (e->comm) {
     const size_t count = (size_t)e->NL * e->PS;
@@ -694,6 +695,27 @@ uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
 }
 
 
+// The arrival slots of the peer barrier (one per rank, fine-grained when peers store into them over
+// xGMI) and the barrier's timeout flag in pinned host memory (the barrier kernel stores it with
+// system scope, so the host sees it without synchronizing the stream; av_run_rounds refuses to
+// enqueue once it is set). Zeroed before any peer can see them: the exchange of handles orders the two.
+int alloc_arrival(av_engine* e) {
+  if (e->peer_fine)
+    AV_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&e->arrive), (size_t)(2u << 20), hipDeviceMallocFinegrained));
+  else
+    AV_HIP(dev_alloc(&e->arrive, (size_t)(2u << 20) / 4));
+  void* hp = nullptr;
+  AV_HIP(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  e->barrier_err_host = static_cast<volatile uint32_t*>(hp);
+  *e->barrier_err_host = 0u;
+  void* dp = nullptr;
+  AV_HIP(hipHostGetDevicePointer(&dp, hp, 0));
+  e->barrier_err = static_cast<uint32_t*>(dp);
+  AV_HIP(hipMemset(e->arrive, 0, (size_t)(avk::kMaxPeers + 1) * 4));
+  AV_HIP(hipDeviceSynchronize());
+  return AV_OK;
+}
+
 int refresh_pref(av_engine* e) {
   ref_invalidate(e);
   AV_HIP(avk::launch_refresh_pref((uint32_t)e->pub_mode, e->planes, e->pref[e->cur], e->byz, (uint32_t)e->n0, e->NL,
@@ -747,8 +769,7 @@ int av_destroy(av_engine* e) {
   if (e->dropin_host) (void)hipHostFree(e->dropin_host);
   if (e->digest) (void)hipFree(e->digest);
   if (e->push_tbl) (void)hipFree(e->push_tbl);
-  if (e->arrive_tbl) (void)hipFree(e->arrive_tbl);
-  if (e->wave_done) (void)hipFree(e->wave_done);
+  if (e->changed) (void)hipFree(e->changed);
   if (e->marker) (void)hipEventDestroy(e->marker);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->kpend, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->readd, e->died_out, e->nopoll,
@@ -848,8 +869,10 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->dlog, (size_t)e->dlog_cap * e->log_shards * dw)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->dlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->upd_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
-  // a medium record holds >= 2 updates: log_cap / 2 records per shard
-  e->mlog_cap = std::max<uint32_t>(e->log_cap / 2, 16);
+  // a medium record holds >= 2 updates: log_cap / 2 records per shard (16 B each: 8 B of capacity per
+  // update, as the singles). Only the sweep kernel at k = 8 emits them (round_common.h
+  // emit_updates_med): other engines keep a token 16 records per shard.
+  e->mlog_cap = e->k == 8 && !e->capped ? std::max<uint32_t>(e->log_cap / 2, 16) : 16u;
   if ((he = dev_alloc(&e->mlog, (size_t)e->mlog_cap * e->log_shards * 2)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->mlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   (void)hipMemsetAsync(e->mlog_count, 0, avk::kLogShards * 4, e->stream);
@@ -868,6 +891,8 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->finalized, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
   (void)hipMemsetAsync(e->finalized, 0, avk::kLogShards * 8, e->stream);
   if ((he = dev_alloc(&e->scratch_count, 1)) != hipSuccess) return hip_fail(he, "alloc counters");
+  if ((he = dev_alloc(&e->changed, 2 * avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
+  (void)hipMemsetAsync(e->changed, 0, 2 * avk::kLogShards * 8, e->stream);
 
   (void)hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
@@ -934,6 +959,15 @@ int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
   p.pub_mode = (uint32_t)e->pub_mode;
   p.param = init_param;
   AV_HIP(avk::launch_init(p, e->stream));
+  if (e->peer_world > 1) {
+    // peer-push engine: this rank's new rows of the current snapshot go to every peer replica, and
+    // no rank's next round may read them before all ranks have pushed (collective: every rank
+    // re-initialises). The other two buffers are untouched, so their replicas stay identical.
+    int rc = push_own_rows(e, e->cur);
+    if (rc != AV_OK) return rc;
+    rc = peer_barrier(e);
+    if (rc != AV_OK) return rc;
+  }
   e->fresh = init_mode != AV_INIT_NONE;
   // lanes of the padded tail of the last tile hold no records
   if (e->Lpad > e->L) {
@@ -1762,6 +1796,33 @@ int av_alg_bytes(av_engine* e, int64_t* out) { return sum_byte_counters(e, 0, ou
 
 int av_alg_bytes_reread(av_engine* e, int64_t* out) { return sum_byte_counters(e, avk::kLogShards, out); }
 
+int av_changed_words(av_engine* e, int64_t* words, int64_t* segments) {
+  AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
+  AV_CHECK(words, AV_ERR_INVALID_ARG, "null argument");
+  int rc = sum_counter(e, e->changed, words);
+  if (rc != AV_OK || !segments) return rc;
+  return sum_counter(e, e->changed + avk::kLogShards, segments);
+}
+
+int av_materialize(av_engine* e) {
+  AV_ENTER(e);
+  AV_PEER_CHECK(e);
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (e->timing && (e->v_stale || e->k_pend)) {
+    AV_HIP(hipEventCreate(&ev0));
+    AV_HIP(hipEventCreate(&ev1));
+    AV_HIP(hipEventRecord(ev0, e->stream));
+  }
+  int rc = materialize_votes(e);
+  if (rc != AV_OK) return rc;
+  if (ev0) {
+    AV_HIP(hipEventRecord(ev1, e->stream));
+    e->events.emplace_back(ev0, ev1);
+  }
+  return AV_OK;
+}
+
 int av_read_pref(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint8_t* out) {
   AV_ENTER(e);
   AV_PEER_SYNC_CHECK(e);
@@ -1856,8 +1917,17 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->settled_fast = value != 0;
   } else if (n == "replay_fast") {
     e->replay_fast = value != 0;
-  } else if (n == "fold_arrival") {  // 0: the separate barrier kernel stores the arrival too (A/B)
-    e->fold_arrival = value != 0;
+  } else if (n == "count_changed") {  // diagnostics: count changed published words in every sweep round
+    e->count_changed = value != 0;
+  } else if (n == "solo_barrier") {  // diagnostics: a one-rank barrier after every round (exchange_cost.py)
+    AV_CHECK(e->peer_world <= 1 && !e->comm, AV_ERR_UNSUPPORTED, "solo_barrier: engine has an exchange");
+    if (value && !e->arrive) {
+      AV_ENTER(e);
+      int rc = alloc_arrival(e);
+      if (rc != AV_OK) return rc;
+      e->peer_arrive.p[0] = e->arrive;
+    }
+    e->solo_barrier = value != 0;
   } else if (n == "dropin_fast") {
     e->dropin_fast = value != 0;
   } else if (n == "settled_lean") {
@@ -1914,6 +1984,7 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   } else if (n == "barrier_timeout_ms") {
     AV_CHECK(value >= 1 && value <= 3600000, AV_ERR_INVALID_ARG, "bad barrier_timeout_ms");
     e->barrier_timeout_ms = (uint32_t)value;
+    e->barrier_ticks = 0;  // recomputed at the next barrier
   } else if (n == "warm_skip") {  // may only be switched off (it is a proven invariant, not a hint)
     if (!value) e->c_monotone = false;
   } else {
@@ -1993,6 +2064,7 @@ int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]) {
   AV_ENTER(e);
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
   static_assert(sizeof(hipIpcMemHandle_t) * 4 + 64 == AV_PEER_HANDLE_BYTES, "peer handle blob size");
+  AV_CHECK(!e->solo_barrier, AV_ERR_UNSUPPORTED, "diagnostics option solo_barrier is set");
   if (!e->arrive) {  // zeroed before any peer can see it: the exchange of handles orders the two
     // Snapshot buffers that peers store into over xGMI are fine-grained: this
     // device's L2 keeps such lines only within a kernel (the system-scope
@@ -2011,22 +2083,9 @@ int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]) {
         AV_HIP(hipFree(e->pref[b]));
         e->pref[b] = fine;
       }
-      AV_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&e->arrive), (size_t)(2u << 20),
-                                   hipDeviceMallocFinegrained));
-    } else {
-      AV_HIP(dev_alloc(&e->arrive, (size_t)(2u << 20) / 4));
     }
-    // the timeout flag lives in pinned host memory: the host sees it without
-    // synchronizing the stream (av_run_rounds refuses to enqueue once it is set)
-    void* hp = nullptr;
-    AV_HIP(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
-    e->barrier_err_host = static_cast<volatile uint32_t*>(hp);
-    *e->barrier_err_host = 0u;
-    void* dp = nullptr;
-    AV_HIP(hipHostGetDevicePointer(&dp, hp, 0));
-    e->barrier_err = static_cast<uint32_t*>(dp);
-    AV_HIP(hipMemset(e->arrive, 0, (size_t)(avk::kMaxPeers + 1) * 4));
-    AV_HIP(hipDeviceSynchronize());
+    int rc = alloc_arrival(e);
+    if (rc != AV_OK) return rc;
   }
   void* bufs[4] = {e->pref[0], e->pref[1], e->pref[2], e->arrive};
   for (int i = 0; i < 4; ++i) {
@@ -2091,12 +2150,6 @@ int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handl
     }
     AV_HIP(dev_alloc(&e->push_tbl, (size_t)3 * avk::kMaxPeers));
     AV_HIP(hipMemcpy(e->push_tbl, tbl, sizeof(tbl), hipMemcpyHostToDevice));
-    uint32_t* arr[avk::kMaxPeers + 1] = {};
-    for (int r = 0; r < world; ++r) arr[r] = e->peer_arrive.p[r];
-    AV_HIP(dev_alloc(&e->arrive_tbl, (size_t)avk::kMaxPeers + 1));
-    AV_HIP(hipMemcpy(e->arrive_tbl, arr, sizeof(arr), hipMemcpyHostToDevice));
-    AV_HIP(dev_alloc(&e->wave_done, 2));
-    AV_HIP(hipMemset(e->wave_done, 0, 8));
   }
   e->peer_world = world;
   e->peer_rank = rank;

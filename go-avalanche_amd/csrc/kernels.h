@@ -134,13 +134,14 @@ struct RoundParams {
   // device table, read only by lanes that push).
   uint32_t push_n;
   uint32_t* const* push_dst;
-  // Arrival folded into the round (k_round_sweep's last wave; launch_peer_wait then only waits):
-  // every wave counts itself in wave_done[arrive_seq & 1] once its stores (the pushes included) are
-  // acknowledged; the last one stores arrive_seq into slot arrive_rank of every rank's arrival array
-  // (arrive_dst[i], system scope) and resets the other counter. arrive_n = 0: no fold.
-  uint32_t* const* arrive_dst;
-  uint32_t arrive_n, arrive_rank, arrive_seq;
-  uint32_t* wave_done;
+  // Changed published words (engine option "count_changed"; always counted in a peer-push round): a
+  // lane whose published word differs from the word it overwrites in pref_out (= what every peer
+  // replica holds) counts one in changed[shard] — the words a peer-push round sends to each peer
+  // 
+  // (and [kLogShards + shard]: the 16-lane groups of a wave holding a changed word = 64-B row segments
+  // when a wave's lanes are contiguous row words, PS == BL a multiple of 16; per-wave 16-bit sums)
+  uint32_t count_changed;
+  unsigned long long* changed;  // [2 kLogShards]
   // Deferred count planes (`kl`, k = 8, warm sim rounds in which no record can
   // finalize): a tile all of whose polled records agreed with
   // their accepted bit on all 8 votes gains exactly +8 on every polled count
@@ -294,12 +295,11 @@ hipError_t launch_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, u
 // Barrier across the ranks of a node-sharded network: lane i writes `seq`
 // into slot `rank` of rank i's arrival array (arrive[i], system scope), then
 // waits until every slot of its own array (arrive[rank]) has reached `seq`.
-// Gives up after ~timeout_ms and sets *err (later barriers then return at once).
+// Gives up after timeout_ticks of the wall clock and sets *err (later barriers then return at once).
 hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
-                               uint32_t timeout_ms, hipStream_t s);
-// The waiting half alone (the round kernel stored this rank's arrival: RoundParams::arrive_*).
-hipError_t launch_peer_wait(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
-                            uint32_t timeout_ms, hipStream_t s);
+                               uint64_t timeout_ticks, hipStream_t s);
+// Wall-clock ticks of a timeout (the device's wall clock rate; queried once per engine).
+hipError_t peer_timeout_ticks(int device, uint32_t timeout_ms, uint64_t* ticks);
 
 struct InitParams {
   uint32_t* planes;

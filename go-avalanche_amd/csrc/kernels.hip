@@ -909,14 +909,13 @@ __global__ __launch_bounds__(256) void k_push_rows(const uint32_t* src, PeerPtrs
 // waiting; the host refuses further rounds and results (engine.cpp
 // peer_failed, AV_ERR_PEER).
 __global__ __launch_bounds__(64) void k_peer_barrier(PeerPtrs arrive, const uint32_t* own, uint32_t world,
-                                                     uint32_t rank, uint32_t seq, uint32_t* err, uint64_t ticks,
-                                                     uint32_t store) {
+                                                     uint32_t rank, uint32_t seq, uint32_t* err, uint64_t ticks) {
   const uint32_t i = threadIdx.x;
   uint32_t* mine = arrive.p[0];  // lane i's rank-i array, selected with static indices
 #pragma unroll
   for (int r = 1; r <= kMaxPeers; ++r)
     if ((uint32_t)r == i) mine = arrive.p[r];
-  if (store && i < world) __hip_atomic_store(mine + rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (i < world) __hip_atomic_store(mine + rank, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   const bool failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
   if (i >= world || failed) return;
   const uint32_t* slot = own + i;  // own == arrive.p[rank]
@@ -986,27 +985,19 @@ hipError_t launch_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, u
   return hipGetLastError();
 }
 
-hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
-                               uint32_t timeout_ms, hipStream_t s) {
-  if (world > (uint32_t)kMaxPeers + 1u || rank >= world) return hipErrorInvalidValue;
-  int dev = 0, khz = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+hipError_t peer_timeout_ticks(int device, uint32_t timeout_ms, uint64_t* ticks) {
+  int khz = 0;
+  const hipError_t e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
   if (e != hipSuccess) return e;
-  const uint64_t ticks = (uint64_t)timeout_ms * (uint64_t)(khz > 0 ? khz : 100000);
-  hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, s, arrive, arrive.p[rank], world, rank, seq, err, ticks, 1u);
-  return hipGetLastError();
+  *ticks = (uint64_t)timeout_ms * (uint64_t)(khz > 0 ? khz : 100000);
+  return hipSuccess;
 }
 
-hipError_t launch_peer_wait(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
-                            uint32_t timeout_ms, hipStream_t s) {
+hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
+                               uint64_t timeout_ticks, hipStream_t s) {
   if (world > (uint32_t)kMaxPeers + 1u || rank >= world) return hipErrorInvalidValue;
-  int dev = 0, khz = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
-  if (e != hipSuccess) return e;
-  const uint64_t ticks = (uint64_t)timeout_ms * (uint64_t)(khz > 0 ? khz : 100000);
-  hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, s, arrive, arrive.p[rank], world, rank, seq, err, ticks, 0u);
+  hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, s, arrive, arrive.p[rank], world, rank, seq, err,
+                     timeout_ticks);
   return hipGetLastError();
 }
 

@@ -44,7 +44,32 @@ struct SweepAcc {
   uint32_t reread = 0;  // per lane: gathered preference bytes beyond the one compulsory read of each word
   uint32_t emitted_bytes = 0, updates = 0;  // wave-uniform: StatusUpdate log bytes written, updates emitted
   uint32_t umis = 0;  // per lane: some published word differed from ref_node's word of pref_in (p.uni_out)
+  // wave-uniform (p.count_changed): published words that differ from the word they overwrite (bits 0-15)
+  // and the 16-lane groups holding one (bits 16-31: 64-B row segments when PS == BL, a multiple of 16)
+  uint32_t changed = 0;
 };
+
+// The published word of one lane into pref_out. In a peer-push round the word being overwritten is
+// what every peer replica holds (kernels.h), so only a changed word is stored into each replica
+// (system-scope write-through stores over xGMI; the barrier after the round orders them before any
+// peer reads them). Changed words are counted when p.count_changed (the push volume),
+// per wave by ballot (a scalar: a per-lane counter live across the tile loop spilled).
+template <int POL>
+__device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uint32_t pub, uint32_t& changed) {
+  if (p.count_changed) {
+    const uint32_t old = p.pref_out[prow];
+    const unsigned long long m = __ballot(pub != old);
+    const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+    const uint32_t groups = ((lo & 0xFFFFu) ? 1u : 0u) + ((lo >> 16) ? 1u : 0u) + ((hi & 0xFFFFu) ? 1u : 0u) + ((hi >> 16) ? 1u : 0u);
+    changed += (uint32_t)__popcll(m) + (groups << 16);
+    if (pub != old) {
+      for (uint32_t r = 0; r < p.push_n; ++r)
+        __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
+  st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
+}
 
 enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3, kModeWarmPipe = 4, kModeFresh = 5 };
 
@@ -459,19 +484,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^31
     const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
     if (p.uni_out) acc.umis |= pub != in.uref ? 1u : 0u;  // uniform rows (kernels.h)
-    if (p.push_n) {
-      // peer-push exchange (kernels.h): the word being overwritten is what
-      // every peer replica holds; push only a changed word
-      const uint32_t old = p.pref_out[prow];
-      if (pub != old) {
-        // system-scope stores write through to the peer's memory (xGMI); the
-        // barrier after the round orders them before any peer reads them
-        for (uint32_t r = 0; r < p.push_n; ++r)
-          __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
-    st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
+    publish<POL>(p, prow, pub, acc.changed);
     // a record deleted this round keeps the vote/consider planes stored
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
@@ -526,7 +539,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
                           (WARM && (in.kw & kHiVirt) && !(kunread && kdefer) ? 16u : 0u) + (hv && !kdefer ? 16u : 0u);
   // V read: 32 B stored, 28 B regathered (stale), 0 B uniform
   acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale == kVStale ? 4u : in.stale == kVUniform ? 32u : 0u) -
-                                 (virt ? 32u : 0u) - (cvirt ? 32u : 0u) + (p.push_n ? 4u : 0u) -
+                                 (virt ? 32u : 0u) - (cvirt ? 32u : 0u) + (p.count_changed ? 4u : 0u) -
                                  kbytes - (astore ? 0u : 4u)
                            : 0u;
   acc.emitted_bytes += emitted;
@@ -594,15 +607,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   if (active) {
     if (p.uni_out) acc.umis |= pub != uref ? 1u : 0u;
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-    if (p.push_n) {  // peer-push exchange: as process_tile
-      const uint32_t old = p.pref_out[prow];
-      if (pub != old) {
-        for (uint32_t r = 0; r < p.push_n; ++r)
-          __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
-    const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
-    st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
+    publish<POL>(p, prow, pub, acc.changed);
   }
   if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, p.pref_in[p.ref_node * p.PS + (active ? b : 0u)]);
   if (lane == 0) p.kpend[tile] = ((kw & 0xFFu) + 1u) | kPendAllLive | (kw & kHiVirt);
@@ -613,7 +618,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   // reference rows: 8 flag bytes per node read, the reference word instead of
   // the 32 B of gathered votes, the next reference word + the flag written
   acc.reread += active && gather ? 28u : 0u;
-  acc.lane_bytes += (active ? 40u + (p.push_n ? 4u : 0u) + rbytes - (gather ? 0u : 32u) +
+  acc.lane_bytes += (active ? 40u + (p.count_changed ? 4u : 0u) + rbytes - (gather ? 0u : 32u) +
                                   (REF && p.rflag_out ? 4u + (b == 0u ? 1u : 0u) : 0u)
                             : 0u) +
                     (lane == 0 ? 8u : 0u);
@@ -650,7 +655,6 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
   const __amdgpu_buffer_rsrc_t ta =
       __builtin_amdgcn_make_buffer_rsrc(p.planes + (size_t)t0 * (kPlanes * 64u), 0, (int)(ntiles * kPlanes * 64u * 4u),
                                         kRsrcWord3);
-  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
   const uint32_t aoff = (1536u + lane) * 4u;
   // reference words of this lane's block: the snapshot being written is flagged against rin, the
   // flags of the snapshot being read (prefetched for the run's nodes: wd.flagok) against rprev
@@ -705,21 +709,14 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     if (active) {
       umis |= pub != rin ? 1u : 0u;
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-      if (p.push_n) {  // peer-push exchange: as process_tile
-        const uint32_t old = p.pref_out[prow];
-        if (pub != old) {
-          for (uint32_t r = 0; r < p.push_n; ++r)
-            __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-      st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
+      publish<POL>(p, prow, pub, acc.changed);
     }
     if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, rin);
     done |= 1u << i;
     applied += 8u * (uint32_t)__popc(P0);
     // settled_tile's accounting: 40 B per active lane (+ 4 B push read), 28 of the 32 gathered re-read;
     // reference rows: the 8 flag bytes per node instead of the 32 B of votes, the flag byte written
-    bytes += active ? 40u + (p.push_n ? 4u : 0u) - (gather ? 0u : 32u) +
+    bytes += active ? 40u + (p.count_changed ? 4u : 0u) - (gather ? 0u : 32u) +
                           (REF && p.rflag_out ? (b == 0u ? 1u : 0u) : 0u)
                     : 0u;
     reread += active && gather ? 28u : 0u;
@@ -759,7 +756,6 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
   const __amdgpu_buffer_rsrc_t ta =
       __builtin_amdgcn_make_buffer_rsrc(p.planes + (size_t)t0 * (kPlanes * 64u), 0, (int)(ntiles * kPlanes * 64u * 4u),
                                         kRsrcWord3);
-  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
   const uint32_t aoff = (1536u + lane) * 4u;
   // the candidates' A planes are all loaded before the first test: up to kUniRun loads in flight
   // per wave instead of one load latency per tile
@@ -789,19 +785,12 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
     if (active) {
       umis |= pub != rin ? 1u : 0u;
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-      if (p.push_n) {  // peer-push exchange: as process_tile
-        const uint32_t old = p.pref_out[prow];
-        if (pub != old) {
-          for (uint32_t r = 0; r < p.push_n; ++r)
-            __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
-      st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
+      publish<POL>(p, prow, pub, acc.changed);
     }
     done |= 1u << i;
     applied += 8u * (uint32_t)__popc(P0);
     // settled_run's accounting without the 32 B of gathered votes: A read, valid, published word
-    bytes += active ? 8u + (p.push_n ? 4u : 0u) : 0u;
+    bytes += active ? 8u + (p.count_changed ? 4u : 0u) : 0u;
   }
   if (lane < ntiles && ((done >> lane) & 1u)) {
     p.kpend[t0 + lane] = ((meta & 0xFFu) + 1u) | kPendAllLive | (meta & kHiVirt);
@@ -1004,6 +993,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     if (rr) atomicAdd(&p.bytes[kLogShards + shard], rr);
     if (acc.updates) atomicAdd(&p.upd_count[shard], acc.updates);
   }
+  if (p.count_changed && lane == 0 && acc.changed) {
+    atomicAdd(&p.changed[wave0 % p.log_shards], (unsigned long long)(acc.changed & 0xFFFFu));
+    atomicAdd(&p.changed[kLogShards + wave0 % p.log_shards], (unsigned long long)(acc.changed >> 16));
+  }
   if (p.uni_out && __ballot(acc.umis != 0u) != 0ull && lane == 0) {
     // some word this wave published differs from the reference row: tag the output snapshot's slot
     // of this rank in every replica (read by the next round, after the barrier in a peer exchange)
@@ -1011,24 +1004,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     p.uni_out[p.uni_rank] = tag;
     for (uint32_t r = 0; r < p.push_n; ++r)
       __hip_atomic_store(p.push_dst[r] + p.uni_off + p.uni_rank, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (p.arrive_n) {
-    // peer exchange: this rank's arrival, stored by the round's last wave once every wave's stores
-    // (its pushes into the peers' replicas: system-scope, written through) are acknowledged, so the
-    // barrier kernel behind the round only waits (one launch gap off the exchange's critical path)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t last = 0u;
-    if (lane == 0)
-      last = __hip_atomic_fetch_add(&p.wave_done[p.arrive_seq & 1u], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-                     nwaves - 1u
-                 ? 1u
-                 : 0u;
-    if (__builtin_amdgcn_readfirstlane((int)last)) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
-      if (lane < p.arrive_n)
-        __hip_atomic_store(p.arrive_dst[lane] + p.arrive_rank, p.arrive_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (lane == 0) __hip_atomic_store(&p.wave_done[(p.arrive_seq + 1u) & 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
   }
 }
 

@@ -82,7 +82,7 @@ EXPORTED = [
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
     "av_peer_handles", "av_peer_init", "av_get_round", "av_set_round", "av_log_base_round", "av_updates_digest",
     "av_updates_digest_range", "av_read_pref_words", "av_set_polling",
-    "av_register_votes_batch",
+    "av_register_votes_batch", "av_changed_words", "av_materialize",
 ]
 
 _lib = None
@@ -125,6 +125,8 @@ def lib():
         "av_applied_votes": (i32, [_vp, P(i64)]),
         "av_alg_bytes": (i32, [_vp, P(i64)]),
         "av_alg_bytes_reread": (i32, [_vp, P(i64)]),
+        "av_changed_words": (i32, [_vp, P(i64), P(i64)]),
+        "av_materialize": (i32, [_vp]),
         "av_finalized_count": (i32, [_vp, P(i64)]),
         "av_live_records": (i32, [_vp, i32, P(i64)]),
         "av_discard_updates": (i32, [_vp]),
@@ -414,6 +416,17 @@ class Engine:
         out = C.c_int64(0)
         _check(lib().av_alg_bytes_reread(self._h, C.byref(out)))
         return out.value
+
+    def changed_words(self):
+        """(words, 64-B segments) of published words that changed in sweep rounds (pushed to every
+        peer on a peer-push engine; counted on any engine with option count_changed=1)."""
+        w, g = C.c_int64(0), C.c_int64(0)
+        _check(lib().av_changed_words(self._h, C.byref(w), C.byref(g)))
+        return w.value, g.value
+
+    def materialize(self):
+        """Write back the deferred state (stale vote planes, pending count steps) now."""
+        _check(lib().av_materialize(self._h))
 
     def read_records(self, n0=None, n1=None, t0=None, t1=None):
         n0 = self.node_range[0] if n0 is None else n0

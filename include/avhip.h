@@ -116,12 +116,21 @@ const char* av_strerror(int code);
 const char* av_last_error(void); /* thread-local detail of the last failure */
 
 /* ---- population (processor.go:45-58) ---- */
+/* AddTargetToReconcile of every target for every local node (a fresh network:
+ * NewVoteRecord, vote.go:33-35) with the initial acceptance of init_mode. On a
+ * peer-push engine (av_peer_init) this is collective: every rank calls it, and
+ * the new rows reach every peer replica before the next round. */
 int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param);
 /* AddTargetToReconcile for targets[0..n) of one node, in order;
  * added[i] = 1 iff a record was created (false if !IsValid or live record). */
 int av_add_targets(av_engine* e, int64_t node, const int64_t* targets, const uint8_t* accepted, int64_t n,
                    uint8_t* added);
-/* Target.IsValid() of a target for every node (isWorthyPolling). */
+/* Target.IsValid() of a target for every node (isWorthyPolling, processor.go:101).
+ * Validity is per target (per Hash), shared by every node of the engine: the
+ * reference keeps, per Processor, the Target object it was given
+ * (processor.go:55) and asks it IsValid() at vote time (:101), so two
+ * Processors holding different Target objects under one Hash could disagree.
+ * This engine cannot represent that case ("Validity"). */
 int av_set_valid(av_engine* e, int64_t target, int32_t valid);
 
 /* ---- one-node Processor methods (drop-in path) ---- */
@@ -136,7 +145,10 @@ int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const 
  * Response, as main.go:136 calls it): Response i is registered by node
  * nodes[i] with the votes offsets[i] .. offsets[i+1]-1 of targets/errs, in
  * order; a node may appear several times (its Responses apply one after the
- * other). status_out[v] as for av_register_votes. */
+ * other). status_out[v] as for av_register_votes.
+ * Limits of both drop-in calls: AV_ERR_UNSUPPORTED on an engine (shard) with
+ * more than 4M (2^22) local targets (a packed vote carries a 22-bit local
+ * target index), AV_ERR_INVALID_ARG for >= 2^31 votes or Responses in one call. */
 int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, const int64_t* offsets,
                             const int64_t* targets, const uint32_t* errs, int32_t* status_out);
 int av_is_accepted(av_engine* e, int64_t node, int64_t target, int32_t* out);
@@ -220,6 +232,20 @@ int av_alg_bytes(av_engine* e, int64_t* out);
  * minus this = the compulsory bytes (every word read or written once), a lower
  * bound on HBM traffic. Diagnostics; no reference counterpart. */
 int av_alg_bytes_reread(av_engine* e, int64_t* out);
+/* Published preference words that changed in sweep rounds since creation: a
+ * word differs from the word of the snapshot buffer it overwrites (the snapshot
+ * of two rounds before, which every peer replica holds). Counted in every round
+ * of a peer-push engine (= the words pushed to each peer) and,
+ * with option "count_changed" = 1, in every sweep round of any engine.
+ * segments (may be null): the 64-B row segments holding a changed word (16
+ * consecutive words of a row; exact when the rows are 16 or 32 words wide).
+ * Diagnostics; no reference counterpart. */
+int av_changed_words(av_engine* e, int64_t* words, int64_t* segments);
+/* Write back the engine's deferred state (stale vote planes, pending count
+ * steps: DESIGN.md §3) now instead of at the next access that needs it. Every
+ * result is the same either way; timed as one launch when timing is on.
+ * Engine maintenance; no reference counterpart. */
+int av_materialize(av_engine* e);
 /* Canonical words for local nodes [n0,n1) x targets [t0,t1) (global ids). */
 int av_read_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, uint32_t* out);
 int av_write_records(av_engine* e, int64_t n0, int64_t n1, int64_t t0, int64_t t1, const uint32_t* in);
@@ -265,7 +291,10 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  * round). Diagnostics that make results invalid: "ablate_gather",
  * "ablate_emit" (StatusUpdates counted, not stored), "ablate_node"
  * (k_round_node: 1 = lanes past the cap skipped, 4 = no plane stores),
- * "unsynced_shard". */
+ * "unsynced_shard". Diagnostics that leave results valid: "count_changed"
+ * (1: count changed published words in every sweep round, av_changed_words),
+ * "solo_barrier" (1: a one-rank peer barrier after every round of an engine
+ * without an exchange: the barrier's fixed cost alone). */
 int av_set_option(av_engine* e, const char* name, int64_t value);
 
 /* ---- measurement ---- */

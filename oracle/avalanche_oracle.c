@@ -397,6 +397,10 @@ void avo_sim_set_round(avo_sim* s, int64_t node, int64_t round) { avo_processor_
 
 void avo_sim_set_valid(avo_sim* s, int64_t t, int valid) { s->valid[t] = (uint8_t)(valid != 0); }
 int64_t avo_sim_round_index(const avo_sim* s) { return s->round; }
+/* The harness's round counter (R1: the peer draw's RNG counter): a network
+ * created now behaves as if populated at round r (the engine's av_init_records
+ * on an engine that has run r rounds). */
+void avo_sim_set_round_index(avo_sim* s, int64_t r) { s->round = r; }
 int avo_sim_is_byzantine(const avo_sim* s, int64_t node) { return s->byz[node]; }
 
 int avo_sim_add(avo_sim* s, int64_t node, int64_t t, int accepted) {

@@ -126,6 +126,7 @@ void avo_sim_set_valid(avo_sim* s, int64_t t, int valid);
 int64_t avo_sim_get_round(const avo_sim* s, int64_t node); /* node's Processor.GetRound */
 void avo_sim_set_round(avo_sim* s, int64_t node, int64_t round);
 int64_t avo_sim_round_index(const avo_sim* s);
+void avo_sim_set_round_index(avo_sim* s, int64_t r); /* harness RNG counter (re-population at round r) */
 /* One round. replay_errs: NULL (sim mode: votes from peers' published
  * preferences) or [n_nodes][k][n_targets] err words. Updates are written as
  * 5 int64 columns (round, node, slot, target, status) in reference append order.

@@ -76,6 +76,8 @@ def lib():
         L.avo_sim_set_valid.argtypes = [C.c_void_p, C.c_int64, C.c_int]
         L.avo_sim_round_index.restype = C.c_int64
         L.avo_sim_round_index.argtypes = [C.c_void_p]
+        L.avo_sim_set_round_index.restype = None
+        L.avo_sim_set_round_index.argtypes = [C.c_void_p, C.c_int64]
         L.avo_sim_round.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
                                     C.POINTER(C.c_int64), C.c_int32, C.POINTER(C.c_int64)]
         L.avo_sim_round_range.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
@@ -183,6 +185,11 @@ class Sim:
     @property
     def round(self):
         return lib().avo_sim_round_index(self._h)
+
+    def set_round_index(self, r):
+        """Start this (freshly populated) network's rounds at round r: the engine's
+        av_init_records on an engine that has already run r rounds."""
+        lib().avo_sim_set_round_index(self._h, r)
 
     def get_round(self, node):
         return lib().avo_sim_get_round(self._h, node)

@@ -82,3 +82,58 @@ def test_cpu_baseline_threads_respect_the_quota():
     assert 1 <= hc["threads"] <= hc["affinity_cpus"]
     if hc["cgroup_cpu_quota"]:
         assert hc["threads"] <= max(1, round(hc["cgroup_cpu_quota"]))
+
+
+def test_gpus_n_without_launcher_spawns_ranks(monkeypatch):
+    """`python3 bench.py --gpus 2` with no torch.distributed.run around it starts ONE child
+    process running the same bench under torch.distributed.run with 2 ranks (rendezvous on
+    127.0.0.1), before any GPU call, and exits with the child's status."""
+    calls = []
+
+    def fake_call(cmd):
+        calls.append(cmd)
+        return 7
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench.subprocess, "call", fake_call)
+    monkeypatch.setattr(bench.torch.cuda, "set_device", lambda *a: pytest.fail("GPU touched before the spawn"))
+    with pytest.raises(SystemExit) as ex:
+        bench.main(["--gpus", "2", "--steps", "3", "--rehearse-one-gpu"])
+    assert ex.value.code == 7
+    assert len(calls) == 1
+    cmd = calls[0]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    i = cmd.index(os.path.abspath(bench.__file__))
+    assert cmd[i + 1:] == ["--gpus", "2", "--steps", "3", "--rehearse-one-gpu"]
+
+
+def test_launcher_present_runs_in_process(monkeypatch):
+    """Under a launcher (WORLD_SIZE set) nothing is spawned; a mismatch is refused."""
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setattr(bench.subprocess, "call", lambda cmd: pytest.fail("spawned under a launcher"))
+    with pytest.raises(SystemExit) as ex:
+        bench.main(["--gpus", "2"])
+    assert "WORLD_SIZE=4" in str(ex.value.code)
+
+
+def test_exchange_model_per_link_bytes():
+    changed = [{"round": 0, "words": 1000, "segments": 100}, {"round": 1, "words": 0, "segments": 0}]
+    m = bench.exchange_model(changed, n=1_000_000, ps=32)
+    # g8: 100 segments / 8 ranks * 64 B per link
+    assert m["g8"]["push_bytes_per_link_max"] == pytest.approx(100 / 8 * 64)
+    assert m["g8"]["push_ms_per_round_max"] == pytest.approx(100 / 8 * 64 / (bench.XGMI_LINK_GBS * 1e9) * 1e3)
+    assert m["g2"]["allgather_ms_per_round"] == pytest.approx(500_000 * 128 / (bench.XGMI_LINK_GBS * 1e9) * 1e3)
+    assert bench.exchange_model(None, 10, 1) is None
+
+
+def test_line_roofline_is_compact():
+    rows = [{"round": r, "kernel_ms": 0.1 if r >= 4 else 1.0, "launches": 1,
+             "model_bytes": 8e8 if r >= 4 else 4e9, "reread_bytes": 0} for r in range(6)]
+    full = bench.roofline(_r(rows), window=None)
+    c = bench.compact_roofline(full)
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in c
+    assert set(c["kinds"]) == {"fresh", "storm", "klazy"}
+    assert len(json.dumps(c)) < 900

@@ -23,6 +23,12 @@ CASES = {
     "byz_pairs": (256, 200, 8, BYZ20, 4, 0, 30, {}),
     "k5_first_gen": (192, 130, 5, BYZ20, 3, P80, 12, {"kernel": 1}),
     "capped": (64, 4200, 8, 0, 3, P80, 6, {}),
+    # bench.py's epoch protocol: the network re-populated (av_init_records, collective) after 9
+    # rounds; the new rows must reach every replica (compared: the rounds after the re-population)
+    "c4_shape_reinit": (512, 1000, 8, 0, 3, P80, 22, {"_reinit": 9}),
+    "byz_pairs_reinit": (256, 200, 8, BYZ20, 4, 0, 20, {"_reinit": 7}),
+    # uniform rows on / off across ranks (mismatch slots pushed to the replicas)
+    "c4_shape_uniform_off": (512, 1000, 8, 0, 3, P80, 22, {"uniform_rows": 0}),
 }
 
 
@@ -35,7 +41,8 @@ def _rank_main(case, world, rank, d, q):
         e = avhip.Engine(n, m, k=k, seed=11, byz_threshold=byz, node_range=(rank * per, (rank + 1) * per),
                          device=0, log_capacity=1 << 22)
         for name, v in opts.items():
-            e.set_option(name, v)
+            if not name.startswith("_"):
+                e.set_option(name, v)
         e.init_records(init_mode, init_param)
         tmp = os.path.join(d, f"h{rank}.tmp")
         with open(tmp, "wb") as f:
@@ -57,9 +64,16 @@ def _rank_main(case, world, rank, d, q):
             raise AssertionError("add_targets accepted on a peer-push engine")
         except avhip.AvError:
             pass
-        # two calls: stale vote planes and snapshot rotation carried across them
-        e.run_rounds(rounds // 2)
-        e.run_rounds(rounds - rounds // 2)
+        if "_reinit" in opts:  # bench.py's epoch start: a fresh network at round r1 (collective)
+            e.run_rounds(opts["_reinit"])
+            e.synchronize()
+            e.discard_updates()
+            e.init_records(init_mode, init_param)
+            e.run_rounds(rounds - opts["_reinit"])
+        else:
+            # two calls: stale vote planes and snapshot rotation carried across them
+            e.run_rounds(rounds // 2)
+            e.run_rounds(rounds - rounds // 2)
         e.synchronize()
         np.save(os.path.join(d, f"rec{rank}.npy"), e.read_records())
         np.save(os.path.join(d, f"upd{rank}.npy"), e.fetch_updates())
@@ -101,9 +115,12 @@ def run_ranks(case, world, tmp_path):
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_peer_push_vs_oracle(oracle, case, world, tmp_path):
-    n, m, k, byz, init_mode, init_param, rounds, _ = CASES[case]
+    n, m, k, byz, init_mode, init_param, rounds, opts = CASES[case]
     rec, upd, prefs = run_ranks(case, world, tmp_path)
     sim = oracle.Sim(n, m, k, seed=11, byz_threshold=byz, init_mode=init_mode, init_param=init_param)
+    if "_reinit" in opts:  # a fresh network populated at round r1 (oracle Sim.set_round_index)
+        sim.set_round_index(opts["_reinit"])
+        rounds -= opts["_reinit"]
     exp = [sim.run_round()[0] for _ in range(rounds)]
     exp = np.concatenate(exp)
     exp = exp[np.lexsort(exp.T[::-1])]

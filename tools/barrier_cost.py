@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """Fixed per-round cost of the peer-push exchange, measured in
-the one-GPU rehearsal: `world` rank processes, each a node shard of a small
-network with the peer exchange (av_peer_init; every rank on device 0), time
-R back-to-back warm rounds; the same network on one engine without an
-exchange is the baseline. On a small network the round kernels take a few
-microseconds, so the difference per round is the exchange's fixed cost: the
-folded arrival in the round kernel's last wave, the 1-wave wait kernel and its
-launch gap (plus the interleaving of the ranks' kernels on one GPU, which the
-8-GPU case does not have).
+the one-GPU rehearsal: `world` rank processes, each a node shard of one
+network (every rank on device 0). Each rank times R back-to-back warm rounds
+of its shard twice, in the same contended setup (all ranks running at once,
+started together):
+  1. `unsynced`: the shard alone (option unsynced_shard: no pushes, no barrier);
+  2. `exchange`: the same shard with the peer exchange (av_peer_init: changed
+     words pushed into the peers' replicas + the device barrier per round).
+The exchange's cost per round = slowest rank's (2) - slowest rank's (1): the
+same shards, the same GPU sharing, only the exchange differs. (The previous
+form subtracted the unsharded engine's round / world, which charged the
+contention of the shared GPU to the exchange.)
 
     python tools/barrier_cost.py [--world 2] [--nodes 8192] [--targets 1000] [--rounds 200]
 """
@@ -38,20 +41,45 @@ def _run(eng, warm, rounds):
     eng.run_rounds(rounds)
     ms, nl = eng.kernel_stats()
     eng.set_timing(False)
+    eng.discard_updates()
     return dt / rounds * 1e3, ms / max(1, nl)
+
+
+def _meet(d, name, world, rank, timeout=60):
+    """File barrier across the rank processes (host side, between phases)."""
+    open(os.path.join(d, f"{name}.{rank}"), "w").close()
+    t0 = time.time()
+    while not all(os.path.exists(os.path.join(d, f"{name}.{r}")) for r in range(world)):
+        if time.time() - t0 > timeout:
+            raise TimeoutError(f"ranks did not meet at {name}")
+        time.sleep(0.005)
+
+
+def _engine(args, world, rank):
+    import avhip
+
+    per = args.nodes // world
+    e = avhip.Engine(args.nodes, args.targets, k=8, seed=3, node_range=(rank * per, (rank + 1) * per), device=0,
+                     log_capacity=1 << 24)
+    for o in args.option:
+        name, v = o.split("=")
+        e.set_option(name, int(v))
+    e.init_records(avhip.INIT_BERNOULLI, P80)
+    return e
 
 
 def _rank(args, world, rank, d, q):
     try:
-        import avhip
-
-        per = args.nodes // world
-        e = avhip.Engine(args.nodes, args.targets, k=8, seed=3, node_range=(rank * per, (rank + 1) * per), device=0,
-                         log_capacity=1 << 24)
-        for o in args.option:
-            name, v = o.split("=")
-            e.set_option(name, int(v))
-        e.init_records(avhip.INIT_BERNOULLI, P80)
+        out = {}
+        # 1. the shard alone, every rank at once (no exchange)
+        e = _engine(args, world, rank)
+        e.set_option("unsynced_shard", 1)
+        _meet(d, "a", world, rank)
+        ms, kms = _run(e, args.warm, args.rounds)
+        e.close()
+        out["unsynced"] = {"ms_per_round": ms, "kernel_ms_per_launch": kms}
+        # 2. the same shard with the peer exchange
+        e = _engine(args, world, rank)
         with open(os.path.join(d, f"h{rank}.tmp"), "wb") as f:
             f.write(e.peer_handles())
         os.rename(os.path.join(d, f"h{rank}.tmp"), os.path.join(d, f"h{rank}.bin"))
@@ -62,9 +90,12 @@ def _rank(args, world, rank, d, q):
                 raise TimeoutError("peer handles did not arrive")
             time.sleep(0.02)
         e.peer_init(world, rank, [open(p, "rb").read() for p in paths])
+        _meet(d, "b", world, rank)
         ms, kms = _run(e, args.warm, args.rounds)
+        out["exchange"] = {"ms_per_round": ms, "kernel_ms_per_launch": kms,
+                           "changed_words_per_round": e.changed_words()[0] / (args.warm + 2 * args.rounds)}
         e.close()
-        q.put((rank, {"ms_per_round": ms, "kernel_ms_per_launch": kms}))
+        q.put((rank, out))
     except Exception as ex:
         q.put((rank, {"error": repr(ex)[:300]}))
 
@@ -79,12 +110,6 @@ def main():
     ap.add_argument("--option", action="append", default=[], help="name=value engine option for the rank engines")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
-    import avhip
-
-    e = avhip.Engine(args.nodes, args.targets, k=8, seed=3, device=0, log_capacity=1 << 24)
-    e.init_records(avhip.INIT_BERNOULLI, P80)
-    base_ms, base_kms = _run(e, args.warm, args.rounds)
-    e.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with tempfile.TemporaryDirectory() as d:
@@ -92,7 +117,7 @@ def main():
         for p in procs:
             p.start()
         res = {}
-        deadline = time.time() + 120
+        deadline = time.time() + 150
         while len(res) < args.world and time.time() < deadline:
             try:
                 r, v = q.get(timeout=1.0)
@@ -103,13 +128,15 @@ def main():
             p.join(timeout=10)
             if p.is_alive():
                 p.kill()
-    out = {"options": args.option, "world": args.world, "nodes": args.nodes, "targets": args.targets, "rounds": args.rounds,
-           "single_engine": {"ms_per_round": base_ms, "kernel_ms_per_launch": base_kms}, "ranks": res}
-    ok = [v for v in res.values() if "ms_per_round" in v]
+    out = {"options": args.option, "world": args.world, "nodes": args.nodes, "targets": args.targets,
+           "rounds": args.rounds, "ranks": res}
+    ok = [v for v in res.values() if "exchange" in v]
     if len(ok) == args.world:
-        out["exchange_fixed_cost_us"] = (max(v["ms_per_round"] for v in ok) - base_ms / args.world) * 1e3
-        out["note"] = ("per-round wall time of the slowest rank minus the unsharded engine's per-round time / world "
-                       "(the ranks' shards share one GPU here)")
+        ex = max(v["exchange"]["ms_per_round"] for v in ok)
+        un = max(v["unsynced"]["ms_per_round"] for v in ok)
+        out["exchange_fixed_cost_us"] = (ex - un) * 1e3
+        out["note"] = ("slowest rank's per-round wall time with the exchange minus the same shards without it "
+                       "(unsynced_shard), all ranks on one GPU at once in both phases")
     print(json.dumps(out))
     if args.json:
         with open(args.json, "w") as f:

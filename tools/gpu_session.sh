@@ -159,6 +159,13 @@ for s in "$@"; do
     abw6) step abw6 600 bash -c 'for w in c4 c4p c4pb; do for v in base w6 w7; do echo "== $w $v"; if [ $v = base ]; then python tools/round_probe.py --workload $w; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w; fi; done; done' ;;
     pmcall) for W in c4 c4pb c3; do WL=$W bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $?; done
             WL=c2 PMC_LAUNCHES=2 PMC_REPLAY=1 bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $? ;;
+    bench4) step bench 900 python bench.py --detail gpurun_out/bench_detail.json ;;
+    self2) step self2 600 python bench.py --gpus 2 --rehearse-one-gpu --no-secondary --detail gpurun_out/rehearse2_detail.json ;;
+    self2s) step self2s 900 python bench.py --gpus 2 --rehearse-one-gpu --detail gpurun_out/rehearse2s_detail.json ;;
+    exchcost) step exchcost 300 python tools/exchange_cost.py --json gpurun_out/exchange_cost.json ;;
+    barrier4) step barrier4 400 bash -c 'python tools/barrier_cost.py --world 2 --json gpurun_out/barrier2_small.json && python tools/barrier_cost.py --world 2 --nodes 131072 --json gpurun_out/barrier2_big.json && python tools/barrier_cost.py --world 4 --nodes 131072 --json gpurun_out/barrier4_big.json && python tools/barrier_cost.py --world 2 --nodes 1000000 --rounds 40 --json gpurun_out/barrier2_c4.json' ;;
+    abr3) step abr3 600 bash -c 'for w in c4 c4p c4pb; do for v in new r3; do echo "== $w $v"; if [ $v = new ]; then python tools/round_probe.py --workload $w | tail -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_r3.so python tools/round_probe.py --workload $w | tail -1; fi; done; done' ;;
+    peer4) step peer4 600 python -u -m pytest tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
