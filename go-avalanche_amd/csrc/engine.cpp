@@ -870,9 +870,9 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->dlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->upd_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   // a medium record holds >= 2 updates: log_cap / 2 records per shard (16 B each: 8 B of capacity per
-  // update, as the singles). Only the sweep kernel at k = 8 emits them (round_common.h
-  // emit_updates_med): other engines keep a token 16 records per shard.
-  e->mlog_cap = e->k == 8 && !e->capped ? std::max<uint32_t>(e->log_cap / 2, 16) : 16u;
+  // update, as the singles). Only k = 8 kernels emit them (round_common.h emit_updates_med: the sweep,
+  // k_replay_fast): other engines keep a token 16 records per shard.
+  e->mlog_cap = e->k == 8 ? std::max<uint32_t>(e->log_cap / 2, 16) : 16u;
   if ((he = dev_alloc(&e->mlog, (size_t)e->mlog_cap * e->log_shards * 2)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->mlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   (void)hipMemsetAsync(e->mlog_count, 0, avk::kLogShards * 4, e->stream);

@@ -536,35 +536,69 @@ __device__ __forceinline__ uint32_t emit_updates_flat(const RoundParams& p, uint
 // its updates into the payload in registers. Statuses as emit_updates_flat (A
 // after slot j = A_final, flipped back for the first of a record's two
 // updates; vote.go:77-91). Returns the bytes stored (wave-uniform).
+// The reservation half of emit_updates_med: per-lane update count, the wave's
+// per-kind totals and the three reserving atomics, issued but not waited for
+// (their results are read in emit_store_med). A caller that issues it before
+// its plane stores waits for the atomics' return only, not for those stores
+// (vmcnt counts in issue order: an atomic issued after the stores would make
+// the wave wait for every store of the tile first).
+struct EmitRes {
+  uint32_t tot_s, tot_m, tot_d;  // wave-uniform: lanes of each kind
+  uint32_t raw;                  // lanes 0, 1, 2: the singles / medium / dense atomics' results (one VGPR)
+  bool any;                      // wave-uniform: some lane has an update
+};
+
+__device__ __forceinline__ uint32_t lane_updates8(const uint32_t* E, int K) {
+  uint32_t c = 0;
+  for (int j = 0; j < K; ++j) c += (uint32_t)__popc(E[j]);
+  return c;
+}
+
 template <int K>
-__device__ __forceinline__ uint32_t emit_updates_med(const RoundParams& p, uint32_t wave_id, uint32_t lane,
-                                                     uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
-                                                     uint32_t A_final, uint32_t died, uint32_t& updates,
-                                                     uint32_t round_rel) {
-  static_assert(K <= 8, "slot fits 3 bits of a medium field; two updates per record per round at most");
+__device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32_t wave_id, uint32_t lane,
+                                                    const uint32_t (&E)[K], uint32_t& updates) {
+  EmitRes r;
   uint32_t any = 0;
 #pragma unroll
   for (int j = 0; j < K; ++j) any |= E[j];
-  if (__ballot(any != 0u) == 0ull) return 0u;
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int j = 0; j < K; ++j) cnt += (uint32_t)__popc(E[j]);
+  r.any = __ballot(any != 0u) != 0ull;
+  r.tot_s = r.tot_m = r.tot_d = 0u;
+  r.raw = 0u;
+  if (!r.any) return r;
+  const uint32_t cnt = lane_updates8(E, K);
+  const uint32_t dmin = max(p.dense_min, kMedMax + 1u);
+  const bool dense = cnt >= dmin, med = !dense && cnt >= 2u, single = cnt == 1u;
+  r.tot_d = (uint32_t)__popcll(__ballot(dense));
+  r.tot_m = (uint32_t)__popcll(__ballot(med));
+  r.tot_s = (uint32_t)__popcll(__ballot(single));
+  updates += wave_sum(cnt);
+  if (p.ablate_emit == 1u) return r;  // diagnostics: the cost of the round without its log stores
+  const uint32_t shard = wave_id % p.log_shards;
+  // one atomic instruction, lanes 0 / 1 / 2 reserving the singles / medium / dense runs
+  const uint32_t want = lane == 0 ? r.tot_s : lane == 1 ? r.tot_m : lane == 2 ? r.tot_d : 0u;
+  uint32_t* const ctr = lane == 0 ? p.log_count : lane == 1 ? p.mlog_count : p.dlog_count;
+  if (want) r.raw = atomicAdd(ctr + shard, want);
+  return r;
+}
+
+// The store half: every lane with updates stores its one entry at its rank among the wave's lanes
+// of its kind (see emit_updates_med). Returns the bytes stored (wave-uniform).
+template <int K>
+__device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_t wave_id, uint32_t lane,
+                                                   uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
+                                                   uint32_t A_final, uint32_t died, const EmitRes& r,
+                                                   uint32_t round_rel) {
+  static_assert(K <= 8, "slot fits 3 bits of a medium field; two updates per record per round at most");
+  if (!r.any || p.ablate_emit == 1u) return 0u;
+  const uint32_t cnt = lane_updates8(E, K);
   const uint32_t dmin = max(p.dense_min, kMedMax + 1u);
   const bool dense = cnt >= dmin, med = !dense && cnt >= 2u, single = cnt == 1u;
   const uint64_t dl = __ballot(dense), ml = __ballot(med), sl = __ballot(single);
-  const uint32_t tot_d = (uint32_t)__popcll(dl), tot_m = (uint32_t)__popcll(ml), tot_s = (uint32_t)__popcll(sl);
-  updates += wave_sum(cnt);
-  if (p.ablate_emit == 1u) return 0u;  // diagnostics: the cost of the round without its log stores
+  const uint32_t tot_d = r.tot_d, tot_m = r.tot_m, tot_s = r.tot_s;
   const uint32_t shard = wave_id % p.log_shards;
-  uint32_t base = 0, mbase = 0, dbase = 0;
-  if (lane == 0) {
-    if (tot_s) base = atomicAdd(&p.log_count[shard], tot_s);
-    if (tot_m) mbase = atomicAdd(&p.mlog_count[shard], tot_m);
-    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard], tot_d);
-  }
-  base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-  mbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)mbase);
-  dbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)dbase);
+  const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 0);
+  const uint32_t mbase = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 1);
+  const uint32_t dbase = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 2);
   const uint32_t st_d = dbase >= p.dlog_cap ? 0u : min(tot_d, p.dlog_cap - dbase);
   const uint32_t st_m = mbase >= p.mlog_cap ? 0u : min(tot_m, p.mlog_cap - mbase);
   const uint32_t st_s = base >= p.log_cap ? 0u : min(tot_s, p.log_cap - base);
@@ -606,14 +640,14 @@ __device__ __forceinline__ uint32_t emit_updates_med(const RoundParams& p, uint3
     uint32_t S = 0u, j = 0u, cur = 0u;
     uint64_t pl = cnt;  // payload: n, then one field per update
 #pragma unroll
-    for (uint32_t r = 0; r < kMedMax; ++r) {
-      if (r < cnt) {
+    for (uint32_t q = 0; q < kMedMax; ++q) {
+      if (q < cnt) {
         if (cur == 0u) {  // next slot with updates
           j = (uint32_t)__ffs(nz) - 1u;
           nz &= nz - 1u;
           cur = E[0];
 #pragma unroll
-          for (int q = 1; q < K; ++q) cur = j == (uint32_t)q ? E[q] : cur;
+          for (int t = 1; t < K; ++t) cur = j == (uint32_t)t ? E[t] : cur;
         }
         const uint32_t bit = (uint32_t)__ffs(cur) - 1u;
         cur &= cur - 1u;
@@ -621,7 +655,7 @@ __device__ __forceinline__ uint32_t emit_updates_med(const RoundParams& p, uint3
         const uint32_t a = ((A_final ^ (T & ~S)) >> bit) & 1u;  // A after slot j (vote.go:77-91)
         S |= m;
         const uint32_t st = (died & m) ? (a ? 3u : 0u) : (a ? 2u : 1u);
-        pl |= (uint64_t)med_field(j, bit, st) << (4u + 10u * r);
+        pl |= (uint64_t)med_field(j, bit, st) << (4u + 10u * q);
       }
     }
     if (med) {
@@ -635,6 +669,24 @@ __device__ __forceinline__ uint32_t emit_updates_med(const RoundParams& p, uint3
   }
   if (__ballot(ovf) != 0ull) note_overflow(p, lane);
   return 8u * st_s + 16u * st_m + 8u * dense_words(K) * st_d;
+}
+
+// StatusUpdate emission with medium records (p.med, k <= 8): every lane with
+// updates stores exactly one entry — a single packed word (1 update), a
+// medium record (2..kMedMax: key + 10 bits per update, kernels.h) or a dense
+// record (more) — at its rank among the wave's lanes of that kind, so each
+// kind is one contiguous run per wave written by one store instruction (the
+// dense record: three dwordx4). No per-update store loop: a medium lane folds
+// its updates into the payload in registers. Statuses as emit_updates_flat (A
+// after slot j = A_final, flipped back for the first of a record's two
+// updates; vote.go:77-91). Returns the bytes stored (wave-uniform).
+template <int K>
+__device__ __forceinline__ uint32_t emit_updates_med(const RoundParams& p, uint32_t wave_id, uint32_t lane,
+                                                     uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
+                                                     uint32_t A_final, uint32_t died, uint32_t& updates,
+                                                     uint32_t round_rel) {
+  const EmitRes r = emit_reserve_med<K>(p, wave_id, lane, E, updates);
+  return emit_store_med<K>(p, wave_id, lane, node, tbase, E, A_final, died, r, round_rel);
 }
 
 __device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied,

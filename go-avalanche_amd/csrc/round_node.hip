@@ -483,6 +483,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   uint32_t w[K], cw[K], w1[K], cw1[K];
   replay_load<K>(p.replay, g, w, cw);
   if (R > 1u) replay_load<K>(p.replay + p.replay_stride, g, w1, cw1);
+  // StatusUpdates (k = 8: medium records, one entry per lane): round r's log space is reserved at the
+  // end of round r and its entries stored after round r + 1's slot network, so the reserving atomics'
+  // round trip overlaps a round of compute instead of stalling every round
+  EmitRes pend{};
+  uint32_t Epend[K], Apend = 0u;
+  bool have_pend = false;
   for (uint32_t r = 0; r < R; ++r) {
     if (r >= J) {  // a record with count >= 120 may finalize (and leave the poll set) this round
       const uint32_t nearfin = Kp[6] & Kp[5] & Kp[4] & Kp[3];
@@ -528,7 +534,18 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       p.pref_ring[(p.ring_next + r) % 3u][prow] = byz ? byz_pattern(p.round + r + 1u) : A;
       ++pubs;
     }
-    emitted += emit_updates_flat<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, 0u, upd, p.round_rel + r);
+    if constexpr (K == 8) {
+      const EmitRes cur = emit_reserve_med<K>(p, wave_id, lane, E, upd);
+      if (have_pend)
+        emitted += emit_store_med<K>(p, wave_id, lane, node, p.t0 + b * 32u, Epend, Apend, 0u, pend, p.round_rel + r - 1u);
+#pragma unroll
+      for (int j = 0; j < K; ++j) Epend[j] = E[j];
+      Apend = A;
+      pend = cur;
+      have_pend = true;
+    } else {
+      emitted += emit_updates_flat<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, 0u, upd, p.round_rel + r);
+    }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       w[j] = w1[j];
@@ -538,6 +555,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
         cw1[j] = ncw[j];
       }
     }
+  }
+  if constexpr (K == 8) {  // the last round run's entries (round done - 1)
+    if (have_pend)
+      emitted += emit_store_med<K>(p, wave_id, lane, node, p.t0 + b * 32u, Epend, Apend, 0u, pend, p.round_rel + done - 1u);
   }
   if (done < R && b == 0) p.node_flags[nl] = done + 1u;  // the exact pass takes rounds done..R-1
   if (done > 0u) {

@@ -36,6 +36,12 @@
 #include "round_common.h"
 #include "round_slots.h"
 
+// A/B build knob: the StatusUpdate log reservation issued before the tile's stores (1) or after
+// them, inside the emission (0)
+#ifndef AVK_EMIT_HOIST
+#define AVK_EMIT_HOIST 1
+#endif
+
 namespace avk {
 namespace {
 
@@ -449,6 +455,12 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   }
   // count_new = F ? c : count + c on planes 0..6 (survivors stay <= 127); deleted: count 128 (K7 set)
   const uint32_t died = P0 & ~alive;
+#if AVK_EMIT_HOIST
+  // StatusUpdate log reservation (k = 8) before this tile's plane and published-word stores, so that
+  // reading the atomics' results waits for them alone, not for those stores (round_common.h)
+  EmitRes er{};
+  if constexpr (K == 8) er = emit_reserve_med<K>(p, tile, lane, E, acc.updates);
+#endif
   {
     uint32_t cy = 0u;
 #pragma unroll
@@ -522,7 +534,11 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   // k = 8: single words, medium and dense records, one contiguous entry per lane (round_common.h)
   uint32_t emitted;
   if constexpr (K == 8)
+#if AVK_EMIT_HOIST
+    emitted = emit_store_med<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, er, p.round_rel);
+#else
     emitted = emit_updates_med<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, p.round_rel);
+#endif
   else
     emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates);
 

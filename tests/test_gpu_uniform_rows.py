@@ -105,3 +105,30 @@ def test_uniform_rows_add_targets_midrun(oracle):
         assert rows(eng.fetch_updates()) == rows(e_exp), f"round {r}"
     np.testing.assert_array_equal(eng.read_records(), sim.dump(threads=T))
     eng.close()
+
+
+@pytest.mark.parametrize("tpw,merge", [(4, 4), (8, 2)])
+def test_uni_merge_on_off_identical(tpw, merge):
+    """Option uni_merge > 1 (a round with a uniform input: every merge-th wave takes its
+    neighbours' runs, the others end at once) changes only the work split, never a result:
+    digests, records and published rows equal to uni_merge = 1 at runs of tpw tiles (so that
+    tpw * merge <= 16 and the merge really happens)."""
+    n, m = 20_000, 1000
+    out = []
+    for um in (1, merge):
+        eng = avhip.Engine(n, m, k=8, seed=7, log_capacity=1 << 26)
+        eng.set_option("tiles_per_wave", tpw)
+        eng.set_option("uni_merge", um)
+        eng.init_records(avhip.INIT_BERNOULLI, P80)
+        digests = []
+        for _ in range(20):
+            eng.run_rounds(1)
+            digests.append(eng.updates_digest())
+            eng.discard_updates()
+        out.append((digests, eng.read_records(), eng.read_pref(), eng.finalized_count()))
+        eng.close()
+    a, b = out
+    assert a[0] == b[0]
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[2], b[2])
+    assert a[3] == b[3] > 0
