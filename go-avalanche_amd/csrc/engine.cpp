@@ -130,6 +130,7 @@ struct av_engine {
   bool ablate_gather = false;  // diagnostics option "ablate_gather" (invalid results)
   uint32_t ablate_node = 0;  // diagnostics option "ablate_node" (k_round_node, invalid results)
   int ablate_emit = 0;  // diagnostics option "ablate_emit": 1 = StatusUpdates counted, not stored; 2 = no reserving atomic
+  uint32_t ablate_phase = 0;  // diagnostics option "ablate_phase" (kernels.h; results invalid)
   // diagnostics option "unsynced_shard": a node-sharded engine runs rounds with no exchange (other
   // shards' preference rows keep their initial values; per-rank kernel timing only, invalid results)
   bool unsynced_shard = false;
@@ -307,6 +308,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.plane_nt = e->plane_nt ? 1u : 0u;
   p.ablate_gather = e->ablate_gather ? 1u : 0u;
   p.ablate_emit = (uint32_t)e->ablate_emit;
+  p.ablate_phase = e->ablate_phase;
   p.ablate_node = e->ablate_node;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
@@ -547,8 +549,9 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   // uniform rows: sweep rounds at k = 8 tag the snapshot they write; a round whose input snapshot
   // is known uniform tests settled tiles with no peer draw and no gather (kernels.h uni_*)
   // (a node-sharded engine sees every row only through the peer exchange, whose pushes carry the slots)
+  // (unsynced_shard, diagnostics: a rank's share alone, on its own slot: timing as in a peer-push run)
   bool uni = e->uni_rows && sweep && e->k == 8 && !replay && !e->comm && !e->ablate_gather &&
-             (e->NL == (uint32_t)e->N || e->peer_world > 1);
+             (e->NL == (uint32_t)e->N || e->peer_world > 1 || e->unsynced_shard);
   if (uni) {
     int rc = ref_pick(e);
     if (rc != AV_OK) return rc;
@@ -1876,6 +1879,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   const std::string n(name);
   if (n == "plane_nt") {
     e->plane_nt = value != 0;
+  } else if (n == "ablate_phase") {  // diagnostics (kernels.h RoundParams::ablate_phase; results invalid)
+    e->ablate_phase = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(31, value));
   } else if (n == "ablate_emit") {
     e->ablate_emit = (int)std::max<int64_t>(0, std::min<int64_t>(2, value));
   } else if (n == "k_hi_virtual") {  // A/B: virtual K4..K7 group (kernels.h kHiVirt)

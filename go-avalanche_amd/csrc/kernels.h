@@ -105,6 +105,10 @@ struct RoundParams {
   uint32_t plane_nt;         // stream state planes with non-temporal loads/stores
   uint32_t ablate_gather;    // diagnostics only: gather the node's own row (wrong results)
   uint32_t ablate_emit;      // diagnostics only: count StatusUpdates, store none (log left empty)
+  // diagnostics only (k_round_sweep's warm k = 8 general tiles; results invalid), per-phase ablation:
+  // 1 = no peer-row gathers (the votes are made from the row offsets), 2 = no K / A plane loads,
+  // 4 = no K / A / published-word stores, 16 = no slot network (no vote changes anything)
+  uint32_t ablate_phase;
   uint32_t ablate_node;      // diagnostics only (k_round_node, wrong results): 1 = only the lanes below the
                              // cap run, 4 = no plane stores
   // k_round_sweep only

@@ -41,9 +41,16 @@
 #ifndef AVK_EMIT_HOIST
 #define AVK_EMIT_HOIST 1
 #endif
+// A/B build knob: compile the per-phase ablation diagnostics (option "ablate_phase") into the warm
+// path (1: the Makefile's "ablate" variant library only; the product kernel is built without them)
+#ifndef AVK_ABLATE_PHASE
+#define AVK_ABLATE_PHASE 0
+#endif
 
 namespace avk {
 namespace {
+
+constexpr bool kAblatePhase = AVK_ABLATE_PHASE != 0;
 
 struct SweepAcc {
   uint32_t applied = 0, died = 0, lane_bytes = 0;
@@ -172,7 +179,10 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
     if constexpr (VV) {
       if (p.klazy || p.kconsume) in.kw = meta ? meta_of(*wd, tile) & (kPendAllLive | kHiVirt | 0xFFu) : uni(p.kpend[tile]);
     }
-    if (!(in.kw & kPendAllLive) || !p.klazy) {
+    if (kAblatePhase && VV && (p.ablate_phase & 2u)) {  // diagnostics: no K / A loads
+      in.k0 = u32x4{lane, 0u, 0u, 0u};
+      in.k1 = u32x4{0u, 0u, 0u, ~real_mask(p.tn, x.b)};
+    } else if (!(in.kw & kPendAllLive) || !p.klazy) {
       in.k0 = ld4<POL>(grp + 128);
       if (in.kw & kHiVirt)  // the K4..K7 group is virtual (kernels.h kHiVirt)
         in.k1 = u32x4{0u, 0u, 0u, ~real_mask(p.tn, x.b)};
@@ -187,7 +197,7 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
       for (int i = 0; i < 8; ++i) in.C[i] = ld1<POL>(tp + 1024u + (uint32_t)i * 64u + lane);
     }
   }
-  in.A = ld1<POL>(tp + 1536u + lane);
+  in.A = kAblatePhase && VV && (p.ablate_phase & 2u) ? (lane * 0x9E3779B9u) : ld1<POL>(tp + 1536u + lane);
   if (in.stale == kVUniform) {  // the vote register of every polled record = its accepted bit (kernels.h)
     in.v0 = u32x4{in.A, in.A, in.A, in.A};
     in.v1 = u32x4{in.A, in.A, in.A, in.A};
@@ -211,17 +221,23 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
     if constexpr (VV) {
       if (wd && wd->ok) {  // the wave's draws, made once for its run of tiles (implies off32)
         const uint32_t base = (x.nl - wd->nlA) * 2u;
+        const bool nog = kAblatePhase && (p.ablate_phase & 1u);  // diagnostics: no gathers (votes from the row offsets)
         if (in.stale == kVStale) {
           uint32_t pp[K];
           pick_parked(p, wd->sdp, wd->badp, base, x.node, p.round - 1u, rb, pp);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) in.v0[i] = at_byte(p.pref_prev, pp[7 - i] + bo);
+          for (int i = 0; i < 4; ++i) in.v0[i] = nog ? pp[7 - i] * 0x9E3779B9u : at_byte(p.pref_prev, pp[7 - i] + bo);
 #pragma unroll
-          for (int i = 0; i < 3; ++i) in.v1[i] = at_byte(p.pref_prev, pp[3 - i] + bo);
+          for (int i = 0; i < 3; ++i) in.v1[i] = nog ? pp[3 - i] * 0x9E3779B9u : at_byte(p.pref_prev, pp[3 - i] + bo);
           in.v1[3] = 0u;
         }
         pick_parked(p, wd->sdc, wd->badc, base, x.node, p.round, rb, rows);
         drawn = have_rows = true;
+        if (nog) {
+#pragma unroll
+          for (int j = 0; j < K; ++j) in.w[j] = (rows[j] + bo) * 0x9E3779B9u;
+          return;
+        }
       } else if (in.stale == kVStale) {
         // the vote register after last round's 8 sim votes is those votes:
         // V_i = (previous round's slot 7 - i vote); V_7 is never read at k = 8
@@ -393,6 +409,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   }
   uint32_t E[K], alive = P0, applied = 0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u;
   const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
+  constexpr bool KLZ_ABLATE = VVM && WARM && !REPLAY && K == 8;  // the warm general tiles (ablate_phase)
   // count >= 120: may reach 128 (K <= 8); never in a klazy round (engine bound)
   const uint32_t nearfin = klazy ? 0u : P0 & Kp[6] & Kp[5] & Kp[4] & Kp[3];
   const bool det = __ballot(nearfin != 0u) != 0ull;
@@ -412,6 +429,11 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     }
   }
   if (settled) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) E[j] = 0u;
+    c[3] = P0;
+    applied = 8u * (uint32_t)__popc(P0);
+  } else if (kAblatePhase && KLZ_ABLATE && (p.ablate_phase & 16u)) {  // diagnostics: no slot network
 #pragma unroll
     for (int j = 0; j < K; ++j) E[j] = 0u;
     c[3] = P0;
@@ -481,7 +503,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   bool hv = false;
   if (K == 8 && p.hivirt && ((!WARM && p.fresh) || (klazy && (in.kw & kHiVirt))))
     hv = kdefer || __ballot(active && ((Kp[4] | Kp[5] | Kp[6] | died) != 0u)) == 0ull;
-  if (active) {
+  if (active && !(kAblatePhase && KLZ_ABLATE && (p.ablate_phase & 4u))) {
     if (!kdefer) {
       u32x4 o2, o3;
 #pragma unroll

@@ -165,6 +165,8 @@ for s in "$@"; do
     exchcost) step exchcost 300 python tools/exchange_cost.py --json gpurun_out/exchange_cost.json ;;
     barrier4) step barrier4 400 bash -c 'python tools/barrier_cost.py --world 2 --json gpurun_out/barrier2_small.json && python tools/barrier_cost.py --world 2 --nodes 131072 --json gpurun_out/barrier2_big.json && python tools/barrier_cost.py --world 4 --nodes 131072 --json gpurun_out/barrier4_big.json && python tools/barrier_cost.py --world 2 --nodes 1000000 --rounds 40 --json gpurun_out/barrier2_c4.json' ;;
     abr3) step abr3 600 bash -c 'for w in c4 c4p c4pb; do for v in new nohoist r3; do echo "== $w $v"; if [ $v = new ]; then python tools/round_probe.py --workload $w | tail -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w | tail -1; fi; done; done; for v in new r3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
+    ablate) step ablate 600 bash -c 'for w in c4 c4p; do for o in "ablate_phase=0" "ablate_phase=1" "ablate_phase=2" "ablate_phase=4" "ablate_phase=16" "ablate_emit=1" "ablate_phase=7 --option ablate_emit=1"; do echo "== $w $o"; AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_ablate.so python tools/round_probe.py --workload $w --rounds 8 --option $o | grep -v "^{\"workload"; done; done' ;;
+    shardmodel) step shardmodel 600 bash -c 'python tools/shard_model.py --workload c4 --json gpurun_out/shard_model_c4.json && python tools/shard_model.py --workload c4p --json gpurun_out/shard_model_c4p.json' ;;
     fused4) step fused4 600 python -u -m pytest tests/test_gpu_replay_fused.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     peer4) step peer4 600 python -u -m pytest tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
