@@ -124,6 +124,9 @@ def parse(argv=None):
                          "barrier/reductions (not a measurement)")
     ap.add_argument("--no-roofline-pass", action="store_true",
                     help="skip the HIP-event pass (rocprofv3 PMC runs: one window only)")
+    ap.add_argument("--no-exchange-pass", action="store_true",
+                    help="skip the one-GPU changed-word pass (rocprofv3 PMC runs: the roofline pass stays the "
+                         "process's last round-kernel dispatches, tools/pmc_bench.py)")
     ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
                     help="where the full per-round / per-workload detail goes (the line stays compact)")
     return ap.parse_args(argv)
@@ -413,7 +416,7 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     # ---- exchange pass (one GPU, sim workloads): the same steps again with the changed published
     # words counted per round (option count_changed), the input of the multi-GPU push model
     changed = None
-    if world == 1 and not replay and not args.no_roofline_pass:
+    if world == 1 and not replay and not args.no_roofline_pass and not args.no_exchange_pass:
         run.goto(warmup)
         eng.set_option("count_changed", 1)
         changed = []
@@ -497,7 +500,7 @@ def allgather_probe(world, local_rank, total_bytes=1_000_000 * 128, reps=5):
             "note": "C4 node-sharded round exchange (1M x 1000 bits), torch.distributed all_gather_into_tensor"}
 
 
-PMC_DIR = os.path.join(ROOT, "profiles", "r03")
+PMC_DIR = os.path.join(ROOT, "profiles", "r04")
 
 
 def load_pmc(wl, window, world):

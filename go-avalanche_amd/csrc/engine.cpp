@@ -771,8 +771,8 @@ int av_destroy(av_engine* e) {
   if (e->fetch_scratch) (void)hipFree(e->fetch_scratch);
   if (e->dropin_host) (void)hipHostFree(e->dropin_host);
   if (e->digest) (void)hipFree(e->digest);
-  if (e->push_tbl) (void)hipFree(e->push_tbl);
   if (e->changed) (void)hipFree(e->changed);
+  if (e->push_tbl) (void)hipFree(e->push_tbl);
   if (e->marker) (void)hipEventDestroy(e->marker);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->kpend, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->readd, e->died_out, e->nopoll,

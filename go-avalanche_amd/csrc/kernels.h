@@ -52,6 +52,12 @@ __host__ __device__ constexpr uint32_t pref_stride(uint32_t BL) {
   return BL > 32u ? (BL + 31u) / 32u * 32u : (BL <= 1u ? 1u : 1u << (32 - __builtin_clz(BL - 1u)));
 }
 
+// Device pointers of every rank's copy of a buffer, passed by value (kernel arguments: static
+// indices keep them in SGPRs, no table load per use).
+struct PeerPtrs {
+  uint32_t* p[kMaxPeers + 1];
+};
+
 struct RoundParams {
   uint32_t* planes;
   const uint32_t* pref_in;   // [N_pad][PS] published preference (round start)
@@ -135,7 +141,8 @@ struct RoundParams {
   // word a lane is about to overwrite in its own row of pref_out is also what
   // every peer's replica holds; a lane whose published word changed stores the
   // new word into each peer's replica (push_dst[i] = peer i's pref_out; a
-  // device table, read only by lanes that push).
+  // device table, read with scalar loads through the constant address space: no vector load and no
+  // vmcnt drain per push).
   uint32_t push_n;
   uint32_t* const* push_dst;
   // Changed published words (engine option "count_changed"; always counted in a peer-push round): a
@@ -291,9 +298,6 @@ hipError_t launch_kl_materialize(const RoundParams& p, hipStream_t s);
 
 // Peer-push exchange helpers (kernels.hip). push_rows: copy words [w0, w1) of
 // a local snapshot buffer into the same range of every peer replica.
-struct PeerPtrs {
-  uint32_t* p[kMaxPeers + 1];
-};
 hipError_t launch_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, uint64_t w0, uint64_t w1,
                             hipStream_t s);
 // Barrier across the ranks of a node-sharded network: lane i writes `seq`

@@ -46,6 +46,11 @@
 #ifndef AVK_ABLATE_PHASE
 #define AVK_ABLATE_PHASE 0
 #endif
+// A/B build knob: in rounds that count changed words (peer pushes), the overwritten published words
+// are loaded ahead of time with the tile (1) or by each publish (0)
+#ifndef AVK_CC_PREFETCH
+#define AVK_CC_PREFETCH 1
+#endif
 
 namespace avk {
 namespace {
@@ -62,22 +67,34 @@ struct SweepAcc {
   uint32_t changed = 0;
 };
 
+// Peer r's replica pointer from the engine's device table: a scalar load through the constant address
+// space (the table is written once at av_peer_init), so a pushing lane issues no vector load and its
+// wave no vmcnt drain.
+__device__ __forceinline__ uint32_t* peer_ptr(uint32_t* const* tbl, uint32_t r) {
+  using cptr = __attribute__((address_space(4))) const uint64_t*;
+  const cptr t = (cptr)(tbl);
+  return reinterpret_cast<uint32_t*>(t[__builtin_amdgcn_readfirstlane((int)r)]);
+}
+
 // The published word of one lane into pref_out. In a peer-push round the word being overwritten is
 // what every peer replica holds (kernels.h), so only a changed word is stored into each replica
 // (system-scope write-through stores over xGMI; the barrier after the round orders them before any
 // peer reads them). Changed words are counted when p.count_changed (the push volume),
 // per wave by ballot (a scalar: a per-lane counter live across the tile loop spilled).
-template <int POL>
-__device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uint32_t pub, uint32_t& changed) {
-  if (p.count_changed) {
-    const uint32_t old = p.pref_out[prow];
+// `old`: the overwritten word, loaded by the caller ahead of time (p.count_changed only): a load here
+// would put its full latency on the tile's dependence chain.
+template <int POL, bool CC>
+__device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uint32_t pub, uint32_t old,
+                                        uint32_t& changed) {
+  if (CC && p.count_changed) {
+    if (!AVK_CC_PREFETCH) old = p.pref_out[prow];
     const unsigned long long m = __ballot(pub != old);
     const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
     const uint32_t groups = ((lo & 0xFFFFu) ? 1u : 0u) + ((lo >> 16) ? 1u : 0u) + ((hi & 0xFFFFu) ? 1u : 0u) + ((hi >> 16) ? 1u : 0u);
     changed += (uint32_t)__popcll(m) + (groups << 16);
     if (pub != old) {
       for (uint32_t r = 0; r < p.push_n; ++r)
-        __hip_atomic_store(p.push_dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(peer_ptr(p.push_dst, r) + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
@@ -100,6 +117,7 @@ struct TileIn {
   uint32_t kw;                   // wave-uniform: kpend[tile] (kernels.h klazy); K planes not loaded if all-live
   uint32_t C[WARM ? 1 : 8];
   uint32_t uref;                 // uniform rows (p.uni_out): ref_node's word of pref_in for the lane's block
+  uint32_t old;                  // p.count_changed: the word of pref_out this lane's published word overwrites
   uint32_t w[K];                 // yes bits: err == 0 (vote.go:55)
   uint32_t cw[REPLAY ? K : 1];   // consider bits: int32(err) >= 0 (vote.go:56); sim votes: all-ones
 };
@@ -150,7 +168,7 @@ __device__ __forceinline__ LaneIdx lane_idx(const RoundParams& p, uint32_t tile,
   return x;
 }
 
-template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE, bool VVM = false, bool FRESH = false>
+template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE, bool VVM = false, bool FRESH = false, bool CC = true>
 __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
                                           TileIn<K, REPLAY, WARM>& in, const WaveDraw* wd = nullptr) {
   const LaneIdx x = lane_idx(p, tile, lane);
@@ -207,6 +225,7 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
   // loaded with the tile (an in-order vmcnt wait for it late in the step would also wait for the
   // step's plane stores)
   in.uref = p.uni_out ? p.pref_in[p.ref_node * p.PS + x.b] : 0u;
+  in.old = AVK_CC_PREFETCH && CC && p.count_changed ? p.pref_out[x.node * p.PS + x.b] : 0u;  // (publish)
   if constexpr (REPLAY) {
     replay_load<K>(p.replay, x.gc, in.w, in.cw);
   } else {
@@ -287,14 +306,14 @@ __device__ __forceinline__ void ref_flag_store(const RoundParams& p, uint32_t la
     const uint8_t f = (eq & seg) == seg ? ref_tag(p.round + 1u) : 0u;  // pref_out = snapshot round + 1
     if (p.push_n && p.rflag_out[node] != f) {
       for (uint32_t r = 0; r < p.push_n; ++r)
-        __hip_atomic_store(reinterpret_cast<uint8_t*>(p.push_dst[r]) + p.rflag_off + node, f, __ATOMIC_RELAXED,
+        __hip_atomic_store(reinterpret_cast<uint8_t*>(peer_ptr(p.push_dst, r)) + p.rflag_off + node, f, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
     p.rflag_out[node] = f;
   }
 }
 
-template <int K, bool REPLAY, bool WARM, int POL, bool VVM = false, bool REF = false>
+template <int K, bool REPLAY, bool WARM, int POL, bool VVM = false, bool REF = false, bool CC = true>
 __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
                                              const TileIn<K, REPLAY, WARM>& in, uint32_t extra_bytes, SweepAcc& acc) {
   const LaneIdx x = lane_idx(p, tile, lane);
@@ -518,7 +537,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^31
     const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
     if (p.uni_out) acc.umis |= pub != in.uref ? 1u : 0u;  // uniform rows (kernels.h)
-    publish<POL>(p, prow, pub, acc.changed);
+    publish<POL, CC>(p, prow, pub, in.old, acc.changed);
     // a record deleted this round keeps the vote/consider planes stored
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
@@ -595,7 +614,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
 // more): no flip, no StatusUpdate, no deletion, V stays uniform, A and K
 // unchanged. This reads A, the validity word and the 8 votes and does exactly
 // that; any other tile returns false and takes the general load + step.
-template <int POL, bool REF>
+template <int POL, bool REF, bool CC>
 __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile, uint32_t lane, uint32_t kw,
                                              const WaveDraw& wd, SweepAcc& acc) {
   const uint32_t g = tile * 64u + lane;
@@ -610,6 +629,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   const __amdgpu_buffer_rsrc_t ta =
       __builtin_amdgcn_make_buffer_rsrc(p.planes + (size_t)tile * (kPlanes * 64u), 0, kPlanes * 64 * 4, kRsrcWord3);
   const uint32_t A = __builtin_amdgcn_raw_buffer_load_b32(ta, (1536u + lane) * 4u, 0, POL > 0 ? 2 : 0);
+  const uint32_t old = AVK_CC_PREFETCH && CC && p.count_changed ? p.pref_out[(p.n0 + nl) * p.PS + b] : 0u;  // (publish)
   const uint32_t P0 = active ? at_byte(p.valid, b * 4u) : 0u;  // polled = live (kPendAllLive) and valid
   const uint32_t uref = p.uni_out ? p.pref_in[p.ref_node * p.PS + b] : 0u;  // uniform rows (kernels.h)
   uint32_t rows[8];
@@ -645,7 +665,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   if (active) {
     if (p.uni_out) acc.umis |= pub != uref ? 1u : 0u;
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-    publish<POL>(p, prow, pub, acc.changed);
+    publish<POL, CC>(p, prow, pub, old, acc.changed);
   }
   if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, p.pref_in[p.ref_node * p.PS + (active ? b : 0u)]);
   if (lane == 0) p.kpend[tile] = ((kw & 0xFFu) + 1u) | kPendAllLive | (kw & kHiVirt);
@@ -681,7 +701,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
 // read in the prologue next to the draw (4 byte loads per producer lane, from
 // 1 MB at C4: L2-resident where the 128 MB of rows are not) and kept as one
 // ballot. Every settled tile writes its nodes' flags for the row it published.
-template <int POL, bool REF>
+template <int POL, bool REF, bool CC>
 __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t lane, uint32_t tile_end,
                                                 const WaveDraw& wd, SweepAcc& acc) {
   const uint32_t t0 = wd.t0, ntiles = tile_end - t0;
@@ -709,6 +729,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     const uint32_t g = tile * 64u + lane;
     const bool active = g < p.L;
     const uint32_t nl = (active ? g : p.L - 1u) >> p.bl_log2;
+    const uint32_t old = AVK_CC_PREFETCH && CC && p.count_changed ? p.pref_out[(p.n0 + nl) * p.PS + b] : 0u;  // (publish)
     const uint32_t P0 = active ? vw : 0u;  // polled = live (kPendAllLive) and valid
     const uint32_t rel = nl - wd.nlA;
     uint32_t rows[8];
@@ -747,7 +768,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     if (active) {
       umis |= pub != rin ? 1u : 0u;
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-      publish<POL>(p, prow, pub, acc.changed);
+      publish<POL, CC>(p, prow, pub, old, acc.changed);
     }
     if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, rin);
     done |= 1u << i;
@@ -780,7 +801,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
 // general path.
 constexpr uint32_t kUniRun = 16;  // longest run settled_run_uni takes (p.tpw <= 16)
 
-template <int POL>
+template <int POL, bool CC>
 __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32_t lane, uint32_t t0,
                                                     uint32_t tile_end, uint32_t meta, uint32_t nlA, uint32_t nn,
                                                     SweepAcc& acc) {
@@ -802,11 +823,18 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
     const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, (int)i);
     if ((m & (kPendAllLive | (kVMask << 8))) == (kPendAllLive | (kVUniform << 8))) cand |= 1u << i;
   }
-  uint32_t Av[kUniRun];
+  uint32_t Av[kUniRun], Ov[kUniRun];
 #pragma unroll
   for (uint32_t i = 0; i < kUniRun; ++i)
     Av[i] = (cand >> i) & 1u ? __builtin_amdgcn_raw_buffer_load_b32(ta, aoff + i * (kPlanes * 64u * 4u), 0, POL > 0 ? 2 : 0)
                              : 0u;
+  // the overwritten published words (p.count_changed: publish) with them, not one dependent load per tile
+#pragma unroll
+  for (uint32_t i = 0; i < kUniRun; ++i) {
+    const uint32_t g = (t0 + i) * 64u + lane;
+    const uint32_t nl = (g < p.L ? g : p.L - 1u) >> p.bl_log2;
+    Ov[i] = AVK_CC_PREFETCH && CC && p.count_changed && ((cand >> i) & 1u) ? p.pref_out[(p.n0 + nl) * p.PS + b] : 0u;
+  }
   uint32_t done = 0u, applied = 0u, bytes = 0u, umis = 0u;
 #pragma unroll
   for (uint32_t i = 0; i < kUniRun; ++i) {
@@ -823,7 +851,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
     if (active) {
       umis |= pub != rin ? 1u : 0u;
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-      publish<POL>(p, prow, pub, acc.changed);
+      publish<POL, CC>(p, prow, pub, Ov[i], acc.changed);
     }
     done |= 1u << i;
     applied += 8u * (uint32_t)__popc(P0);
@@ -852,7 +880,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
 #ifndef AVK_WARM_WPE
 #define AVK_WARM_WPE 6
 #endif
-template <int K, int MODE, int POL, bool REF = false>
+template <int K, int MODE, int POL, bool REF = false, bool CC = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeWarm ? AVK_WARM_WPE : MODE == kModeReplay || MODE == kModeFresh ? 6 : 7))) void k_round_sweep(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave0 = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -919,7 +947,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           // uniform rows: the run's settled candidates first, with no draw; the draw only if a tile is left
           const uint32_t all_tiles = (uint32_t)((1ull << (tile_end - tile)) - 1ull);
           if (uniform && p.lean && p.settled_fast && p.klazy && p.vv && nn <= 64u && tile_end - tile <= kUniRun) {
-            uni_done = settled_run_uni<POL>(p, lane, tile, tile_end, wd.meta, nlA, nn, acc);
+            uni_done = settled_run_uni<POL, CC>(p, lane, tile, tile_end, wd.meta, nlA, nn, acc);
             uni_ran = true;
           }
           const bool any_stale = __ballot((st & kVMask) == kVStale) != 0ull;
@@ -969,7 +997,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     bool lean_ran = uni_ran;        // the run's settled candidates were all tested by it
     if constexpr (MODE == kModeWarm && K == 8) {
       if (!uni_ran && wd.ok && wd.badc == 0ull && p.lean && p.settled_fast && p.klazy && p.vv && tile < tile_end) {
-        lean_done = settled_run<POL, REF>(p, lane, tile_end, wd, acc);
+        lean_done = settled_run<POL, REF, CC>(p, lane, tile_end, wd, acc);
         lean_ran = true;
       }
     }
@@ -981,13 +1009,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           if (wd.ok && p.settled_fast && p.klazy && p.vv && !lean_ran) {
             const uint32_t m = meta_of(wd, tile);
             if (((m >> 8) & kVMask) == kVUniform && (m & kPendAllLive) &&
-                settled_tile<POL, REF>(p, tile, lane, m & (kPendAllLive | kHiVirt | 0xFFu), wd, acc))
+                settled_tile<POL, REF, CC>(p, tile, lane, m & (kPendAllLive | kHiVirt | 0xFFu), wd, acc))
               continue;
           }
         }
         TileIn<K, false, true> in;
-        load_tile<K, false, true, POL, false, true>(p, tile, lane, in, &wd);
-        process_tile<K, false, true, POL, true, REF>(p, tile, lane, in, 0u, acc);
+        load_tile<K, false, true, POL, false, true, false, CC>(p, tile, lane, in, &wd);
+        process_tile<K, false, true, POL, true, REF, CC>(p, tile, lane, in, 0u, acc);
       } else if constexpr (MODE == kModeFresh) {
         TileIn<K, false, false> in;
         load_tile<K, false, false, POL, false, true, true>(p, tile, lane, in);
@@ -1041,36 +1069,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     const uint32_t tag = p.round + 1u;
     p.uni_out[p.uni_rank] = tag;
     for (uint32_t r = 0; r < p.push_n; ++r)
-      __hip_atomic_store(p.push_dst[r] + p.uni_off + p.uni_rank, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(peer_ptr(p.push_dst, r) + p.uni_off + p.uni_rank, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
-template <int K, int MODE>
-hipError_t launch_mode(const RoundParams& p, uint32_t grid, hipStream_t s) {
+template <int K, int MODE, bool CC>
+hipError_t launch_mode_cc(const RoundParams& p, uint32_t grid, hipStream_t s) {
   // write-through store policies are built for k = 8 only (the measured workloads)
   const uint32_t pol = (K == 8 && p.store_policy >= 2) ? p.store_policy : (p.plane_nt ? 1u : 0u);
   if constexpr (K == 8 && MODE == kModeWarm) {
     // reference rows (kernels.h): the walking warm mode writes the flags and settled tiles read them
     if (p.rflag_out) {
       if (pol == 1)
-        hipLaunchKernelGGL((k_round_sweep<K, MODE, 1, true>), dim3(grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((k_round_sweep<K, MODE, 1, true, CC>), dim3(grid), dim3(256), 0, s, p);
       else
-        hipLaunchKernelGGL((k_round_sweep<K, MODE, 0, true>), dim3(grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((k_round_sweep<K, MODE, 0, true, CC>), dim3(grid), dim3(256), 0, s, p);
       return hipGetLastError();
     }
   }
   switch (pol) {
-    case 0: hipLaunchKernelGGL((k_round_sweep<K, MODE, 0>), dim3(grid), dim3(256), 0, s, p); break;
-    case 1: hipLaunchKernelGGL((k_round_sweep<K, MODE, 1>), dim3(grid), dim3(256), 0, s, p); break;
+    case 0: hipLaunchKernelGGL((k_round_sweep<K, MODE, 0, false, CC>), dim3(grid), dim3(256), 0, s, p); break;
+    case 1: hipLaunchKernelGGL((k_round_sweep<K, MODE, 1, false, CC>), dim3(grid), dim3(256), 0, s, p); break;
     default:
       if constexpr (K == 8) {
         if (pol == 2)
-          hipLaunchKernelGGL((k_round_sweep<K, MODE, 2>), dim3(grid), dim3(256), 0, s, p);
+          hipLaunchKernelGGL((k_round_sweep<K, MODE, 2, false, CC>), dim3(grid), dim3(256), 0, s, p);
         else
-          hipLaunchKernelGGL((k_round_sweep<K, MODE, 3>), dim3(grid), dim3(256), 0, s, p);
+          hipLaunchKernelGGL((k_round_sweep<K, MODE, 3, false, CC>), dim3(grid), dim3(256), 0, s, p);
       }
   }
   return hipGetLastError();
+}
+
+// CC (changed-word counting and peer pushes, p.count_changed): the walking warm mode at k = 8 (the
+// hot path) has a separate build without it, so that its single-GPU rounds carry none of the
+// prefetched overwritten words' registers; every other mode keeps the runtime switch
+template <int K, int MODE>
+hipError_t launch_mode(const RoundParams& p, uint32_t grid, hipStream_t s) {
+  if constexpr (K == 8 && MODE == kModeWarm) {
+    if (!p.count_changed) return launch_mode_cc<K, MODE, false>(p, grid, s);
+  }
+  return launch_mode_cc<K, MODE, true>(p, grid, s);
 }
 
 template <int K>

@@ -68,13 +68,13 @@ def test_pmc_summary_used_only_when_digest_and_window_match(tmp_path, monkeypatc
 
 
 def test_committed_pmc_summaries_are_well_formed():
-    d = os.path.join(ROOT, "profiles", "r03")
+    d = bench.PMC_DIR
     files = [f for f in os.listdir(d) if f.startswith("pmc_") and f.endswith(".json")] if os.path.isdir(d) else []
     for f in files:
         pm = json.load(open(os.path.join(d, f)))
         assert pm["window"] == "5+20" and len(pm["src_sha"]) == 16
         assert pm["fabric_bytes_per_launch"] > 0 and 0 < pm["issue"]["frac_valu"] < 1
-        assert all(src.startswith("profiles/r03/") for src in pm["source"].values())
+        assert all(src.startswith(os.path.relpath(d, ROOT) + "/") for src in pm["source"].values())
 
 
 def test_cpu_baseline_threads_respect_the_quota():

@@ -86,17 +86,17 @@ for s in "$@"; do
     prof) step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- \
             python3 bench.py --no-cpu-baseline ;;
     pmcb_sq) step pmcb_sq_${WL:-c4} 600 timeout -s KILL 500 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
-            --output-format csv -d $OUT/pmcb_sq_${WL:-c4} -o bench -- python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary ;;
+            --output-format csv -d $OUT/pmcb_sq_${WL:-c4} -o bench -- python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary --no-exchange-pass ;;
     pmcb_fetch) step pmcb_fetch_${WL:-c4} 600 timeout -s KILL 500 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmcb_fetch_${WL:-c4} -o bench -- \
-            python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary ;;
+            python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary --no-exchange-pass ;;
     pmcb_write) step pmcb_write_${WL:-c4} 600 timeout -s KILL 500 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmcb_write_${WL:-c4} -o bench -- \
-            python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary ;;
+            python3 bench.py --workload ${WL:-c4} --no-cpu-baseline --no-secondary --no-exchange-pass ;;
     pmcb_sum) step pmcb_sum_${WL:-c4} 300 python tools/pmc_bench.py --workload ${WL:-c4} --sq $OUT/pmcb_sq_${WL:-c4} --fetch $OUT/pmcb_fetch_${WL:-c4} \
             --write $OUT/pmcb_write_${WL:-c4} --calib-fetch $OUT/calib_fetch --calib-write $OUT/calib_write ${PMC_LAUNCHES:+--launches $PMC_LAUNCHES} ${PMC_REPLAY:+--replay} --out $OUT/pmc_${WL:-c4}.json ;;
     pmc_fetch) step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o bench -- \
-            python3 bench.py --no-cpu-baseline --no-secondary ;;
+            python3 bench.py --no-cpu-baseline --no-secondary --no-exchange-pass ;;
     pmc_write) step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o bench -- \
-            python3 bench.py --no-cpu-baseline --no-secondary ;;
+            python3 bench.py --no-cpu-baseline --no-secondary --no-exchange-pass ;;
     calib_fetch) step calib_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib_fetch -o calib -- \
             go-avalanche_amd/bin/pmc_calib ;;
     calib_write) step calib_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/calib_write -o calib -- \
@@ -137,8 +137,8 @@ for s in "$@"; do
     probe_tpw) step probe_tpw 600 bash -c 'for w in c4 c3; do for o in "tiles_per_wave=4" "tiles_per_wave=6" "tiles_per_wave=8" "tiles_per_wave=3"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o | tail -1 | grep -o "kernel_ms_total.*"; done; done' ;;
     c4ptests) step c4ptests 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread -k "c4p" ;;
     hostcpu) step hostcpu 300 bash -c 'cat /sys/fs/cgroup/cpu.max; nproc; python -c "import bench, json; print(json.dumps(bench.host_cpus()))"; for t in 16 32 64 128; do python tools/cpu_scaling.py --threads $t; done' ;;
-    bench_c4p) step bench_c4p 900 python bench.py --workload c4p --no-cpu-baseline --no-secondary ;;
-    bench_c4pb) step bench_c4pb 900 python bench.py --workload c4pb --no-cpu-baseline --no-secondary ;;
+    bench_c4p) step bench_c4p 900 python bench.py --workload c4p --no-cpu-baseline --no-secondary --no-exchange-pass ;;
+    bench_c4pb) step bench_c4pb 900 python bench.py --workload c4pb --no-cpu-baseline --no-secondary --no-exchange-pass ;;
     probe_lean) step probe_lean 600 bash -c 'for w in c4 c5; do for o in "settled_lean=1" "settled_lean=0"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
     fullc4) step fullc4 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread -k "c4_fullsize" ;;
     probe_ref2) step probe_ref2 600 bash -c 'for w in c4 c5; do for o in "ref_rows=1" "ref_rows=0"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o; done; done' ;;
@@ -166,6 +166,8 @@ for s in "$@"; do
     barrier4) step barrier4 400 bash -c 'python tools/barrier_cost.py --world 2 --json gpurun_out/barrier2_small.json && python tools/barrier_cost.py --world 2 --nodes 131072 --json gpurun_out/barrier2_big.json && python tools/barrier_cost.py --world 4 --nodes 131072 --json gpurun_out/barrier4_big.json && python tools/barrier_cost.py --world 2 --nodes 1000000 --rounds 40 --json gpurun_out/barrier2_c4.json' ;;
     abr3) step abr3 600 bash -c 'for w in c4 c4p c4pb; do for v in new nohoist r3; do echo "== $w $v"; if [ $v = new ]; then python tools/round_probe.py --workload $w | tail -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w | tail -1; fi; done; done; for v in new r3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
     ablate) step ablate 600 bash -c 'for w in c4 c4p; do for o in "ablate_phase=0" "ablate_phase=1" "ablate_phase=2" "ablate_phase=4" "ablate_phase=16" "ablate_emit=1" "ablate_phase=7 --option ablate_emit=1"; do echo "== $w $o"; AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_ablate.so python tools/round_probe.py --workload $w --rounds 8 --option $o | grep -v "^{\"workload"; done; done' ;;
+    quick) step quick 900 python -u -m pytest tests/test_gpu_peer_push.py tests/test_gpu_parity.py tests/test_gpu_uniform_rows.py tests/test_gpu_count_lazy.py tests/test_gpu_virtual_votes.py tests/test_gpu_fresh.py tests/test_gpu_replay_fused.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    abcc) step abcc 600 bash -c 'for w in c4 c4p; do for v in new noccpf; do for cc in 0 1; do echo "== $w $v count_changed=$cc"; if [ $v = new ]; then python tools/round_probe.py --workload $w --option count_changed=$cc | tail -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w --option count_changed=$cc | tail -1; fi; done; done; done; python tools/round_probe.py --workload c4pb | tail -1' ;;
     shardmodel) step shardmodel 600 bash -c 'python tools/shard_model.py --workload c4 --json gpurun_out/shard_model_c4.json && python tools/shard_model.py --workload c4p --json gpurun_out/shard_model_c4p.json' ;;
     fused4) step fused4 600 python -u -m pytest tests/test_gpu_replay_fused.py tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     peer4) step peer4 600 python -u -m pytest tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;

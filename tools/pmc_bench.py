@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """PMC summary of exactly the bench window, for bench.py's roofline
-(profiles/r03/pmc_<workload>.json, used only while its src_sha matches the
+(profiles/r04/pmc_<workload>.json, used only while its src_sha matches the
 kernel sources): window averages and one row per roofline-pass step.
 
 bench.py runs, per workload: one untimed device warm-up epoch, goto(warmup),
@@ -10,7 +10,7 @@ last `steps` round-kernel dispatches of the process (run with --no-secondary),
 so this averages the counters over exactly those dispatches.
 
 Inputs are rocprofv3 --pmc passes of `python3 bench.py --workload W
---no-cpu-baseline --no-secondary --steps S --warmup W` (one pass per counter
+--no-cpu-baseline --no-secondary --no-exchange-pass --steps S --warmup W` (one pass per counter
 group, MI355X_MICROARCH.md §HBM / the 8-SQ-counter limit):
   --sq    SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR
           SQ_INSTS_LDS SQ_WAVES SQ_WAIT_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
