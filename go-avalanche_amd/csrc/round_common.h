@@ -536,6 +536,23 @@ __device__ __forceinline__ uint32_t emit_updates_flat(const RoundParams& p, uint
 // its updates into the payload in registers. Statuses as emit_updates_flat (A
 // after slot j = A_final, flipped back for the first of a record's two
 // updates; vote.go:77-91). Returns the bytes stored (wave-uniform).
+// E[j] for a per-lane slot j: a 3-level mux at K = 8 (7 selects on 3 masks instead of a 7-step
+// compare-and-select chain), the chain otherwise.
+template <int K>
+__device__ __forceinline__ uint32_t select_slot(const uint32_t (&E)[K], uint32_t j) {
+  if constexpr (K == 8) {
+    const bool b0 = (j & 1u) != 0u, b1 = (j & 2u) != 0u, b2 = (j & 4u) != 0u;
+    const uint32_t a0 = b0 ? E[1] : E[0], a1 = b0 ? E[3] : E[2], a2 = b0 ? E[5] : E[4], a3 = b0 ? E[7] : E[6];
+    const uint32_t c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
+    return b2 ? c1 : c0;
+  } else {
+    uint32_t cur = E[0];
+#pragma unroll
+    for (int t = 1; t < K; ++t) cur = j == (uint32_t)t ? E[t] : cur;
+    return cur;
+  }
+}
+
 // The reservation half of emit_updates_med: per-lane update count, the wave's
 // per-kind totals and the three reserving atomics, issued but not waited for
 // (their results are read in emit_store_med). A caller that issues it before
@@ -555,7 +572,7 @@ __device__ __forceinline__ uint32_t lane_updates8(const uint32_t* E, int K) {
 }
 
 template <int K>
-__device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32_t wave_id, uint32_t lane,
+__device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32_t shard, uint32_t lane,
                                                     const uint32_t (&E)[K], uint32_t& updates) {
   EmitRes r;
   uint32_t any = 0;
@@ -573,7 +590,6 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
   r.tot_s = (uint32_t)__popcll(__ballot(single));
   updates += wave_sum(cnt);
   if (p.ablate_emit == 1u) return r;  // diagnostics: the cost of the round without its log stores
-  const uint32_t shard = wave_id % p.log_shards;
   // one atomic instruction, lanes 0 / 1 / 2 reserving the singles / medium / dense runs
   const uint32_t want = lane == 0 ? r.tot_s : lane == 1 ? r.tot_m : lane == 2 ? r.tot_d : 0u;
   uint32_t* const ctr = lane == 0 ? p.log_count : lane == 1 ? p.mlog_count : p.dlog_count;
@@ -584,7 +600,7 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
 // The store half: every lane with updates stores its one entry at its rank among the wave's lanes
 // of its kind (see emit_updates_med). Returns the bytes stored (wave-uniform).
 template <int K>
-__device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_t wave_id, uint32_t lane,
+__device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_t shard, uint32_t lane,
                                                    uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
                                                    uint32_t A_final, uint32_t died, const EmitRes& r,
                                                    uint32_t round_rel) {
@@ -595,7 +611,6 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
   const bool dense = cnt >= dmin, med = !dense && cnt >= 2u, single = cnt == 1u;
   const uint64_t dl = __ballot(dense), ml = __ballot(med), sl = __ballot(single);
   const uint32_t tot_d = r.tot_d, tot_m = r.tot_m, tot_s = r.tot_s;
-  const uint32_t shard = wave_id % p.log_shards;
   const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 0);
   const uint32_t mbase = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 1);
   const uint32_t dbase = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 2);
@@ -645,9 +660,7 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
         if (cur == 0u) {  // next slot with updates
           j = (uint32_t)__ffs(nz) - 1u;
           nz &= nz - 1u;
-          cur = E[0];
-#pragma unroll
-          for (int t = 1; t < K; ++t) cur = j == (uint32_t)t ? E[t] : cur;
+          cur = select_slot<K>(E, j);
         }
         const uint32_t bit = (uint32_t)__ffs(cur) - 1u;
         cur &= cur - 1u;
@@ -681,12 +694,12 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
 // after slot j = A_final, flipped back for the first of a record's two
 // updates; vote.go:77-91). Returns the bytes stored (wave-uniform).
 template <int K>
-__device__ __forceinline__ uint32_t emit_updates_med(const RoundParams& p, uint32_t wave_id, uint32_t lane,
+__device__ __forceinline__ uint32_t emit_updates_med(const RoundParams& p, uint32_t shard, uint32_t lane,
                                                      uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
                                                      uint32_t A_final, uint32_t died, uint32_t& updates,
                                                      uint32_t round_rel) {
-  const EmitRes r = emit_reserve_med<K>(p, wave_id, lane, E, updates);
-  return emit_store_med<K>(p, wave_id, lane, node, tbase, E, A_final, died, r, round_rel);
+  const EmitRes r = emit_reserve_med<K>(p, shard, lane, E, updates);
+  return emit_store_med<K>(p, shard, lane, node, tbase, E, A_final, died, r, round_rel);
 }
 
 __device__ __forceinline__ void count_stats(const RoundParams& p, uint32_t wave_id, uint32_t lane, uint32_t applied,

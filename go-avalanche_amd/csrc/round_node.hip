@@ -250,8 +250,12 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
   const uint32_t tl = g & 63u;
   u32x4* const grp = reinterpret_cast<u32x4*>(tp) + tl;
   const u32x4 k1 = pld4<NT>(grp + 192);
-  uint32_t A = pld<NT>(tp + 1536u + tl);
   const uint32_t vmask = active ? p.valid[bc] : 0u;
+  // k_replay_fast ran this launch's rounds for nodes whose first 128 lanes hold 4096 live, valid
+  // records (the poll set is exactly those) and published their other lanes' words: such a node's
+  // workgroup leaves before any other load (workgroup-uniform)
+  if (p.replay_fast && p.BL >= kMaxPoll / 32u && __syncthreads_and(!early || (~k1[3] & vmask) == ~0u)) return;
+  uint32_t A = pld<NT>(tp + 1536u + tl);
   u32x4 v0 = u32x4{0u, 0u, 0u, 0u}, v1 = v0, k0 = v0;
   uint32_t C[8];
 #pragma unroll
@@ -436,11 +440,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   uint32_t* const tp = p.planes + (size_t)(g >> 6) * (kPlanes * 64u);
   const uint32_t tl = g & 63u;
   u32x4* const grp = reinterpret_cast<u32x4*>(tp) + tl;
+  // every load of the launch's start issued at once (planes, the first two rounds' replayed votes),
+  // before the eligibility barrier: one memory latency instead of three in a row (an ineligible node,
+  // rare, has loaded for nothing and runs in k_replay_node)
   const u32x4 k1 = pld4<NT>(grp + 192);
   const uint32_t vmask = p.valid[b];
-  // eligibility: every record of lanes 0..127 live and valid
-  const bool all = __syncthreads_and((~k1[3] & vmask) == ~0u) != 0;
-  if (!all) return;  // workgroup-uniform: k_replay_node runs the node
   uint32_t A = pld<NT>(tp + 1536u + tl);
   const u32x4 v0 = pld4<NT>(grp), v1 = pld4<NT>(grp + 64), k0 = pld4<NT>(grp + 128);
   uint32_t V[8], C[8], Kp[8];
@@ -453,10 +457,29 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
+  const uint32_t R = p.fuse_rounds;
+  uint32_t w[K], cw[K], w1[K], cw1[K];
+  replay_load<K>(p.replay, g, w, cw);
+  if (R > 1u) replay_load<K>(p.replay + p.replay_stride, g, w1, cw1);
+  // eligibility: every record of lanes 0..127 live and valid
+  const bool all = __syncthreads_and((~k1[3] & vmask) == ~0u) != 0;
+  if (!all) return;  // workgroup-uniform: k_replay_node runs the node
   const uint32_t wave_id = blockIdx.x * 2u + wave;
   const uint32_t prow = node * p.PS + b;
   const bool byz = is_byz(p.byz, node);
-  const uint32_t R = p.fuse_rounds;
+  // the node's other lanes take no vote in the launch (the poll set is lanes 0..127): their records
+  // are unchanged, so their published words for the launch's last three rounds are their A planes
+  uint32_t pub_bytes = 0u;
+  {
+    const uint32_t r0 = R > 3u ? R - 3u : 0u;
+    for (uint32_t lb = b + kMaxPoll / 32u; lb < p.BL; lb += kMaxPoll / 32u) {
+      const uint32_t go = nl * p.BL + lb;
+      const uint32_t Ao = pld<NT>(p.planes + (size_t)(go >> 6) * (kPlanes * 64u) + 1536u + (go & 63u));
+      for (uint32_t r = r0; r < R; ++r)
+        p.pref_ring[(p.ring_next + r) % 3u][node * p.PS + lb] = byz ? byz_pattern(p.round + r + 1u) : Ao;
+      pub_bytes += 4u + 4u * (R - r0);
+    }
+  }
   // largest count of the node (bit by bit from the top, as k_replay_node): no record can reach 120
   // before round J, so those rounds need no workgroup check
   uint32_t hi = 0u;
@@ -478,17 +501,15 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   const uint32_t maxc = max(wmax[0], wmax[1]);
   const uint32_t J = maxc >= 120u ? 0u : (120u - maxc + (uint32_t)K - 1u) / (uint32_t)K;
   uint32_t done = R, applied = 0u, upd = 0u, emitted = 0u, pubs = 0u;
-  // the replayed votes are prefetched two rounds ahead (w: this round, w1: the next one): a round's
-  // compute is shorter than a load's latency with two waves per SIMD
-  uint32_t w[K], cw[K], w1[K], cw1[K];
-  replay_load<K>(p.replay, g, w, cw);
-  if (R > 1u) replay_load<K>(p.replay + p.replay_stride, g, w1, cw1);
+  // the replayed votes are prefetched two rounds ahead (w: this round, w1: the next one, loaded
+  // above): a round's compute is shorter than a load's latency with two waves per SIMD
   // StatusUpdates (k = 8: medium records, one entry per lane): round r's log space is reserved at the
   // end of round r and its entries stored after round r + 1's slot network, so the reserving atomics'
   // round trip overlaps a round of compute instead of stalling every round
   EmitRes pend{};
   uint32_t Epend[K], Apend = 0u;
   bool have_pend = false;
+  const uint32_t shard = wave_id % p.log_shards;  // once (a runtime modulo is a long sequence)
   for (uint32_t r = 0; r < R; ++r) {
     if (r >= J) {  // a record with count >= 120 may finalize (and leave the poll set) this round
       const uint32_t nearfin = Kp[6] & Kp[5] & Kp[4] & Kp[3];
@@ -535,9 +556,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       ++pubs;
     }
     if constexpr (K == 8) {
-      const EmitRes cur = emit_reserve_med<K>(p, wave_id, lane, E, upd);
+      const EmitRes cur = emit_reserve_med<K>(p, shard, lane, E, upd);
       if (have_pend)
-        emitted += emit_store_med<K>(p, wave_id, lane, node, p.t0 + b * 32u, Epend, Apend, 0u, pend, p.round_rel + r - 1u);
+        emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Epend, Apend, 0u, pend, p.round_rel + r - 1u);
 #pragma unroll
       for (int j = 0; j < K; ++j) Epend[j] = E[j];
       Apend = A;
@@ -558,7 +579,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
   if constexpr (K == 8) {  // the last round run's entries (round done - 1)
     if (have_pend)
-      emitted += emit_store_med<K>(p, wave_id, lane, node, p.t0 + b * 32u, Epend, Apend, 0u, pend, p.round_rel + done - 1u);
+      emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Epend, Apend, 0u, pend, p.round_rel + done - 1u);
   }
   if (done < R && b == 0) p.node_flags[nl] = done + 1u;  // the exact pass takes rounds done..R-1
   if (done > 0u) {
@@ -573,7 +594,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   // bytes: 25 planes read once and written once (if a round ran), 8 B per replayed vote word pair
   // per round, the published words
   const uint32_t lane_bytes = kPlanes * 4u + 8u * K * done + 4u * pubs + (done > 0u ? kPlanes * 4u : 0u);
-  count_stats(p, wave_id, lane, applied, true, lane_bytes, emitted, upd, 0u);
+  count_stats(p, wave_id, lane, applied, true, lane_bytes, emitted + wave_sum(pub_bytes), upd, 0u);
 }
 
 template <int K, int MAXT>

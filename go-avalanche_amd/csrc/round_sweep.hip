@@ -48,8 +48,10 @@
 #endif
 // A/B build knob: in rounds that count changed words (peer pushes), the overwritten published words
 // are loaded ahead of time with the tile (1) or by each publish (0)
+// (0: the prefetched words' registers spilled in the counting build: C4 epoch 7.40 ms against 5.95,
+// C4p 24.0 against 15.4 with count_changed on, profiles/r04/ab_count_changed.log)
 #ifndef AVK_CC_PREFETCH
-#define AVK_CC_PREFETCH 1
+#define AVK_CC_PREFETCH 0
 #endif
 
 namespace avk {
@@ -65,6 +67,7 @@ struct SweepAcc {
   // wave-uniform (p.count_changed): published words that differ from the word they overwrite (bits 0-15)
   // and the 16-lane groups holding one (bits 16-31: 64-B row segments when PS == BL, a multiple of 16)
   uint32_t changed = 0;
+  uint32_t shard = 0;  // wave-uniform: this wave's log / counter shard (wave index % log_shards)
 };
 
 // Peer r's replica pointer from the engine's device table: a scalar load through the constant address
@@ -81,13 +84,17 @@ __device__ __forceinline__ uint32_t* peer_ptr(uint32_t* const* tbl, uint32_t r) 
 // (system-scope write-through stores over xGMI; the barrier after the round orders them before any
 // peer reads them). Changed words are counted when p.count_changed (the push volume),
 // per wave by ballot (a scalar: a per-lane counter live across the tile loop spilled).
-// `old`: the overwritten word, loaded by the caller ahead of time (p.count_changed only): a load here
-// would put its full latency on the tile's dependence chain.
+// `old`: the overwritten word when the caller knows it (`known`: loaded ahead of time, or implied by
+// the tile's history, below); else it is loaded here (its latency then sits on the tile's chain).
+// A tile whose count steps were deferred in the two rounds before this one (kpend >= 2) kept its
+// accepted plane through them, so an honest row it publishes unchanged this round equals the
+// snapshot being overwritten (written three rounds ago): no load, no push; a Byzantine row's word
+// there is the pattern of that snapshot.
 template <int POL, bool CC>
 __device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uint32_t pub, uint32_t old,
-                                        uint32_t& changed) {
+                                        uint32_t& changed, bool known = false) {
   if (CC && p.count_changed) {
-    if (!AVK_CC_PREFETCH) old = p.pref_out[prow];
+    if (!known && !AVK_CC_PREFETCH) old = p.pref_out[prow];
     const unsigned long long m = __ballot(pub != old);
     const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
     const uint32_t groups = ((lo & 0xFFFFu) ? 1u : 0u) + ((lo >> 16) ? 1u : 0u) + ((hi & 0xFFFFu) ? 1u : 0u) + ((hi >> 16) ? 1u : 0u);
@@ -500,7 +507,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   // StatusUpdate log reservation (k = 8) before this tile's plane and published-word stores, so that
   // reading the atomics' results waits for them alone, not for those stores (round_common.h)
   EmitRes er{};
-  if constexpr (K == 8) er = emit_reserve_med<K>(p, tile, lane, E, acc.updates);
+  if constexpr (K == 8) er = emit_reserve_med<K>(p, acc.shard, lane, E, acc.updates);
 #endif
   {
     uint32_t cy = 0u;
@@ -537,7 +544,9 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^31
     const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
     if (p.uni_out) acc.umis |= pub != in.uref ? 1u : 0u;  // uniform rows (kernels.h)
-    publish<POL, CC>(p, prow, pub, in.old, acc.changed);
+    const bool known = AVK_CC_PREFETCH || (kdefer && pend >= 2u);  // (publish)
+    publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? in.old : (is_byz(p.byz, node) ? byz_pattern(p.round - 2u) : pub),
+                     acc.changed, known);
     // a record deleted this round keeps the vote/consider planes stored
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
@@ -576,9 +585,9 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   uint32_t emitted;
   if constexpr (K == 8)
 #if AVK_EMIT_HOIST
-    emitted = emit_store_med<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, er, p.round_rel);
+    emitted = emit_store_med<K>(p, acc.shard, lane, node, p.t0 + b * 32u, E, A, died, er, p.round_rel);
 #else
-    emitted = emit_updates_med<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, p.round_rel);
+    emitted = emit_updates_med<K>(p, acc.shard, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, p.round_rel);
 #endif
   else
     emitted = emit_updates<K>(p, tile, lane, node, p.t0 + b * 32u, E, A, died, acc.updates);
@@ -665,7 +674,9 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
   if (active) {
     if (p.uni_out) acc.umis |= pub != uref ? 1u : 0u;
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-    publish<POL, CC>(p, prow, pub, old, acc.changed);
+    const bool known = AVK_CC_PREFETCH || (kw & 0xFFu) >= 2u;  // (publish)
+    publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? old : (is_byz(p.byz, node) ? byz_pattern(p.round - 2u) : pub),
+                     acc.changed, known);
   }
   if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, p.pref_in[p.ref_node * p.PS + (active ? b : 0u)]);
   if (lane == 0) p.kpend[tile] = ((kw & 0xFFu) + 1u) | kPendAllLive | (kw & kHiVirt);
@@ -768,7 +779,9 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
     if (active) {
       umis |= pub != rin ? 1u : 0u;
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-      publish<POL, CC>(p, prow, pub, old, acc.changed);
+      const bool known = AVK_CC_PREFETCH || (m & 0xFFu) >= 2u;  // (publish)
+      publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? old : (((byzm >> rel) & 1ull) ? byz_pattern(p.round - 2u) : pub),
+                       acc.changed, known);
     }
     if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, rin);
     done |= 1u << i;
@@ -851,7 +864,12 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
     if (active) {
       umis |= pub != rin ? 1u : 0u;
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
-      publish<POL, CC>(p, prow, pub, Ov[i], acc.changed);
+      // kpend >= 2: this settled tile's accepted plane is unchanged since the snapshot being
+      // overwritten (publish): honest rows publish that word again, Byzantine rows its pattern's
+      const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, (int)i);
+      const bool known = AVK_CC_PREFETCH || (m & 0xFFu) >= 2u;
+      const uint32_t old = AVK_CC_PREFETCH ? Ov[i] : (((byzm >> (nl - nlA)) & 1ull) ? byz_pattern(p.round - 2u) : pub);
+      publish<POL, CC>(p, prow, pub, old, acc.changed, known);
     }
     done |= 1u << i;
     applied += 8u * (uint32_t)__popc(P0);
@@ -887,6 +905,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   const uint32_t nwaves = gridDim.x * 4u;
   const uint32_t tiles = p.Lpad >> 6;
   SweepAcc acc;
+  acc.shard = wave0 % p.log_shards;  // once per wave (a runtime modulo is a ~20-instruction sequence)
   // uniform rows (kernels.h): no rank's slot of pref_in carries this round's tag
   bool uniform = p.uni_in != nullptr;
   if (uniform)
@@ -1052,7 +1071,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   const unsigned long long by = (unsigned long long)wave_sum(acc.lane_bytes) + acc.emitted_bytes;
   const unsigned long long rr = wave_sum(acc.reread);
   if (lane == 0) {
-    const uint32_t shard = wave0 % p.log_shards;
+    const uint32_t shard = acc.shard;
     if (s) atomicAdd(&p.applied[shard], s);
     if (f) atomicAdd(&p.finalized[shard], f);
     if (by) atomicAdd(&p.bytes[shard], by);
@@ -1060,8 +1079,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     if (acc.updates) atomicAdd(&p.upd_count[shard], acc.updates);
   }
   if (p.count_changed && lane == 0 && acc.changed) {
-    atomicAdd(&p.changed[wave0 % p.log_shards], (unsigned long long)(acc.changed & 0xFFFFu));
-    atomicAdd(&p.changed[kLogShards + wave0 % p.log_shards], (unsigned long long)(acc.changed >> 16));
+    atomicAdd(&p.changed[acc.shard], (unsigned long long)(acc.changed & 0xFFFFu));
+    atomicAdd(&p.changed[kLogShards + acc.shard], (unsigned long long)(acc.changed >> 16));
   }
   if (p.uni_out && __ballot(acc.umis != 0u) != 0ull && lane == 0) {
     // some word this wave published differs from the reference row: tag the output snapshot's slot
