@@ -469,16 +469,15 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   const bool byz = is_byz(p.byz, node);
   // the node's other lanes take no vote in the launch (the poll set is lanes 0..127): their records
   // are unchanged, so their published words for the launch's last three rounds are their A planes
-  uint32_t pub_bytes = 0u;
-  {
-    const uint32_t r0 = R > 3u ? R - 3u : 0u;
-    for (uint32_t lb = b + kMaxPoll / 32u; lb < p.BL; lb += kMaxPoll / 32u) {
-      const uint32_t go = nl * p.BL + lb;
-      const uint32_t Ao = pld<NT>(p.planes + (size_t)(go >> 6) * (kPlanes * 64u) + 1536u + (go & 63u));
-      for (uint32_t r = r0; r < R; ++r)
-        p.pref_ring[(p.ring_next + r) % 3u][node * p.PS + lb] = byz ? byz_pattern(p.round + r + 1u) : Ao;
-      pub_bytes += 4u + 4u * (R - r0);
-    }
+  // (loaded here, stored after the round loop: no load latency before the loop)
+  constexpr uint32_t kOther = 2u;  // other lanes per thread: BL <= 3 * 128 (M <= 12288; more take k_replay_node's
+                                   // per-lane loop below)
+  uint32_t Aother[kOther];
+#pragma unroll
+  for (uint32_t q = 0; q < kOther; ++q) {
+    const uint32_t lb = b + (q + 1u) * (kMaxPoll / 32u);
+    const uint32_t go = nl * p.BL + lb;
+    Aother[q] = lb < p.BL ? pld<NT>(p.planes + (size_t)(go >> 6) * (kPlanes * 64u) + 1536u + (go & 63u)) : 0u;
   }
   // largest count of the node (bit by bit from the top, as k_replay_node): no record can reach 120
   // before round J, so those rounds need no workgroup check
@@ -590,6 +589,21 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
     pst4<NT>(grp + 128, u32x4{Kp[0], Kp[1], Kp[2], Kp[3]});
     pst4<NT>(grp + 192, u32x4{Kp[4], Kp[5], Kp[6], Kp[7]});
     pst<NT>(tp + 1536u + tl, A);
+  }
+  // the other lanes' published words (see above); lanes past 3 * 128 (BL > 384) one by one
+  uint32_t pub_bytes = 0u;
+  {
+    const uint32_t r0 = R > 3u ? R - 3u : 0u;
+    for (uint32_t lb = b + kMaxPoll / 32u, q = 0; lb < p.BL; lb += kMaxPoll / 32u, ++q) {
+      uint32_t Ao = q == 0u ? Aother[0] : Aother[1];
+      if (q >= kOther) {
+        const uint32_t go = nl * p.BL + lb;
+        Ao = pld<NT>(p.planes + (size_t)(go >> 6) * (kPlanes * 64u) + 1536u + (go & 63u));
+      }
+      for (uint32_t r = r0; r < R; ++r)
+        p.pref_ring[(p.ring_next + r) % 3u][node * p.PS + lb] = byz ? byz_pattern(p.round + r + 1u) : Ao;
+      pub_bytes += 4u + 4u * (R - r0);
+    }
   }
   // bytes: 25 planes read once and written once (if a round ran), 8 B per replayed vote word pair
   // per round, the published words

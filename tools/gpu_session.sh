@@ -167,6 +167,11 @@ for s in "$@"; do
     abr3) step abr3 600 bash -c 'for w in c4 c4p c4pb; do for v in new nohoist r3; do echo "== $w $v"; if [ $v = new ]; then python tools/round_probe.py --workload $w | tail -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w | tail -1; fi; done; done; for v in new r3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
     ablate) step ablate 600 bash -c 'for w in c4 c4p; do for o in "ablate_phase=0" "ablate_phase=1" "ablate_phase=2" "ablate_phase=4" "ablate_phase=16" "ablate_emit=1" "ablate_phase=7 --option ablate_emit=1"; do echo "== $w $o"; AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_ablate.so python tools/round_probe.py --workload $w --rounds 8 --option $o | grep -v "^{\"workload"; done; done' ;;
     quick) step quick 900 python -u -m pytest tests/test_gpu_peer_push.py tests/test_gpu_parity.py tests/test_gpu_uniform_rows.py tests/test_gpu_count_lazy.py tests/test_gpu_virtual_votes.py tests/test_gpu_fresh.py tests/test_gpu_replay_fused.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    tshard) step tshard 600 bash -c 'for o in tiles_per_wave=4 tiles_per_wave=8 tiles_per_wave=16; do python tools/shard_model.py --workload c4 --kinds targets --no-one-gpu --ranks 2,4,8 --option $o --json gpurun_out/tshard_c4_$o.json | tail -3; done' ;;
+    shardmodel2) step shardmodel2 600 bash -c 'python tools/shard_model.py --workload c4 --json gpurun_out/shard_model_c4.json && python tools/shard_model.py --workload c4p --json gpurun_out/shard_model_c4p.json && python tools/shard_model.py --workload c4pb --json gpurun_out/shard_model_c4pb.json' ;;
+    c2ab) step c2ab 300 bash -c 'for v in new s3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
+    reh2pb) step reh2pb 600 python bench.py --gpus 2 --rehearse-one-gpu --workload c4pb --no-secondary --detail gpurun_out/rehearse2_c4pb_detail.json ;;
+    reh2t) step reh2t 600 python bench.py --gpus 2 --rehearse-one-gpu --shard targets --no-secondary --detail gpurun_out/rehearse2_targets_detail.json ;;
     abs3) step abs3 900 bash -c 'for w in c4 c4p c4pb c3; do for v in new s3; do for cc in 0 1; do echo "== $w $v count_changed=$cc"; if [ $v = new ]; then python tools/round_probe.py --workload $w --option count_changed=$cc | tail -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w --option count_changed=$cc | tail -1; fi; done; done; done; for v in new s3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
     profc2b) step profc2b 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc2b -o c2 -- python3 bench.py --workload c2 --no-cpu-baseline --no-secondary ;;
     abcc) step abcc 600 bash -c 'for w in c4 c4p; do for v in new noccpf; do for cc in 0 1; do echo "== $w $v count_changed=$cc"; if [ $v = new ]; then python tools/round_probe.py --workload $w --option count_changed=$cc | tail -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w --option count_changed=$cc | tail -1; fi; done; done; done; python tools/round_probe.py --workload c4pb | tail -1' ;;

@@ -73,32 +73,47 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ranks", default="2,4,8")
     ap.add_argument("--barrier-us", type=float, default=6.0)
+    ap.add_argument("--option", action="append", default=[], help="name=value on the rank-0 share engines")
+    ap.add_argument("--kinds", default="nodes,targets")
+    ap.add_argument("--no-one-gpu", action="store_true", help="skip the whole-network pass (projections need it)")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
     N, M, K, init_mode, init_param, byz, replay, desc = WORKLOADS[args.workload]
     assert not replay, "sim workloads only"
     init = (init_mode, init_param)
     cap = min(int(1.25 * N * M) + (1 << 20), (1 << 31) - 1)
-    e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz, log_capacity=cap)
-    window_rounds(e, init, args.warmup, args.steps)  # device warm-up
-    one = window_rounds(e, init, args.warmup, args.steps, count_changed=True)
-    e.close()
+    if args.no_one_gpu:
+        one = [{"round": (args.warmup + i) % EPOCH, "ms": 0.0, "words": 0, "segments": 0} for i in range(args.steps)]
+    else:
+        e = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz, log_capacity=cap)
+        window_rounds(e, init, args.warmup, args.steps)  # device warm-up
+        plain = window_rounds(e, init, args.warmup, args.steps)
+        one = window_rounds(e, init, args.warmup, args.steps, count_changed=True)
+        e.close()
+        for a, b in zip(one, plain):  # kernel time without the counting; words / segments from the counting pass
+            a["ms_counting"], a["ms"] = a["ms"], b["ms"]
     t1 = sum(r["ms"] for r in one)
     out = {"workload": desc, "window": f"{args.warmup}+{args.steps}", "one_gpu": one, "one_gpu_ms": t1,
            "link_GBs_per_direction": XGMI_LINK_GBS, "barrier_us": args.barrier_us, "ranks": {}}
     print(json.dumps({"one_gpu_ms": t1}), flush=True)
     for g in [int(x) for x in args.ranks.split(",")]:
-        en = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz, node_range=sharding.node_shard(N, g, 0),
-                          log_capacity=max(1 << 24, cap // g))
-        en.set_option("unsynced_shard", 1)
-        window_rounds(en, init, args.warmup, args.steps)
-        ns = window_rounds(en, init, args.warmup, args.steps)
-        en.close()
-        et = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz,
-                          target_range=sharding.target_shard(M, g, 0), log_capacity=max(1 << 24, cap // g))
-        window_rounds(et, init, args.warmup, args.steps)
-        ts = window_rounds(et, init, args.warmup, args.steps)
-        et.close()
+        def share(kind):
+            kw = dict(node_range=sharding.node_shard(N, g, 0)) if kind == "nodes" else \
+                dict(target_range=sharding.target_shard(M, g, 0))
+            if kind not in args.kinds.split(","):
+                return [{"ms": 0.0} for _ in range(args.steps)]
+            en = avhip.Engine(N, M, k=K, seed=0xA7A1A9C4, byz_threshold=byz, log_capacity=max(1 << 24, cap // g), **kw)
+            if kind == "nodes":
+                en.set_option("unsynced_shard", 1)
+            for o in args.option:
+                name, v = o.split("=")
+                en.set_option(name, int(v))
+            window_rounds(en, init, args.warmup, args.steps)
+            rows = window_rounds(en, init, args.warmup, args.steps)
+            en.close()
+            return rows
+
+        ns, ts = share("nodes"), share("targets")
         per = []
         for a, b, c in zip(one, ns, ts):
             push_ms = a["segments"] / g * 64.0 / (XGMI_LINK_GBS * 1e9) * 1e3
@@ -106,10 +121,11 @@ def main():
                         "node_ms": max(b["ms"], push_ms) + args.barrier_us * 1e-3, "target_ms": c["ms"]})
         tn = sum(p["node_ms"] for p in per)
         tt = sum(p["target_ms"] for p in per)
+        eff = (lambda t: t1 / (g * t) if t > 0 and t1 > 0 else None)
         out["ranks"][g] = {"per_round": per, "node_push_ms": tn, "target_ms": tt,
-                           "node_push_efficiency": t1 / (g * tn), "target_efficiency": t1 / (g * tt)}
-        print(json.dumps({"g": g, "node_push_ms": tn, "target_ms": tt, "eff_node": t1 / (g * tn),
-                          "eff_target": t1 / (g * tt)}), flush=True)
+                           "node_push_efficiency": eff(tn), "target_efficiency": eff(tt)}
+        print(json.dumps({"g": g, "node_push_ms": tn, "target_ms": tt, "eff_node": eff(tn), "eff_target": eff(tt),
+                          "options": args.option}), flush=True)
     if args.json:
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
