@@ -838,15 +838,63 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
   }
   uint32_t Av[kUniRun], Ov[kUniRun];
 #pragma unroll
-  for (uint32_t i = 0; i < kUniRun; ++i)
-    Av[i] = (cand >> i) & 1u ? __builtin_amdgcn_raw_buffer_load_b32(ta, aoff + i * (kPlanes * 64u * 4u), 0, POL > 0 ? 2 : 0)
-                             : 0u;
+  for (uint32_t i = 0; i < kUniRun; ++i) {
+    if constexpr (!CC) {  // no branch: a non-candidate's offset is past the run's resource (reads 0, no access)
+      Av[i] = __builtin_amdgcn_raw_buffer_load_b32(ta, (cand >> i) & 1u ? aoff + i * (kPlanes * 64u * 4u) : 0x80000000u,
+                                                   0, POL > 0 ? 2 : 0);
+    } else {
+      Av[i] = (cand >> i) & 1u ? __builtin_amdgcn_raw_buffer_load_b32(ta, aoff + i * (kPlanes * 64u * 4u), 0, POL > 0 ? 2 : 0)
+                               : 0u;
+    }
+  }
   // the overwritten published words (p.count_changed: publish) with them, not one dependent load per tile
 #pragma unroll
   for (uint32_t i = 0; i < kUniRun; ++i) {
     const uint32_t g = (t0 + i) * 64u + lane;
     const uint32_t nl = (g < p.L ? g : p.L - 1u) >> p.bl_log2;
     Ov[i] = AVK_CC_PREFETCH && CC && p.count_changed && ((cand >> i) & 1u) ? p.pref_out[(p.n0 + nl) * p.PS + b] : 0u;
+  }
+  if constexpr (!CC) {
+    // The single-GPU (non-counting) build walks the run with no per-tile branch: a tile is settled iff
+    // it is a candidate and no polled record's A differs from the reference word (one ballot, a
+    // scalar bit); its published words are stored through a resource bounded to the snapshot, with
+    // an out-of-range offset for the lanes that must not store (the store is dropped), and the
+    // counters take the settled bit as a factor. Per tile: ~half the scalar instructions of the
+    // branching walk (the settled rounds are bound by the CU's scalar issue).
+    const __amdgpu_buffer_rsrc_t prb =
+        __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)(p.n_nodes * p.PS * 4u), kRsrcWord3);
+    uint32_t done = 0u, applied = 0u, bytes = 0u, umis = 0u;
+    // a tile holds 64 / BL nodes: the lane's node and row advance by constants from tile to tile
+    // (lanes past the last lane compute a row they never store)
+    const uint32_t npt = 64u >> p.bl_log2;
+    const uint32_t rel0 = ((t0 * 64u + lane) >> p.bl_log2) - nlA;
+    uint32_t prow = (p.n0 + nlA + rel0) * p.PS + b;  // < N * PS < 2^30 (sweep gate)
+#pragma unroll
+    for (uint32_t i = 0; i < kUniRun; ++i) {
+      const uint32_t g = (t0 + i) * 64u + lane;
+      const bool active = g < p.L;
+      const uint32_t rel = rel0 + i * npt;
+      const uint32_t P0 = active ? vw : 0u;  // polled = live (kPendAllLive) and valid
+      const uint32_t A = Av[i];
+      const uint32_t mis = __ballot((refp ^ A) & P0) != 0ull ? 1u : 0u;  // always evaluated: no branch
+      const bool ok = (((cand >> i) & 1u) & (mis ^ 1u)) != 0u;             // wave-uniform
+      const uint32_t pub = ((byzm >> (rel & 63u)) & 1ull) ? bpat : A;
+      const bool st = ok && active;
+      __builtin_amdgcn_raw_buffer_store_b32(pub, prb, st ? prow * 4u : 0xFFFFFFFCu, 0, POL == 1 ? 2 : 0);  // (table < 4 GiB: 0xFFFFFFFC is past it)
+      umis |= (st & (pub != rin)) ? 1u : 0u;
+      done |= ok ? 1u << i : 0u;
+      applied += st ? 8u * (uint32_t)__popc(P0) : 0u;
+      bytes += st ? 8u : 0u;  // settled_run's accounting without the 32 B of gathered votes
+      prow += npt * p.PS;
+    }
+    if (lane < ntiles && ((done >> lane) & 1u)) {
+      p.kpend[t0 + lane] = ((meta & 0xFFu) + 1u) | kPendAllLive | (meta & kHiVirt);
+      bytes += 8u;  // kpend read (prologue) + written
+    }
+    acc.applied += applied;
+    acc.lane_bytes += bytes;
+    if (p.uni_out) acc.umis |= umis;
+    return done;
   }
   uint32_t done = 0u, applied = 0u, bytes = 0u, umis = 0u;
 #pragma unroll
