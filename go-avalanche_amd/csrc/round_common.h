@@ -553,6 +553,12 @@ __device__ __forceinline__ uint32_t select_slot(const uint32_t (&E)[K], uint32_t
   }
 }
 
+// A/B build knob: lanes with at least this many updates log a dense record (0: the default, above
+// kMedMax; 2: no medium records, the walk that folds a lane's updates into one is never run)
+#ifndef AVK_MED_DENSE_MIN
+#define AVK_MED_DENSE_MIN 0
+#endif
+
 // The reservation half of emit_updates_med: per-lane update count, the wave's
 // per-kind totals and the three reserving atomics, issued but not waited for
 // (their results are read in emit_store_med). A caller that issues it before
@@ -583,7 +589,7 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
   r.raw = 0u;
   if (!r.any) return r;
   const uint32_t cnt = lane_updates8(E, K);
-  const uint32_t dmin = max(p.dense_min, kMedMax + 1u);
+  const uint32_t dmin = AVK_MED_DENSE_MIN ? AVK_MED_DENSE_MIN : max(p.dense_min, kMedMax + 1u);
   const bool dense = cnt >= dmin, med = !dense && cnt >= 2u, single = cnt == 1u;
   r.tot_d = (uint32_t)__popcll(__ballot(dense));
   r.tot_m = (uint32_t)__popcll(__ballot(med));
@@ -607,7 +613,7 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
   static_assert(K <= 8, "slot fits 3 bits of a medium field; two updates per record per round at most");
   if (!r.any || p.ablate_emit == 1u) return 0u;
   const uint32_t cnt = lane_updates8(E, K);
-  const uint32_t dmin = max(p.dense_min, kMedMax + 1u);
+  const uint32_t dmin = AVK_MED_DENSE_MIN ? AVK_MED_DENSE_MIN : max(p.dense_min, kMedMax + 1u);
   const bool dense = cnt >= dmin, med = !dense && cnt >= 2u, single = cnt == 1u;
   const uint64_t dl = __ballot(dense), ml = __ballot(med), sl = __ballot(single);
   const uint32_t tot_d = r.tot_d, tot_m = r.tot_m, tot_s = r.tot_s;

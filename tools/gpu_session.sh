@@ -169,6 +169,7 @@ for s in "$@"; do
     quick) step quick 900 python -u -m pytest tests/test_gpu_peer_push.py tests/test_gpu_parity.py tests/test_gpu_uniform_rows.py tests/test_gpu_count_lazy.py tests/test_gpu_virtual_votes.py tests/test_gpu_fresh.py tests/test_gpu_replay_fused.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     tshard) step tshard 600 bash -c 'for o in tiles_per_wave=4 tiles_per_wave=8 tiles_per_wave=16; do python tools/shard_model.py --workload c4 --kinds targets --no-one-gpu --ranks 2,4,8 --option $o --json gpurun_out/tshard_c4_$o.json | tail -3; done' ;;
     shardmodel2) step shardmodel2 600 bash -c 'python tools/shard_model.py --workload c4 --json gpurun_out/shard_model_c4.json && python tools/shard_model.py --workload c4p --json gpurun_out/shard_model_c4p.json && python tools/shard_model.py --workload c4pb --json gpurun_out/shard_model_c4pb.json' ;;
+    abuni4) step abuni4 600 bash -c 'for w in c4 c5 c4pb; do for v in new s3; do echo "== $w $v"; if [ $v = new ]; then python tools/round_probe.py --workload $w; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w; fi; done; done' ;;
     c2ab) step c2ab 300 bash -c 'for v in new s3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
     reh2pb) step reh2pb 600 python bench.py --gpus 2 --rehearse-one-gpu --workload c4pb --no-secondary --detail gpurun_out/rehearse2_c4pb_detail.json ;;
     reh2t) step reh2t 600 python bench.py --gpus 2 --rehearse-one-gpu --shard targets --no-secondary --detail gpurun_out/rehearse2_targets_detail.json ;;
