@@ -31,9 +31,9 @@ window : BASELINE.md fixes C4 at its all-live rounds (no record can finalize
          Every StatusUpdate of the timed rounds is stored in the device log
          (sized for the window); an overflow is a hard failure (exit 3, no
          number printed).
-multi-GPU : N ranks split the same network (strong scaling): node shards with
-         the peer-push exchange (default) or an RCCL all-gather, or target
-         shards.
+multi-GPU : N ranks split the same network (strong scaling): target shards
+         (default: no exchange at all), or node shards with the
+         peer-push exchange or an RCCL all-gather (`--shard peers|nodes`).
 
 The line carries the round kernel's roofline: SURVEY.md
 §8(d)'s algorithmic bytes per launch (9.125 B per live (node, target, round)
@@ -109,9 +109,10 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c4", choices=sorted(WORKLOADS))
-    # peers: node shards + peer-push exchange; nodes: node shards +
-    # RCCL all-gather of the preference rows; targets: target shards, no exchange
-    ap.add_argument("--shard", default="peers", choices=["peers", "targets", "nodes"])
+    # targets: target shards, no exchange (default: DESIGN.md §5 measures it ahead of the node
+    # shards at G = 2 and 4, even at 8); peers: node shards + peer-push exchange; nodes: node
+    # shards + RCCL all-gather of the preference rows
+    ap.add_argument("--shard", default="targets", choices=["peers", "targets", "nodes"])
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xA7A1A9C4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")

@@ -868,15 +868,18 @@ int av_create(const av_config* cfg, av_engine** out) {
   // take any log_cap updates that go dense (8 B of capacity per update)
   const uint32_t dw = avk::dense_words((uint32_t)e->k);
   e->dense_min = avk::dense_min((uint32_t)e->k);
-  e->dlog_cap = std::max<uint32_t>(e->log_cap / e->dense_min, 16);
+  // k = 8 with slot records (kernels.h AVK_MED_S4): a lane goes dense from 4 slots with updates on
+  const uint32_t dense_least = e->k == 8 && AVK_MED_S4 ? 4u : e->dense_min;
+  e->dlog_cap = std::max<uint32_t>(e->log_cap / dense_least, 16);
   if ((he = dev_alloc(&e->dlog, (size_t)e->dlog_cap * e->log_shards * dw)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->dlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->upd_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
-  // a medium record holds >= 2 updates: log_cap / 2 records per shard (16 B each: 8 B of capacity per
-  // update, as the singles). Only k = 8 kernels emit them (round_common.h emit_updates_med: the sweep,
-  // k_replay_fast): other engines keep a token 16 records per shard.
+  // a medium record holds >= 2 updates: log_cap / 2 records per shard (kernels.h med_rec_words: 32 B
+  // slot records, 16 B per update of capacity). Only k = 8 kernels emit them (round_common.h
+  // emit_updates_med: the sweep, k_replay_fast): other engines keep a token 16 records per shard.
   e->mlog_cap = e->k == 8 ? std::max<uint32_t>(e->log_cap / 2, 16) : 16u;
-  if ((he = dev_alloc(&e->mlog, (size_t)e->mlog_cap * e->log_shards * 2)) != hipSuccess) return hip_fail(he, "alloc log");
+  if ((he = dev_alloc(&e->mlog, (size_t)e->mlog_cap * e->log_shards * avk::med_rec_words())) != hipSuccess)
+    return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->mlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   (void)hipMemsetAsync(e->mlog_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->dlog_count, 0, avk::kLogShards * 4, e->stream);
@@ -1648,7 +1651,7 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
     AV_HIP(avk::launch_sort_updates(nullptr, &sort_bytes, nullptr, nullptr, (uint64_t)total, 2, end_bit, e->stream));
     auto up = [](size_t b) { return (b + 255) / 256 * 256; };
     const size_t b_words = up((size_t)total * 8), b_rec = up((size_t)records * dw * 8),
-                 b_med = up((size_t)meds * 16), b_cnt = up((size_t)nrec * 8 + 8), b_off = up(3 * avk::kLogShards * 8);
+                 b_med = up((size_t)meds * 8 * avk::med_rec_words()), b_cnt = up((size_t)nrec * 8 + 8), b_off = up(3 * avk::kLogShards * 8);
     const size_t bytes = 2 * b_words + b_rec + b_med + 2 * b_cnt + b_off + up(scan_bytes) + up(sort_bytes);
     void* base = nullptr;
     rc = engine_scratch(e, bytes, &base);
@@ -1692,7 +1695,8 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
     };
     int64_t n_med = 0, n_dense = 0;
     if (meds) {
-      AV_HIP(avk::launch_compact_log(e->mlog, e->mlog_count, moff, e->mlog_cap, e->log_shards, 2, mrecs, e->stream));
+      AV_HIP(avk::launch_compact_log(e->mlog, e->mlog_count, moff, e->mlog_cap, e->log_shards, avk::med_rec_words(),
+                                    mrecs, e->stream));
       rc = expand(mrecs, meds, avk::kMedKind, singles, &n_med);
       if (rc != AV_OK) return rc;
       AV_CHECK(singles + n_med <= total, AV_ERR_HIP, "StatusUpdate log inconsistent (medium records)");

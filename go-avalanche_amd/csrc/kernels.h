@@ -252,11 +252,24 @@ inline void bl_divider(uint32_t d, uint32_t& magic, uint32_t& sh1, uint32_t& sh2
 __host__ __device__ constexpr uint32_t dense_words(uint32_t k) { return (k + 5u) / 2u; }  // u64 words
 __host__ __device__ constexpr uint32_t dense_min(uint32_t k) { return dense_words(k); }   // updates
 
-// A lane with 2..kMedMax StatusUpdates in one round (k <= 8) logs one medium
+// Medium lane records (k = 8 round kernels, round_common.h emit_store_med), two formats:
+//  * AVK_MED_S4 = 1 (default): a slot record of four u64 = u32 words [key lo, key hi (pack_update
+//    with the block's first target, slot 0, status 0), S (bits 0-7: slots with updates; bit 8
+//    kMedS4Died: the last word is the died plane), A (final accepted plane), E of the first, second,
+//    third and fourth slot with updates (zero past the last; the fourth is the died plane when
+//    flagged)]. Logged by a lane with >= 2 updates in at most 4 slots (at most 3 when a record of it
+//    was deleted this round); other lanes with >= 2 updates log a dense record. Expanded as a dense
+//    record over the slots S names.
+//  * AVK_MED_S4 = 0: a lane with 2..kMedMax StatusUpdates in one round (k <= 8) logs one medium
 // record of two u64: the key (pack_update with the block's first target, slot
 // 0, status 0) and a payload: bits [3:0] = n updates, then n 10-bit fields at
 // bit 4 + 10 i, each (slot << 7 | bit << 2 | status) = the update's offset
 // from the key (expanded word = key + (slot << 24) + (bit << 2) + status).
+#ifndef AVK_MED_S4
+#define AVK_MED_S4 1
+#endif
+constexpr uint32_t kMedS4Died = 1u << 8;
+__host__ __device__ constexpr uint32_t med_rec_words() { return AVK_MED_S4 ? 4u : 2u; }  // u64 per medium record
 constexpr uint32_t kMedMax = 6;
 __host__ __device__ constexpr uint32_t med_field(uint32_t slot, uint32_t bit, uint32_t status) {
   return (slot << 7) | (bit << 2) | status;
@@ -394,7 +407,7 @@ hipError_t launch_log_digest(const uint64_t* log, const uint32_t* counts, uint32
 hipError_t launch_dense_expand(const uint64_t* recs, uint64_t n, uint32_t k, uint64_t* counts_scratch,
                                uint64_t* offsets, void* temp, size_t* temp_bytes, uint64_t* out, hipStream_t s);
 // The same for n compacted medium records (k = 0 selects the medium form in launch_dense_expand's
-// kernels: 2 u64 per record, n updates in the payload's low 4 bits).
+// kernels: med_rec_words() u64 per record).
 constexpr uint32_t kMedKind = 0u;
 // Radix sort of packed update words on bits [begin_bit, end_bit) (temp ==
 // nullptr: size query).

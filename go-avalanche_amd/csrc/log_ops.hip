@@ -60,16 +60,38 @@ __device__ __forceinline__ void for_each_dense(const uint32_t* w, uint32_t K, F&
   }
 }
 
-// Medium record (kernels.h kMedMax): w = {key, payload}.
+// Medium record (kernels.h). Slot record (AVK_MED_S4): the dense expansion over the slots its mask
+// names (A after slot j = A ^ parity of the later slots' updates); folded record: {key, payload}.
 template <typename F>
-__device__ __forceinline__ void for_each_med(const uint64_t* w, F&& f) {
-  const uint64_t key = w[0], pl = w[1];
+__device__ __forceinline__ void for_each_med(const uint64_t* rec, F&& f) {
+#if AVK_MED_S4
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(rec);
+  const uint64_t key = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  const uint32_t S = w[2], A = w[3];
+  const uint32_t nw = (S & kMedS4Died) ? 3u : 4u;
+  const uint32_t died = (S & kMedS4Died) ? w[7] : 0u;
+  uint32_t slot[4], n = 0;
+  for (uint32_t m = S & 0xFFu; m && n < nw; m &= m - 1u) slot[n++] = (uint32_t)__builtin_ctz(m);
+  uint32_t par = 0u;
+  for (int i = (int)n - 1; i >= 0; --i) {
+    const uint32_t aj = A ^ par, e = w[4 + i];
+    par ^= e;
+    for (uint32_t em = e; em; em &= em - 1u) {
+      const uint32_t bit = (uint32_t)__builtin_ctz(em);
+      const uint64_t a = (aj >> bit) & 1u;
+      const uint64_t st = ((died >> bit) & 1u) ? (a ? 3u : 0u) : (a ? 2u : 1u);  // vote.go:77-91
+      f(key + ((uint64_t)slot[i] << 24) + ((uint64_t)bit << 2) + st);
+    }
+  }
+#else
+  const uint64_t key = rec[0], pl = rec[1];
   const uint32_t n = (uint32_t)(pl & 15u);
   for (uint32_t i = 0; i < n && i < kMedMax; ++i) f(med_word(key, (uint32_t)(pl >> (4u + 10u * i)) & 1023u));
+#endif
 }
 
 // u64 words of one record: dense (k >= 1) or medium (kMedKind)
-__host__ __device__ constexpr uint32_t rec_words(uint32_t K) { return K == kMedKind ? 2u : dense_words(K); }
+__host__ __device__ constexpr uint32_t rec_words(uint32_t K) { return K == kMedKind ? med_rec_words() : dense_words(K); }
 
 template <typename F>
 __device__ __forceinline__ void for_each_rec(const uint64_t* rec, uint32_t K, F&& f) {
@@ -119,10 +141,11 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
     });
   }
   const uint32_t nm = mlog ? min(mcounts[shard], mcap) : 0u;
-  const uint64_t* msrc = mlog + (size_t)shard * mcap * 2u;
+  constexpr uint32_t MW = med_rec_words();
+  const uint64_t* msrc = mlog + (size_t)shard * mcap * MW;
   for (uint32_t i = t; i < nm; i += stride) {
-    if (!in_nodes(msrc[2u * i], node0, node1)) continue;
-    for_each_med(msrc + 2u * i, [&](uint64_t wd) {
+    if (!in_nodes(msrc[MW * i], node0, node1)) continue;
+    for_each_med(msrc + MW * i, [&](uint64_t wd) {
       const uint64_t h = mix64(wd);
       s += h;
       x ^= h;
@@ -144,7 +167,15 @@ __global__ __launch_bounds__(256) void k_dense_counts(const uint64_t* recs, uint
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (K == kMedKind) {
+#if AVK_MED_S4
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(recs + i * med_rec_words());
+    const uint32_t nw = (w[2] & kMedS4Died) ? 3u : 4u;
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < nw; ++j) c += (uint32_t)__popc(w[4 + j]);
+    cnt[i] = c;
+#else
     cnt[i] = min((uint32_t)(recs[2u * i + 1u] & 15u), kMedMax);
+#endif
     return;
   }
   const uint32_t* w = reinterpret_cast<const uint32_t*>(recs + i * dense_words(K));

@@ -553,6 +553,34 @@ __device__ __forceinline__ uint32_t select_slot(const uint32_t (&E)[K], uint32_t
   }
 }
 
+// Lowest set bit's index, 0xFFFFFFFF for 0 (v_ffbl_b32 as is: no zero test and select around it)
+__device__ __forceinline__ uint32_t ffbl_u32(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+// bit (b & 31) of x
+__device__ __forceinline__ uint32_t bfe1(uint32_t x, uint32_t b) { return __builtin_amdgcn_ubfe(x, b & 31u, 1u); }
+// E[j & 7] as a bit-select tree: 7 v_bfi_b32 on the sign-extended bits of j (no compare writing a lane
+// mask, so no VALU-wrote-SGPR wait states before the selects)
+template <int K>
+__device__ __forceinline__ uint32_t select_slot_bfi(const uint32_t (&E)[K], uint32_t j) {
+  if constexpr (K != 8) return select_slot<K>(E, j);
+  else {
+  const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)j, 0u, 1u);
+  const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)j, 1u, 1u);
+  const uint32_t m2 = (uint32_t)__builtin_amdgcn_sbfe((int)j, 2u, 1u);
+  const uint32_t a0 = (m0 & E[1]) | (~m0 & E[0]), a1 = (m0 & E[3]) | (~m0 & E[2]);
+  const uint32_t a2 = (m0 & E[5]) | (~m0 & E[4]), a3 = (m0 & E[7]) | (~m0 & E[6]);
+  const uint32_t c0 = (m1 & a1) | (~m1 & a0), c1 = (m1 & a3) | (~m1 & a2);
+  return (m2 & c1) | (~m2 & c0);
+  }
+}
+
+#ifndef AVK_MED_WALK
+#define AVK_MED_WALK 1
+#endif
+
 // A/B build knob: lanes with at least this many updates log a dense record (0: the default, above
 // kMedMax; 2: no medium records, the walk that folds a lane's updates into one is never run)
 #ifndef AVK_MED_DENSE_MIN
@@ -568,6 +596,7 @@ __device__ __forceinline__ uint32_t select_slot(const uint32_t (&E)[K], uint32_t
 struct EmitRes {
   uint32_t tot_s, tot_m, tot_d;  // wave-uniform: lanes of each kind
   uint32_t raw;                  // lanes 0, 1, 2: the singles / medium / dense atomics' results (one VGPR)
+  uint32_t lk;                   // per lane (AVK_MED_S4): slots with updates (bits 0-7), kind (bits 8-9)
   bool any;                      // wave-uniform: some lane has an update
 };
 
@@ -577,9 +606,18 @@ __device__ __forceinline__ uint32_t lane_updates8(const uint32_t* E, int K) {
   return c;
 }
 
+// Medium records, two formats (kernels.h kMedS4 selects; the log readers in log_ops.hip follow it):
+//  * AVK_MED_S4 = 1 (default): a lane whose updates lie in at most 4 slots (3 if a record of it was
+//    deleted this round) stores a 32-byte slot record {key, slot mask | died flag, A_final, up to 4
+//    E_j words in slot order (the 4th: the died plane when flagged)}: the slot words are compacted
+//    by a shift-in network, no per-update work at all;
+//  * AVK_MED_S4 = 0: a 16-byte record folding up to kMedMax updates into 10-bit fields, walked one
+//    update per step (the round-3 form, kept for A/B).
+constexpr uint32_t kLkSingle = 1u << 8, kLkMed = 2u << 8, kLkDense = 3u << 8;
+
 template <int K>
 __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32_t shard, uint32_t lane,
-                                                    const uint32_t (&E)[K], uint32_t& updates) {
+                                                    const uint32_t (&E)[K], uint32_t died, uint32_t& updates) {
   EmitRes r;
   uint32_t any = 0;
 #pragma unroll
@@ -587,10 +625,23 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
   r.any = __ballot(any != 0u) != 0ull;
   r.tot_s = r.tot_m = r.tot_d = 0u;
   r.raw = 0u;
+  r.lk = 0u;
   if (!r.any) return r;
   const uint32_t cnt = lane_updates8(E, K);
+#if AVK_MED_S4
+  uint32_t nz = 0u;
+#pragma unroll
+  for (int j = 0; j < K; ++j) nz |= (E[j] != 0u ? 1u : 0u) << j;
+  const uint32_t ns = (uint32_t)__popc(nz);
+  const bool single = cnt == 1u;
+  const bool med = cnt >= 2u && (ns <= 3u || (ns == 4u && died == 0u));
+  const bool dense = cnt >= 2u && !med;
+  r.lk = nz | (single ? kLkSingle : med ? kLkMed : dense ? kLkDense : 0u);
+#else
+  (void)died;
   const uint32_t dmin = AVK_MED_DENSE_MIN ? AVK_MED_DENSE_MIN : max(p.dense_min, kMedMax + 1u);
   const bool dense = cnt >= dmin, med = !dense && cnt >= 2u, single = cnt == 1u;
+#endif
   r.tot_d = (uint32_t)__popcll(__ballot(dense));
   r.tot_m = (uint32_t)__popcll(__ballot(med));
   r.tot_s = (uint32_t)__popcll(__ballot(single));
@@ -612,6 +663,60 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
                                                    uint32_t round_rel) {
   static_assert(K <= 8, "slot fits 3 bits of a medium field; two updates per record per round at most");
   if (!r.any || p.ablate_emit == 1u) return 0u;
+#if AVK_MED_S4
+  if constexpr (K == 8) {
+    const uint32_t kind = r.lk & (3u << 8), nz = r.lk & 0xFFu;
+    const bool dense = kind == kLkDense, med = kind == kLkMed, single = kind == kLkSingle;
+    const uint64_t dl = __ballot(dense), ml = __ballot(med), sl = __ballot(single);
+    const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 0);
+    const uint32_t mbase = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 1);
+    const uint32_t dbase = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 2);
+    const uint32_t st_d = dbase >= p.dlog_cap ? 0u : min(r.tot_d, p.dlog_cap - dbase);
+    const uint32_t st_m = mbase >= p.mlog_cap ? 0u : min(r.tot_m, p.mlog_cap - mbase);
+    const uint32_t st_s = base >= p.log_cap ? 0u : min(r.tot_s, p.log_cap - base);
+    const bool ovf = st_d < r.tot_d || st_m < r.tot_m || st_s < r.tot_s;
+    const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u);
+    const uint64_t mine = dense ? dl : med ? ml : sl;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+    if (dense) {
+      if (rank < st_d) {
+        constexpr uint32_t DW = dense_words(K);
+        uint64_t* const rec = p.dlog + ((size_t)shard * p.dlog_cap + dbase + rank) * DW;
+        u32x4* const q = reinterpret_cast<u32x4*>(rec);
+        q[0] = u32x4{(uint32_t)key, (uint32_t)(key >> 32), E[0], E[1]};
+        q[1] = u32x4{E[2], E[3], E[4], E[5]};
+        q[2] = u32x4{E[6], E[7], A_final, died};
+      }
+    } else {
+      // the first 4 slots with updates, in slot order: shift in from the last slot down
+      uint32_t o0 = 0u, o1 = 0u, o2 = 0u, o3 = 0u;
+#pragma unroll
+      for (int j = K - 1; j >= 0; --j) {
+        const bool h = E[j] != 0u;
+        o3 = h ? o2 : o3;
+        o2 = h ? o1 : o2;
+        o1 = h ? o0 : o1;
+        o0 = h ? E[j] : o0;
+      }
+      if (med) {
+        if (rank < st_m) {
+          const bool hasd = died != 0u;  // then at most 3 slots: the died plane takes the 4th word
+          u32x4* const q = reinterpret_cast<u32x4*>(p.mlog + ((size_t)shard * p.mlog_cap + mbase + rank) * 4u);
+          q[0] = u32x4{(uint32_t)key, (uint32_t)(key >> 32), nz | (hasd ? kMedS4Died : 0u), A_final};
+          q[1] = u32x4{o0, o1, o2, hasd ? died : o3};
+        }
+      } else if (single && rank < st_s) {
+        // the one update: slot ffbl(nz), record ffbl(o0); status from A_final and died (vote.go:77-91)
+        const uint32_t j = ffbl_u32(nz), bit = ffbl_u32(o0);
+        const uint32_t a = bfe1(A_final, bit), d = bfe1(died, bit);
+        const uint32_t st = (a << 1) | (~(a ^ d) & 1u);
+        p.log[(size_t)shard * p.log_cap + base + rank] = key + ((uint64_t)j << 24) + ((uint64_t)bit << 2) + st;
+      }
+    }
+    if (__ballot(ovf) != 0ull) note_overflow(p, lane);
+    return 8u * st_s + 32u * st_m + 8u * dense_words(K) * st_d;
+  }
+#endif
   const uint32_t cnt = lane_updates8(E, K);
   const uint32_t dmin = AVK_MED_DENSE_MIN ? AVK_MED_DENSE_MIN : max(p.dense_min, kMedMax + 1u);
   const bool dense = cnt >= dmin, med = !dense && cnt >= 2u, single = cnt == 1u;
@@ -648,6 +753,48 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
 #pragma unroll
         for (uint32_t i = 0; i < DW; ++i) rec[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
       }
+    }
+  } else if (AVK_MED_WALK && K == 8) {
+    // T: records with two updates this round. The walk runs for the wave's largest count (one
+    // wave-uniform test per step, no exec-mask branches); lanes past their own count (and dense or
+    // update-less lanes) compute a field that is masked out. Per step: the next slot with updates
+    // when the current one is used up (a bit-select mux on the slot index, select_slot_bfi), its
+    // lowest update, the status from two planes fixed per walk (a = A after slot j, vote.go:77-91:
+    // A_final flipped back for the first of a record's two updates; status bit 0 = ~(a ^ died)).
+    uint32_t seen = 0u, T = 0u, nz = 0u;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      T |= seen & E[j];
+      seen |= E[j];
+      nz |= (E[j] != 0u ? 1u : 0u) << j;
+    }
+    const uint32_t cm = dense ? 0u : cnt;  // updates this lane folds into its payload
+    const uint32_t Ad = A_final ^ died;
+    uint32_t S = 0u, j = 0u, cur = 0u;
+    uint64_t pl = cnt;
+#pragma unroll
+    for (uint32_t q = 0; q < kMedMax; ++q) {
+      if (__ballot(q < cm) == 0ull) break;  // wave-uniform
+      const bool adv = cur == 0u;
+      const uint32_t jn = ffbl_u32(nz);
+      j = adv ? jn : j;
+      nz = adv ? nz & (nz - 1u) : nz;
+      cur = adv ? select_slot_bfi<K>(E, jn) : cur;
+      const uint32_t bit = ffbl_u32(cur);
+      cur &= cur - 1u;
+      const uint32_t first = T & ~S;  // records whose first of two updates is still ahead
+      S |= 1u << bit;
+      const uint32_t st = (bfe1(A_final ^ first, bit) << 1) | bfe1(~(Ad ^ first), bit);
+      const uint32_t f = (j << 7) | (bit << 2) | st;
+      pl |= (uint64_t)(q < cm ? f : 0u) << (4u + 10u * q);
+    }
+    if (med) {
+      if (rank < st_m) {
+        u32x4* rec = reinterpret_cast<u32x4*>(p.mlog + ((size_t)shard * p.mlog_cap + mbase + rank) * 2u);
+        *rec = u32x4{(uint32_t)key, (uint32_t)(key >> 32), (uint32_t)pl, (uint32_t)(pl >> 32)};
+      }
+    } else if (single && rank < st_s) {
+      p.log[(size_t)shard * p.log_cap + base + rank] = med_word(key, (uint32_t)(pl >> 4) & 1023u);
     }
   } else if (cnt) {
     // T: records with two updates this round; walk the updates in slot order
@@ -704,7 +851,7 @@ __device__ __forceinline__ uint32_t emit_updates_med(const RoundParams& p, uint3
                                                      uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
                                                      uint32_t A_final, uint32_t died, uint32_t& updates,
                                                      uint32_t round_rel) {
-  const EmitRes r = emit_reserve_med<K>(p, shard, lane, E, updates);
+  const EmitRes r = emit_reserve_med<K>(p, shard, lane, E, died, updates);
   return emit_store_med<K>(p, shard, lane, node, tbase, E, A_final, died, r, round_rel);
 }
 

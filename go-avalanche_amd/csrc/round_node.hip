@@ -555,7 +555,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       ++pubs;
     }
     if constexpr (K == 8) {
-      const EmitRes cur = emit_reserve_med<K>(p, shard, lane, E, upd);
+      const EmitRes cur = emit_reserve_med<K>(p, shard, lane, E, 0u, upd);
       if (have_pend)
         emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Epend, Apend, 0u, pend, p.round_rel + r - 1u);
 #pragma unroll

@@ -507,7 +507,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   // StatusUpdate log reservation (k = 8) before this tile's plane and published-word stores, so that
   // reading the atomics' results waits for them alone, not for those stores (round_common.h)
   EmitRes er{};
-  if constexpr (K == 8) er = emit_reserve_med<K>(p, acc.shard, lane, E, acc.updates);
+  if constexpr (K == 8) er = emit_reserve_med<K>(p, acc.shard, lane, E, died, acc.updates);
 #endif
   {
     uint32_t cy = 0u;

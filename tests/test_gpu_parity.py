@@ -319,7 +319,7 @@ def dense_words(k):  # kernels.h dense_words: u64 words of a dense lane record
     return (k + 5) // 2
 
 
-MED_MAX = 6  # kernels.h kMedMax
+MED_MAX = 6  # kernels.h kMedMax (folded medium records, AVK_MED_S4 = 0 builds only)
 
 
 def emitted_bytes(u, k=8, med=False):
@@ -327,15 +327,23 @@ def emitted_bytes(u, k=8, med=False):
     node, 32-target block) with c updates. med=False (first-generation
     kernels): c >= dense_words(k) is one dense record of dense_words(k) u64
     words, else c single 8-B words. med=True (the k = 8 sweep,
-    round_common.h emit_updates_med): 1 update a single word, 2..MED_MAX one
-    16-B medium record, more a dense record."""
+    round_common.h emit_store_med, slot records): 1 update a single word;
+    >= 2 updates in at most 4 slots (3 when one of them deletes its record:
+    status Finalized / Invalid) one 32-B slot record; otherwise a dense record."""
     if len(u) == 0:
         return 0
     key = np.stack([u[:, 0], u[:, 1], u[:, 3] // 32], axis=1)
-    _, counts = np.unique(key, axis=0, return_counts=True)
+    _, inv, counts = np.unique(key, axis=0, return_inverse=True, return_counts=True)
+    inv = inv.reshape(-1)
     dw = dense_words(k)
     if med:
-        return int(np.where(counts > MED_MAX, 8 * dw, np.where(counts >= 2, 16, 8 * counts)).sum())
+        g = len(counts)
+        _, first = np.unique(np.stack([inv, u[:, 2]], axis=1), axis=0, return_index=True)
+        ns = np.bincount(inv[first], minlength=g)  # slots with updates per block
+        died = np.bincount(inv, weights=np.isin(u[:, 4], [avhip.STATUS_FINALIZED, avhip.STATUS_INVALID]),
+                           minlength=g) > 0
+        slot_rec = (ns <= 3) | ((ns == 4) & ~died)
+        return int(np.where(counts == 1, 8, np.where(slot_rec, 32, 8 * dw)).sum())
     return int(np.where(counts >= dw, 8 * dw, 8 * counts).sum())
 
 

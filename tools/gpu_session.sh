@@ -170,8 +170,10 @@ for s in "$@"; do
     tshard) step tshard 600 bash -c 'for o in tiles_per_wave=4 tiles_per_wave=8 tiles_per_wave=16; do python tools/shard_model.py --workload c4 --kinds targets --no-one-gpu --ranks 2,4,8 --option $o --json gpurun_out/tshard_c4_$o.json | tail -3; done' ;;
     shardmodel2) step shardmodel2 600 bash -c 'python tools/shard_model.py --workload c4 --json gpurun_out/shard_model_c4.json && python tools/shard_model.py --workload c4p --json gpurun_out/shard_model_c4p.json && python tools/shard_model.py --workload c4pb --json gpurun_out/shard_model_c4pb.json' ;;
     abuni4) step abuni4 600 bash -c 'for w in c4 c5 c4pb; do for v in new s3; do echo "== $w $v"; if [ $v = new ]; then python tools/round_probe.py --workload $w; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w; fi; done; done' ;;
+    abdense) step abdense 600 bash -c 'for w in c4 c4p c4pb; do for v in new dense2 dense4; do echo "== $w $v"; if [ $v = new ]; then python tools/round_probe.py --workload $w | tail -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w | tail -1; fi; done; done' ;;
+    abs4) step abs4 900 bash -c 'for w in c4 c4p c4pb; do for v in new walk walk0; do echo "== $w $v"; if [ $v = new ]; then python tools/round_probe.py --workload $w; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w; fi; done; done; for v in new walk0; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
     c2ab) step c2ab 300 bash -c 'for v in new s3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
-    reh2pb) step reh2pb 600 python bench.py --gpus 2 --rehearse-one-gpu --workload c4pb --no-secondary --detail gpurun_out/rehearse2_c4pb_detail.json ;;
+    reh2pb) step reh2pb 600 python bench.py --gpus 2 --rehearse-one-gpu --workload c4pb --shard peers --no-secondary --detail gpurun_out/rehearse2_c4pb_detail.json ;;
     reh2t) step reh2t 600 python bench.py --gpus 2 --rehearse-one-gpu --shard targets --no-secondary --detail gpurun_out/rehearse2_targets_detail.json ;;
     abs3) step abs3 900 bash -c 'for w in c4 c4p c4pb c3; do for v in new s3; do for cc in 0 1; do echo "== $w $v count_changed=$cc"; if [ $v = new ]; then python tools/round_probe.py --workload $w --option count_changed=$cc | tail -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w --option count_changed=$cc | tail -1; fi; done; done; done; for v in new s3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
     profc2b) step profc2b 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/profc2b -o c2 -- python3 bench.py --workload c2 --no-cpu-baseline --no-secondary ;;
