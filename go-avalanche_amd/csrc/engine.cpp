@@ -129,7 +129,7 @@ struct av_engine {
   bool plane_nt = true;  // tuning option "plane_nt" (A/B on MI355X: -8 % kernel time warm, -16 % cold)
   bool ablate_gather = false;  // diagnostics option "ablate_gather" (invalid results)
   uint32_t ablate_node = 0;  // diagnostics option "ablate_node" (k_round_node, invalid results)
-  int ablate_emit = 0;  // diagnostics option "ablate_emit": 1 = StatusUpdates counted, not stored; 2 = no reserving atomic
+  int ablate_emit = 0;  // diagnostics option "ablate_emit": 1 = StatusUpdates counted, not stored; 2 = no reserving atomic; 3 = atomic issued, result unused
   uint32_t ablate_phase = 0;  // diagnostics option "ablate_phase" (kernels.h; results invalid)
   // diagnostics option "unsynced_shard": a node-sharded engine runs rounds with no exchange (other
   // shards' preference rows keep their initial values; per-rank kernel timing only, invalid results)
@@ -150,9 +150,9 @@ struct av_engine {
   // option "settled_lean": with BL dividing 64, a wave tests its run's settled candidates in one
   // lean loop first (round_sweep.hip settled_run)
   bool settled_lean = true;
-  // option "tiles_per_wave" (default grid, default_sweep_blocks); 0 = by size: 8 from 256k tiles on
-  // at BL >= 16 (C4: 500k tiles, 6.13 -> 5.99 ms per epoch), else 4 (C3's 98k tiles: 8 per wave leaves two
-  // generations of waves and was 6 % slower)
+  // option "tiles_per_wave" (default grid, default_sweep_blocks); 0 = by size: up to 16, at most BL, with
+  // >= 15000 waves (C4: 500k tiles, 16 per wave; C3's 98k tiles: 4 — 8 per wave leaves two generations
+  // of waves and was 6 % slower)
   uint32_t tiles_per_wave = 0;
   // every consider plane of every lane is all-ones: set after a sim round with k >= 8 in which every
   // live record was polled (all targets valid, uncapped); cleared by anything that can write a 0
@@ -691,8 +691,16 @@ uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
   // (a run's nodes must fit the run's peer draw: 2 producer lanes per node and round, 64 lanes; runs
   // of 16 tiles at BL >= 32 draw both rounds in two passes: C4 epoch 5.14 -> 4.95 ms, the settled
   // rounds 0.112 -> 0.088 ms, storm rounds +2 %, profiles/r03/ab_tiles_per_wave.log)
-  const uint64_t tpw = e->tiles_per_wave ? e->tiles_per_wave
-                                         : (tiles >= (1u << 18) ? (e->BL >= 32 ? 16u : e->BL >= 16 ? 8u : 4u) : 4u);
+  // Default: the longest run (16, 8 or 4 tiles) whose nodes fit one 64-lane draw (tiles_per_wave <= BL:
+  // 64 * tpw / BL nodes per run) while the grid keeps >= 15000 waves. Target shards of C4
+  // (tools/shard_model.py, profiles/r04/tshard_c4_*.json, rank 0's settled rounds): BL 16 (G = 2)
+  // 0.083 ms at 4 tiles per wave, 0.038 at 16; BL 8 (G = 4) 0.046 at 4, 0.031 at 8, 0.166 at 16 (the
+  // run's nodes overflow the draw); BL 4 (G = 8) 0.027 at 4, 0.124 at 8.
+  uint64_t tpw = e->tiles_per_wave;
+  if (!tpw) {
+    tpw = 16;
+    while (tpw > 4 && (tpw > (uint64_t)e->BL || tiles / tpw < 15000)) tpw /= 2;
+  }
   const uint64_t waves = (tiles + tpw - 1) / tpw;
   return (uint32_t)std::max<uint64_t>(1, (waves + 3) / 4);
 }
@@ -1886,7 +1894,7 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   } else if (n == "ablate_phase") {  // diagnostics (kernels.h RoundParams::ablate_phase; results invalid)
     e->ablate_phase = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(31, value));
   } else if (n == "ablate_emit") {
-    e->ablate_emit = (int)std::max<int64_t>(0, std::min<int64_t>(2, value));
+    e->ablate_emit = (int)std::max<int64_t>(0, std::min<int64_t>(3, value));
   } else if (n == "k_hi_virtual") {  // A/B: virtual K4..K7 group (kernels.h kHiVirt)
     int rc = materialize_counts(e);
     if (rc != AV_OK) return rc;

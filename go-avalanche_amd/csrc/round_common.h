@@ -650,6 +650,14 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
   // one atomic instruction, lanes 0 / 1 / 2 reserving the singles / medium / dense runs
   const uint32_t want = lane == 0 ? r.tot_s : lane == 1 ? r.tot_m : lane == 2 ? r.tot_d : 0u;
   uint32_t* const ctr = lane == 0 ? p.log_count : lane == 1 ? p.mlog_count : p.dlog_count;
+  if (p.ablate_emit >= 2u) {  // diagnostics (log invalid): stores at made-up per-wave positions; 3: the
+    // reserving atomic still issued, its result unused (no wait for it)
+    const uint32_t wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t cap = lane == 0 ? p.log_cap : lane == 1 ? p.mlog_cap : p.dlog_cap;
+    r.raw = cap > 8192u ? (wv * 509u) % (cap - 4096u) : 0u;
+    if (p.ablate_emit == 3u && want) atomicAdd(ctr + shard, want);
+    return r;
+  }
   if (want) r.raw = atomicAdd(ctr + shard, want);
   return r;
 }

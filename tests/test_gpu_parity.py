@@ -495,6 +495,37 @@ def test_target_shard_identity_8way():
     assert full.finalized_count() == sum(p.finalized_count() for p in parts) > 0
 
 
+@pytest.mark.parametrize("g", [2, 4, 8])
+def test_target_shard_runs(g):
+    """G target shards of a C4-shaped network (BL = 16 / 8 / 4 lanes per node)
+    with the tiles-per-wave the engine picks for that BL at full size
+    (engine.cpp default_sweep_blocks: 16 / 8 / 4, one 64-lane draw per run) ==
+    one engine, bit for bit, through the settled rounds and finalization."""
+    n, m, k, R = 20_000, 1000, 8, 20
+    full = avhip.Engine(n, m, k=k, seed=77, log_capacity=1 << 24)
+    full.init_records(avhip.INIT_BERNOULLI, P80)
+    from avhip import sharding
+    parts = []
+    for r in range(g):
+        p = avhip.Engine(n, m, k=k, seed=77, target_range=sharding.target_shard(m, g, r), log_capacity=1 << 23)
+        p.set_option("tiles_per_wave", {2: 16, 4: 8, 8: 4}[g])
+        p.init_records(avhip.INIT_BERNOULLI, P80)
+        parts.append(p)
+    for r in range(R):
+        full.run_rounds(1)
+        for p in parts:
+            p.run_rounds(1)
+        u = np.concatenate([p.fetch_updates() for p in parts])
+        u = u[np.lexsort((u[:, 3], u[:, 2], u[:, 1], u[:, 0]))]
+        assert np.array_equal(full.fetch_updates(), u), r
+    merged = np.concatenate([p.read_records() for p in parts], axis=1)
+    assert np.array_equal(full.read_records(), merged)
+    assert full.applied_votes() == sum(p.applied_votes() for p in parts)
+    assert full.finalized_count() == sum(p.finalized_count() for p in parts) > 0
+    for p in parts + [full]:
+        p.close()
+
+
 def test_cross_kernel_full_c4():
     """configs C4 at full size (1M nodes x 1000 targets, k=8, Bernoulli(0.8)):
     the sweep kernel and the first-generation per-tile kernel agree on every
