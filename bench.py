@@ -355,8 +355,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
     # the log holds every StatusUpdate of one timed segment (up to 16 rounds:
     # C4 ~2e8 in rounds 0-2, the conflicting C4p/C4pb ~1e9 over rounds 0-8);
-    # 24 B of device memory per entry at k = 8 (singles 8, medium records 8, dense
-    # records 8 B of capacity per update): 30 GB at 1M x 1000
+    # 36 B of device memory per entry at k = 8 (singles 8, slot records 16, dense
+    # records 12 B of capacity per update): 45 GB at 1M x 1000, 77 GB for C5
     log_cap = min(int(1.25 * n * m) + (1 << 20), (1 << 31) - 1)
     run = Runner(wl, args, world, rank, local_rank, log_cap)
     if run.fallback is not None:

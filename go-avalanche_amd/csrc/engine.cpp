@@ -784,7 +784,7 @@ int av_destroy(av_engine* e) {
   if (e->marker) (void)hipEventDestroy(e->marker);
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->kpend, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->readd, e->died_out, e->nopoll,
-                  e->dlog, e->dlog_count, e->upd_count, e->mlog, e->mlog_count,
+                  e->dlog, e->upd_count, e->mlog,
                   e->applied, e->bytes, e->finalized, e->scratch_count, e->replay};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -871,7 +871,11 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->valid, e->BL)) != hipSuccess) return hip_fail(he, "alloc valid");
   if ((he = dev_alloc(&e->byz, (e->N + 31) / 32)) != hipSuccess) return hip_fail(he, "alloc byz");
   if ((he = dev_alloc(&e->log, (size_t)e->log_cap * e->log_shards)) != hipSuccess) return hip_fail(he, "alloc log");
-  if ((he = dev_alloc(&e->log_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  // the singles', medium and dense records' per-shard counters: one array (round_common.h
+  // emit_reserve_med indexes it by kind)
+  if ((he = dev_alloc(&e->log_count, 3 * avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
+  e->mlog_count = e->log_count + avk::kLogShards;
+  e->dlog_count = e->log_count + 2 * avk::kLogShards;
   // a dense record holds >= dense_min(k) updates: log_cap / dense_min records
   // take any log_cap updates that go dense (8 B of capacity per update)
   const uint32_t dw = avk::dense_words((uint32_t)e->k);
@@ -880,7 +884,6 @@ int av_create(const av_config* cfg, av_engine** out) {
   const uint32_t dense_least = e->k == 8 && AVK_MED_S4 ? 4u : e->dense_min;
   e->dlog_cap = std::max<uint32_t>(e->log_cap / dense_least, 16);
   if ((he = dev_alloc(&e->dlog, (size_t)e->dlog_cap * e->log_shards * dw)) != hipSuccess) return hip_fail(he, "alloc log");
-  if ((he = dev_alloc(&e->dlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   if ((he = dev_alloc(&e->upd_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   // a medium record holds >= 2 updates: log_cap / 2 records per shard (kernels.h med_rec_words: 32 B
   // slot records, 16 B per update of capacity). Only k = 8 kernels emit them (round_common.h
@@ -888,7 +891,6 @@ int av_create(const av_config* cfg, av_engine** out) {
   e->mlog_cap = e->k == 8 ? std::max<uint32_t>(e->log_cap / 2, 16) : 16u;
   if ((he = dev_alloc(&e->mlog, (size_t)e->mlog_cap * e->log_shards * avk::med_rec_words())) != hipSuccess)
     return hip_fail(he, "alloc log");
-  if ((he = dev_alloc(&e->mlog_count, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
   (void)hipMemsetAsync(e->mlog_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->dlog_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->upd_count, 0, avk::kLogShards * 4, e->stream);

@@ -66,12 +66,12 @@ struct RoundParams {
   const uint32_t* byz;       // [ceil(N/32)] Byzantine node bits
   const uint32_t* replay;    // replay mode: yes/consider words of each lane and slot (replay_idx)
   uint64_t* log;             // [kLogShards][log_cap] single StatusUpdates
-  uint32_t* log_count;       // [kLogShards] singles reserved per shard
+  uint32_t* log_count;       // [3][kLogShards]: singles, medium, dense records reserved per shard
   uint64_t* dlog;            // [kLogShards][dlog_cap][dense_words(k)] dense lane records
-  uint32_t* dlog_count;      // [kLogShards] dense records reserved per shard
+  uint32_t* dlog_count;      // = log_count + 2 * kLogShards
   uint32_t* upd_count;       // [kLogShards] StatusUpdates emitted (singles + medium + dense)
-  uint64_t* mlog;            // [kLogShards][mlog_cap][2] medium lane records (med_field)
-  uint32_t* mlog_count;      // [kLogShards] medium records reserved per shard
+  uint64_t* mlog;            // [kLogShards][mlog_cap][med_rec_words()] medium lane records
+  uint32_t* mlog_count;      // = log_count + kLogShards
   uint32_t* log_overflow;    // [1]
   uint32_t* node_flags;      // [NL] capped path: nodes left to the exact pass (nullptr: none)
   // exact pass (k_round_capped behind k_round_node / k_replay_node): node_flags[nl] = 1 + the first

@@ -648,12 +648,23 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
   updates += wave_sum(cnt);
   if (p.ablate_emit == 1u) return r;  // diagnostics: the cost of the round without its log stores
   // one atomic instruction, lanes 0 / 1 / 2 reserving the singles / medium / dense runs
+  // The three counter arrays are one allocation, [singles | medium | dense] x kLogShards (engine.cpp),
+  // so lane q's counter is an offset from one kernel argument: a per-lane choice among three pointer
+  // arguments compiles to a load of the chosen argument from the kernarg segment, and the wait for
+  // that load (vmcnt(0)) also waited for every store and load the wave had in flight.
   const uint32_t want = lane == 0 ? r.tot_s : lane == 1 ? r.tot_m : lane == 2 ? r.tot_d : 0u;
-  uint32_t* const ctr = lane == 0 ? p.log_count : lane == 1 ? p.mlog_count : p.dlog_count;
+  // (opaque: the per-lane offset is formed here, not hoisted out of the caller's tile loop as a
+  // 64-bit address that spills to scratch and is reloaded, with a vmcnt(0) wait, before each atomic)
+  uint32_t cofs = min(lane, 2u) * kLogShards;
+  asm volatile("" : "+v"(cofs));
+  uint32_t* const ctr = p.log_count + cofs;
   if (p.ablate_emit >= 2u) {  // diagnostics (log invalid): stores at made-up per-wave positions; 3: the
     // reserving atomic still issued, its result unused (no wait for it)
     const uint32_t wv = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const uint32_t cap = lane == 0 ? p.log_cap : lane == 1 ? p.mlog_cap : p.dlog_cap;
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.log_cap);
+    const uint32_t c1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.mlog_cap);
+    const uint32_t c2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.dlog_cap);
+    const uint32_t cap = lane == 0 ? c0 : lane == 1 ? c1 : c2;
     r.raw = cap > 8192u ? (wv * 509u) % (cap - 4096u) : 0u;
     if (p.ablate_emit == 3u && want) atomicAdd(ctr + shard, want);
     return r;

@@ -458,9 +458,16 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
   for (int i = 0; i < 8; ++i) C[i] = pld<NT>(tp + 1024u + (uint32_t)i * 64u + tl);
   const uint32_t R = p.fuse_rounds;
-  uint32_t w[K], cw[K], w1[K], cw1[K];
-  replay_load<K>(p.replay, g, w, cw);
-  if (R > 1u) replay_load<K>(p.replay + p.replay_stride, g, w1, cw1);
+  // replayed (yes, consider) word pairs as loaded: {w_2i, cw_2i, w_2i+1, cw_2i+1} per dwordx4 (kept as
+  // vectors, so the refilled buffer is the loads' own registers across the loop)
+  constexpr int RQ = (K + 1) / 2;
+  const u32x4* const rq = reinterpret_cast<const u32x4*>(p.replay) + (size_t)(g >> 6) * (RQ * 64) + (g & 63u);
+  const size_t rstride = p.replay_stride / 4u;  // u32x4 per round
+  u32x4 wb0[RQ], wb1[RQ];
+#pragma unroll
+  for (int i = 0; i < RQ; ++i) wb0[i] = pld4<true>(rq + i * 64);
+#pragma unroll
+  for (int i = 0; i < RQ; ++i) wb1[i] = pld4<true>(rq + (R > 1u ? rstride : 0u) + i * 64);  // (R = 1: unused)
   // eligibility: every record of lanes 0..127 live and valid
   const bool all = __syncthreads_and((~k1[3] & vmask) == ~0u) != 0;
   if (!all) return;  // workgroup-uniform: k_replay_node runs the node
@@ -500,32 +507,33 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   const uint32_t maxc = max(wmax[0], wmax[1]);
   const uint32_t J = maxc >= 120u ? 0u : (120u - maxc + (uint32_t)K - 1u) / (uint32_t)K;
   uint32_t done = R, applied = 0u, upd = 0u, emitted = 0u, pubs = 0u;
-  // the replayed votes are prefetched two rounds ahead (w: this round, w1: the next one, loaded
-  // above): a round's compute is shorter than a load's latency with two waves per SIMD
-  // StatusUpdates (k = 8: medium records, one entry per lane): round r's log space is reserved at the
-  // end of round r and its entries stored after round r + 1's slot network, so the reserving atomics'
-  // round trip overlaps a round of compute instead of stalling every round
-  EmitRes pend{};
-  uint32_t Epend[K], Apend = 0u;
-  bool have_pend = false;
+  // The replayed votes are prefetched two rounds ahead into two register buffers, (wb0) for even
+  // rounds and (wb1) for odd ones (the loop is unrolled twice): a round refills its own buffer with
+  // round r + 2's votes as soon as it has read them, and no register is copied while a load into it
+  // is in flight (a rotating copy made every round wait for the load issued at its start).
+  // StatusUpdates (k = 8: one entry per lane): round r's log space is reserved at the end of round r
+  // and its entries stored after round r + 1's slot network, so the reserving atomics' round trip
+  // overlaps a round of compute; the pending reservations alternate between two sets of registers too.
+  EmitRes pendA{}, pendB{};
+  uint32_t EpA[K], EpB[K], ApA = 0u, ApB = 0u;
   const uint32_t shard = wave_id % p.log_shards;  // once (a runtime modulo is a long sequence)
-  for (uint32_t r = 0; r < R; ++r) {
+  auto step = [&](uint32_t r, u32x4 (&wb)[RQ], EmitRes& pc, uint32_t (&Ec)[K], uint32_t& Ac,
+                  const EmitRes& pp, const uint32_t (&Ep)[K], uint32_t Ap) -> bool {
     if (r >= J) {  // a record with count >= 120 may finalize (and leave the poll set) this round
       const uint32_t nearfin = Kp[6] & Kp[5] & Kp[4] & Kp[3];
       if (__syncthreads_or(nearfin != 0u)) {  // workgroup-uniform
         done = r;
-        break;
+        return false;
       }
     }
-    uint32_t nw[K], ncw[K];
-    const bool more = r + 2u < R;
-    if (more) replay_load<K>(p.replay + (size_t)(r + 2u) * p.replay_stride, g, nw, ncw);
-    uint32_t ys[7 + K], ns[7 + K];
+    uint32_t ys[7 + K], ns[7 + K], cv[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const uint32_t yw = w[j] & cw[j];  // err == 0 implies considered (vote.go:55-56)
+      const uint32_t wj = wb[j >> 1][(j & 1) * 2];
+      cv[j] = wb[j >> 1][(j & 1) * 2 + 1];
+      const uint32_t yw = wj & cv[j];  // err == 0 implies considered (vote.go:55-56)
       ys[7 + j] = yw;
-      ns[7 + j] = ~yw & cw[j];
+      ns[7 + j] = ~yw & cv[j];
     }
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
@@ -535,8 +543,21 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
     for (int i = 7; i >= 0; --i) {  // every record shifts in the K votes
       V[i] = i < K ? ys[6 + K - i] : V[i - K];
-      C[i] = i < K ? cw[K - 1 - i] : C[i - K];
+      if (i < K) {  // a real copy: C must not stay in the buffer's registers, which the refill reuses
+        uint32_t cc;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(cc) : "v"(cv[K - 1 - i]));
+        C[i] = cc;
+      } else {
+        C[i] = C[i - K];
+      }
     }
+    // the buffer is read: refill it with round r + 2's votes (unconditionally — the last two rounds
+    // reload round R - 1's, unused — so that the loaded registers need no merge copy, which would wait)
+    // (no instruction crosses this point: the loads below are not hoisted above the buffer's last
+    // reads, so the buffer and the loads' destinations can be the same registers across the loop)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < RQ; ++i) wb[i] = pld4<true>(rq + (size_t)min(r + 2u, R - 1u) * rstride + i * 64);
     uint32_t E[K], alive = ~0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u, ap = 0u;
     const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
     round_slots<K, false>(ys, ns, low3, 0u, false, alive, A, E, c, F, ap);
@@ -555,30 +576,33 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       ++pubs;
     }
     if constexpr (K == 8) {
-      const EmitRes cur = emit_reserve_med<K>(p, shard, lane, E, 0u, upd);
-      if (have_pend)
-        emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Epend, Apend, 0u, pend, p.round_rel + r - 1u);
+      pc = emit_reserve_med<K>(p, shard, lane, E, 0u, upd);
+      if (r > 0u)
+        emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Ep, Ap, 0u, pp, p.round_rel + r - 1u);
 #pragma unroll
-      for (int j = 0; j < K; ++j) Epend[j] = E[j];
-      Apend = A;
-      pend = cur;
-      have_pend = true;
+      for (int j = 0; j < K; ++j) Ec[j] = E[j];
+      Ac = A;
     } else {
+      (void)pc;
+      (void)Ec;
+      (void)Ac;
+      (void)pp;
+      (void)Ep;
+      (void)Ap;
       emitted += emit_updates_flat<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, 0u, upd, p.round_rel + r);
     }
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      w[j] = w1[j];
-      cw[j] = cw1[j];
-      if (more) {
-        w1[j] = nw[j];
-        cw1[j] = ncw[j];
-      }
-    }
+    return true;
+  };
+  for (uint32_t r = 0; r < R; r += 2u) {
+    if (!step(r, wb0, pendA, EpA, ApA, pendB, EpB, ApB)) break;
+    if (r + 1u >= R || !step(r + 1u, wb1, pendB, EpB, ApB, pendA, EpA, ApA)) break;
   }
   if constexpr (K == 8) {  // the last round run's entries (round done - 1)
-    if (have_pend)
-      emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Epend, Apend, 0u, pend, p.round_rel + done - 1u);
+    if (done > 0u) {
+      const bool odd = ((done - 1u) & 1u) != 0u;
+      emitted += odd ? emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpB, ApB, 0u, pendB, p.round_rel + done - 1u)
+                     : emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpA, ApA, 0u, pendA, p.round_rel + done - 1u);
+    }
   }
   if (done < R && b == 0) p.node_flags[nl] = done + 1u;  // the exact pass takes rounds done..R-1
   if (done > 0u) {

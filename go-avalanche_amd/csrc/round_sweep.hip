@@ -326,6 +326,9 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   const LaneIdx x = lane_idx(p, tile, lane);
   const bool active = x.active;
   const uint32_t b = x.b, node = x.node;
+  // the node's Byzantine bit from the word loaded with the tile (a load of it here, after the plane
+  // stores, made the wave wait for those stores: vmcnt counts in issue order)
+  const bool nbyz = ((in.byzw >> (node & 31u)) & 1u) != 0u;
   uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
   u32x4* const grp = reinterpret_cast<u32x4*>(tp) + lane;
   const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(tp, 0, kPlanes * 64 * 4, kRsrcWord3);
@@ -542,17 +545,17 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     }
     if (astore) st1<POL>(tr, tp + 1536u + lane, (1536u + lane) * 4u, A);
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^31
-    const uint32_t pub = is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A;
+    const uint32_t pub = nbyz ? byz_pattern(p.round + 1u) : A;
     if (p.uni_out) acc.umis |= pub != in.uref ? 1u : 0u;  // uniform rows (kernels.h)
     const bool known = AVK_CC_PREFETCH || (kdefer && pend >= 2u);  // (publish)
-    publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? in.old : (is_byz(p.byz, node) ? byz_pattern(p.round - 2u) : pub),
-                     acc.changed, known);
+    publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? in.old : (nbyz ? byz_pattern(p.round - 2u) : pub), acc.changed,
+                     known);
     // a record deleted this round keeps the vote/consider planes stored
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
   }
   if (REF && p.rflag_out && settled) {  // reference-row flag of the row a settled tile just published
-    ref_flag_store(p, lane, active, b, node, is_byz(p.byz, node) ? byz_pattern(p.round + 1u) : A,
+    ref_flag_store(p, lane, active, b, node, nbyz ? byz_pattern(p.round + 1u) : A,
                    p.pref_in[p.ref_node * p.PS + (active ? b : 0u)]);
     if (active) acc.lane_bytes += 4u + (b == 0u ? 1u : 0u);
   }
