@@ -177,6 +177,8 @@ for s in "$@"; do
     ablate5) step ablate5 600 bash -c 'for w in c4p; do for o in "ablate_phase=0" "ablate_phase=1" "ablate_phase=2" "ablate_phase=4" "ablate_phase=16" "ablate_emit=1" "ablate_phase=7 --option ablate_emit=1"; do echo "== $w $o"; AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_ablate.so python tools/round_probe.py --workload $w --rounds 8 --option $o | grep -v "^{\"workload"; done; done' ;;
     tshard2) step tshard2 600 python tools/shard_model.py --workload c4 --kinds targets --ranks 2,4,8 --json gpurun_out/tshard_c4_default.json ;;
     c2x) step c2x 600 bash -c 'AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_c2x.so python -u -m pytest tests/test_gpu_replay_fused.py tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread -k "replay or c2 or capped or fused" && for v in new c2x new c2x; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
+    full4p) step full4p 900 python -u -m pytest tests/test_gpu_fullsize.py tests/test_gpu_bench_protocol.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
+    abs5) step abs5 900 bash -c 'for w in c4 c4p c4pb; do for v in new walk0; do echo "== $w $v"; if [ $v = new ]; then python tools/round_probe.py --workload $w; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w; fi; done; done; for v in new walk0 new walk0; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
     c2ab) step c2ab 300 bash -c 'for v in new s3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
     reh2pb) step reh2pb 600 python bench.py --gpus 2 --rehearse-one-gpu --workload c4pb --shard peers --no-secondary --detail gpurun_out/rehearse2_c4pb_detail.json ;;
     reh2t) step reh2t 600 python bench.py --gpus 2 --rehearse-one-gpu --shard targets --no-secondary --detail gpurun_out/rehearse2_targets_detail.json ;;
