@@ -873,9 +873,9 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->log, (size_t)e->log_cap * e->log_shards)) != hipSuccess) return hip_fail(he, "alloc log");
   // the singles', medium and dense records' per-shard counters: one array (round_common.h
   // emit_reserve_med indexes it by kind)
-  if ((he = dev_alloc(&e->log_count, 3 * avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc log");
-  e->mlog_count = e->log_count + avk::kLogShards;
-  e->dlog_count = e->log_count + 2 * avk::kLogShards;
+  if ((he = dev_alloc(&e->log_count, 3 * avk::kLogShards * avk::kCtrStride)) != hipSuccess) return hip_fail(he, "alloc log");
+  e->mlog_count = e->log_count + avk::kLogShards * avk::kCtrStride;
+  e->dlog_count = e->log_count + 2 * avk::kLogShards * avk::kCtrStride;
   // a dense record holds >= dense_min(k) updates: log_cap / dense_min records
   // take any log_cap updates that go dense (8 B of capacity per update)
   const uint32_t dw = avk::dense_words((uint32_t)e->k);
@@ -891,8 +891,7 @@ int av_create(const av_config* cfg, av_engine** out) {
   e->mlog_cap = e->k == 8 ? std::max<uint32_t>(e->log_cap / 2, 16) : 16u;
   if ((he = dev_alloc(&e->mlog, (size_t)e->mlog_cap * e->log_shards * avk::med_rec_words())) != hipSuccess)
     return hip_fail(he, "alloc log");
-  (void)hipMemsetAsync(e->mlog_count, 0, avk::kLogShards * 4, e->stream);
-  (void)hipMemsetAsync(e->dlog_count, 0, avk::kLogShards * 4, e->stream);
+  (void)hipMemsetAsync(e->log_count, 0, (size_t)3 * avk::kLogShards * avk::kCtrStride * 4, e->stream);
   (void)hipMemsetAsync(e->upd_count, 0, avk::kLogShards * 4, e->stream);
   if ((he = dev_alloc(&e->log_overflow, 1)) != hipSuccess) return hip_fail(he, "alloc log");
   if (e->capped) {
@@ -910,7 +909,6 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->changed, 2 * avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
   (void)hipMemsetAsync(e->changed, 0, 2 * avk::kLogShards * 8, e->stream);
 
-  (void)hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream);
   (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
   (void)hipMemsetAsync(e->applied, 0, avk::kLogShards * 8, e->stream);
   (void)hipMemsetAsync(e->pref[0], 0, e->pref_alloc_words * 4, e->stream);
@@ -1561,9 +1559,7 @@ int av_log_base_round(av_engine* e, int64_t* out) {
 
 // Reset the three log counters (and the overflow flag) on the engine stream.
 int clear_log(av_engine* e) {
-  AV_HIP(hipMemsetAsync(e->log_count, 0, avk::kLogShards * 4, e->stream));
-  AV_HIP(hipMemsetAsync(e->dlog_count, 0, avk::kLogShards * 4, e->stream));
-  AV_HIP(hipMemsetAsync(e->mlog_count, 0, avk::kLogShards * 4, e->stream));
+  AV_HIP(hipMemsetAsync(e->log_count, 0, (size_t)3 * avk::kLogShards * avk::kCtrStride * 4, e->stream));
   AV_HIP(hipMemsetAsync(e->upd_count, 0, avk::kLogShards * 4, e->stream));
   AV_HIP(hipMemsetAsync(e->log_overflow, 0, 4, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
@@ -1607,9 +1603,13 @@ int read_log_counts(av_engine* e, LogCounts& c) {
   c.dense.assign(avk::kLogShards, 0);
   c.upd.assign(avk::kLogShards, 0);
   c.med.assign(avk::kLogShards, 0);
-  AV_HIP(hipMemcpyAsync(c.singles.data(), e->log_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
-  AV_HIP(hipMemcpyAsync(c.dense.data(), e->dlog_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
-  AV_HIP(hipMemcpyAsync(c.med.data(), e->mlog_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
+  // the three kinds' counters, one per 128-B line (kernels.h kCtrStride): copied 2-D, element 0 of each
+  AV_HIP(hipMemcpy2DAsync(c.singles.data(), 4, e->log_count, avk::kCtrStride * 4, 4, avk::kLogShards,
+                          hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpy2DAsync(c.dense.data(), 4, e->dlog_count, avk::kCtrStride * 4, 4, avk::kLogShards,
+                          hipMemcpyDeviceToHost, e->stream));
+  AV_HIP(hipMemcpy2DAsync(c.med.data(), 4, e->mlog_count, avk::kCtrStride * 4, 4, avk::kLogShards,
+                          hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipMemcpyAsync(c.upd.data(), e->upd_count, avk::kLogShards * 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipMemcpyAsync(&c.ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));

@@ -28,6 +28,9 @@ namespace avk {
 constexpr int kPlanes = 25;
 constexpr int kPV = 0, kPC = 8, kPA = 16, kPK = 17;
 constexpr uint32_t kLogShards = 1024;   // update-log / counter shards
+// u32 elements between two shards' log counters: one counter per 128-B line, so that the reserving
+// atomics of different shards (3 per wave-tile in a storm round) do not serialize on shared lines
+constexpr uint32_t kCtrStride = 32;
 constexpr uint32_t kMaxPoll = 4096;     // AvalancheMaxElementPoll, avalanche.go:17
 constexpr int kMaxK = 16;
 constexpr int kMaxPeers = 15;           // peer-push exchange: other ranks of a node-sharded network
@@ -66,12 +69,12 @@ struct RoundParams {
   const uint32_t* byz;       // [ceil(N/32)] Byzantine node bits
   const uint32_t* replay;    // replay mode: yes/consider words of each lane and slot (replay_idx)
   uint64_t* log;             // [kLogShards][log_cap] single StatusUpdates
-  uint32_t* log_count;       // [3][kLogShards]: singles, medium, dense records reserved per shard
+  uint32_t* log_count;       // [3][kLogShards][kCtrStride]: singles, medium, dense records reserved per shard (element 0)
   uint64_t* dlog;            // [kLogShards][dlog_cap][dense_words(k)] dense lane records
-  uint32_t* dlog_count;      // = log_count + 2 * kLogShards
+  uint32_t* dlog_count;      // = log_count + 2 * kLogShards * kCtrStride
   uint32_t* upd_count;       // [kLogShards] StatusUpdates emitted (singles + medium + dense)
   uint64_t* mlog;            // [kLogShards][mlog_cap][med_rec_words()] medium lane records
-  uint32_t* mlog_count;      // = log_count + kLogShards
+  uint32_t* mlog_count;      // = log_count + kLogShards * kCtrStride
   uint32_t* log_overflow;    // [1]
   uint32_t* node_flags;      // [NL] capped path: nodes left to the exact pass (nullptr: none)
   // exact pass (k_round_capped behind k_round_node / k_replay_node): node_flags[nl] = 1 + the first

@@ -727,7 +727,7 @@ __global__ void k_count_live(const uint32_t* planes, const uint32_t* valid, cons
 __global__ void k_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets, uint32_t log_cap,
                               uint32_t words, uint64_t* out) {
   const uint32_t shard = blockIdx.x;
-  const uint32_t n = min(counts[shard], log_cap) * words;
+  const uint32_t n = min(counts[shard * kCtrStride], log_cap) * words;
   const uint64_t* src = log + (size_t)shard * log_cap * words;
   uint64_t* dst = out + offsets[shard] * words;
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];

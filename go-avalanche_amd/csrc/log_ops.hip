@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
   const uint32_t stride = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t s = 0, x = 0, c = 0;
-  const uint32_t n = min(counts[shard], cap);
+  const uint32_t n = min(counts[shard * kCtrStride], cap);
   const uint64_t* src = log + (size_t)shard * cap;
   for (uint32_t i = t; i < n; i += stride) {
     const uint64_t w = src[i];
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
     ++c;
   }
   const uint32_t DW = dense_words(K);
-  const uint32_t nd = min(dcounts[shard], dcap);
+  const uint32_t nd = min(dcounts[shard * kCtrStride], dcap);
   const uint64_t* dsrc = dlog + (size_t)shard * dcap * DW;
   for (uint32_t i = t; i < nd; i += stride) {
     const uint32_t* rw = reinterpret_cast<const uint32_t*>(dsrc + (size_t)i * DW);
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
       ++c;
     });
   }
-  const uint32_t nm = mlog ? min(mcounts[shard], mcap) : 0u;
+  const uint32_t nm = mlog ? min(mcounts[shard * kCtrStride], mcap) : 0u;
   constexpr uint32_t MW = med_rec_words();
   const uint64_t* msrc = mlog + (size_t)shard * mcap * MW;
   for (uint32_t i = t; i < nm; i += stride) {

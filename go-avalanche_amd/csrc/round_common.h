@@ -361,8 +361,8 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
     base = p.log_cap > 8192u ? (wave_id * 509u) % (p.log_cap - 4096u) : 0u;
     dbase = p.dlog_cap > 128u ? (wave_id * 131u) % (p.dlog_cap - 64u) : 0u;
   } else if (lane == 0) {
-    if (tot_s) base = atomicAdd(&p.log_count[shard], tot_s);
-    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard], tot_d);
+    if (tot_s) base = atomicAdd(&p.log_count[shard * kCtrStride], tot_s);
+    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard * kCtrStride], tot_d);
   }
   base = (uint32_t)__shfl((int)base, 0, 64);
   dbase = (uint32_t)__shfl((int)dbase, 0, 64);
@@ -464,8 +464,8 @@ __device__ __forceinline__ uint32_t emit_updates_flat(const RoundParams& p, uint
     base = p.log_cap > 8192u ? (wave_id * 509u) % (p.log_cap - 4096u) : 0u;
     dbase = p.dlog_cap > 128u ? (wave_id * 131u) % (p.dlog_cap - 64u) : 0u;
   } else if (lane == 0) {
-    if (tot_s) base = atomicAdd(&p.log_count[shard], tot_s);
-    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard], tot_d);
+    if (tot_s) base = atomicAdd(&p.log_count[shard * kCtrStride], tot_s);
+    if (tot_d) dbase = atomicAdd(&p.dlog_count[shard * kCtrStride], tot_d);
   }
   base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
   dbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)dbase);
@@ -648,14 +648,14 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
   updates += wave_sum(cnt);
   if (p.ablate_emit == 1u) return r;  // diagnostics: the cost of the round without its log stores
   // one atomic instruction, lanes 0 / 1 / 2 reserving the singles / medium / dense runs
-  // The three counter arrays are one allocation, [singles | medium | dense] x kLogShards (engine.cpp),
+  // The three counter arrays are one allocation, [singles | medium | dense] x kLogShards x kCtrStride (engine.cpp),
   // so lane q's counter is an offset from one kernel argument: a per-lane choice among three pointer
   // arguments compiles to a load of the chosen argument from the kernarg segment, and the wait for
   // that load (vmcnt(0)) also waited for every store and load the wave had in flight.
   const uint32_t want = lane == 0 ? r.tot_s : lane == 1 ? r.tot_m : lane == 2 ? r.tot_d : 0u;
   // (opaque: the per-lane offset is formed here, not hoisted out of the caller's tile loop as a
   // 64-bit address that spills to scratch and is reloaded, with a vmcnt(0) wait, before each atomic)
-  uint32_t cofs = min(lane, 2u) * kLogShards;
+  uint32_t cofs = (min(lane, 2u) * kLogShards + shard) * kCtrStride;
   asm volatile("" : "+v"(cofs));
   uint32_t* const ctr = p.log_count + cofs;
   if (p.ablate_emit >= 2u) {  // diagnostics (log invalid): stores at made-up per-wave positions; 3: the
@@ -666,10 +666,10 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
     const uint32_t c2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.dlog_cap);
     const uint32_t cap = lane == 0 ? c0 : lane == 1 ? c1 : c2;
     r.raw = cap > 8192u ? (wv * 509u) % (cap - 4096u) : 0u;
-    if (p.ablate_emit == 3u && want) atomicAdd(ctr + shard, want);
+    if (p.ablate_emit == 3u && want) atomicAdd(ctr, want);
     return r;
   }
-  if (want) r.raw = atomicAdd(ctr + shard, want);
+  if (want) r.raw = atomicAdd(ctr, want);
   return r;
 }
 

@@ -558,9 +558,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < RQ; ++i) wb[i] = pld4<true>(rq + (size_t)min(r + 2u, R - 1u) * rstride + i * 64);
-    uint32_t E[K], alive = ~0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u, ap = 0u;
+    // the round's update masks go straight into this round's pending set (no copy)
+    uint32_t alive = ~0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u, ap = 0u;
     const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
-    round_slots<K, false>(ys, ns, low3, 0u, false, alive, A, E, c, F, ap);
+    round_slots<K, false>(ys, ns, low3, 0u, false, alive, A, Ec, c, F, ap);
     applied += (uint32_t)K * 32u;
     uint32_t cy = 0u;
 #pragma unroll
@@ -576,20 +577,17 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       ++pubs;
     }
     if constexpr (K == 8) {
-      pc = emit_reserve_med<K>(p, shard, lane, E, 0u, upd);
+      pc = emit_reserve_med<K>(p, shard, lane, Ec, 0u, upd);
       if (r > 0u)
         emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Ep, Ap, 0u, pp, p.round_rel + r - 1u);
-#pragma unroll
-      for (int j = 0; j < K; ++j) Ec[j] = E[j];
       Ac = A;
     } else {
       (void)pc;
-      (void)Ec;
       (void)Ac;
       (void)pp;
       (void)Ep;
       (void)Ap;
-      emitted += emit_updates_flat<K>(p, wave_id, lane, node, p.t0 + b * 32u, E, A, 0u, upd, p.round_rel + r);
+      emitted += emit_updates_flat<K>(p, wave_id, lane, node, p.t0 + b * 32u, Ec, A, 0u, upd, p.round_rel + r);
     }
     return true;
   };
