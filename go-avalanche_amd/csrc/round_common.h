@@ -580,6 +580,12 @@ __device__ __forceinline__ uint32_t select_slot_bfi(const uint32_t (&E)[K], uint
 #ifndef AVK_MED_WALK
 #define AVK_MED_WALK 1
 #endif
+// StatusUpdate log stores (k = 8 slot-record path) non-temporal: the log is read only after the
+// round, so its lines need not displace the gathered preference rows in L2 / MALL (A/B,
+// profiles/r04/session11/ablognt.log: C4p -3.1 / -3.7 %, C4 -3.6 %, C4pb -1.7 % per epoch)
+#ifndef AVK_LOG_NT
+#define AVK_LOG_NT 1
+#endif
 
 // A/B build knob: lanes with at least this many updates log a dense record (0: the default, above
 // kMedMax; 2: no medium records, the walk that folds a lane's updates into one is never run)
@@ -702,9 +708,9 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
         constexpr uint32_t DW = dense_words(K);
         uint64_t* const rec = p.dlog + ((size_t)shard * p.dlog_cap + dbase + rank) * DW;
         u32x4* const q = reinterpret_cast<u32x4*>(rec);
-        q[0] = u32x4{(uint32_t)key, (uint32_t)(key >> 32), E[0], E[1]};
-        q[1] = u32x4{E[2], E[3], E[4], E[5]};
-        q[2] = u32x4{E[6], E[7], A_final, died};
+        pst4<AVK_LOG_NT>(q, u32x4{(uint32_t)key, (uint32_t)(key >> 32), E[0], E[1]});
+        pst4<AVK_LOG_NT>(q + 1, u32x4{E[2], E[3], E[4], E[5]});
+        pst4<AVK_LOG_NT>(q + 2, u32x4{E[6], E[7], A_final, died});
       }
     } else {
       // the first 4 slots with updates, in slot order: shift in from the last slot down
@@ -721,15 +727,17 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
         if (rank < st_m) {
           const bool hasd = died != 0u;  // then at most 3 slots: the died plane takes the 4th word
           u32x4* const q = reinterpret_cast<u32x4*>(p.mlog + ((size_t)shard * p.mlog_cap + mbase + rank) * 4u);
-          q[0] = u32x4{(uint32_t)key, (uint32_t)(key >> 32), nz | (hasd ? kMedS4Died : 0u), A_final};
-          q[1] = u32x4{o0, o1, o2, hasd ? died : o3};
+          pst4<AVK_LOG_NT>(q, u32x4{(uint32_t)key, (uint32_t)(key >> 32), nz | (hasd ? kMedS4Died : 0u), A_final});
+          pst4<AVK_LOG_NT>(q + 1, u32x4{o0, o1, o2, hasd ? died : o3});
         }
       } else if (single && rank < st_s) {
         // the one update: slot ffbl(nz), record ffbl(o0); status from A_final and died (vote.go:77-91)
         const uint32_t j = ffbl_u32(nz), bit = ffbl_u32(o0);
         const uint32_t a = bfe1(A_final, bit), d = bfe1(died, bit);
         const uint32_t st = (a << 1) | (~(a ^ d) & 1u);
-        p.log[(size_t)shard * p.log_cap + base + rank] = key + ((uint64_t)j << 24) + ((uint64_t)bit << 2) + st;
+        uint64_t* const w = p.log + (size_t)shard * p.log_cap + base + rank;
+        const uint64_t word = key + ((uint64_t)j << 24) + ((uint64_t)bit << 2) + st;
+        if constexpr (AVK_LOG_NT) __builtin_nontemporal_store(word, w); else *w = word;
       }
     }
     if (__ballot(ovf) != 0ull) note_overflow(p, lane);
