@@ -943,14 +943,20 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
 // the node's own row: timing diagnostics only, results invalid), kModeWarmPipe
 // (kModeWarm for a resident grid: the next tile's loads are issued before the
 // current tile is computed; 93 VGPRs, 5 waves per SIMD).
-// A/B build knob (Makefile variant libraries): the warm modes' waves per SIMD. 6 (80 VGPRs, 7
-// spilled to scratch in cold paths) beat 5 (87 VGPRs): C4p / C4pb epochs -4 %, C4 storm rounds -2 to
-// -3 %; 7 (54 spilled) ran storm rounds 1.7x slower (profiles/r03/ab_waves_per_simd.log)
+// A/B build knob (Makefile variant libraries): the warm modes' waves per SIMD. Round 3: 6 (80 VGPRs,
+// 7 spilled to scratch in cold paths) beat 5 (87 VGPRs) by 4 % (profiles/r03/ab_waves_per_simd.log).
+// Round 4 (slot records, non-temporal log): 5 (92 VGPRs, none spilled) beats 6 (80, 8-9 spilled):
+// C4p epoch -2.8 / -2.9 %, C4 -0.9 / -1.4 %, C4pb -1.1 %; 7 is 1.3x slower
+// (profiles/r04/session13/abwpe.log; 4 compiles to the same code as 5)
 #ifndef AVK_WARM_WPE
-#define AVK_WARM_WPE 6
+#define AVK_WARM_WPE 5
+#endif
+// (the fresh mode at 5 instead: round 0 -1 %, epochs within noise, profiles/r04/session15/abf5.log)
+#ifndef AVK_FRESH_WPE
+#define AVK_FRESH_WPE 6
 #endif
 template <int K, int MODE, int POL, bool REF = false, bool CC = true>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeWarm ? AVK_WARM_WPE : MODE == kModeReplay || MODE == kModeFresh ? 6 : 7))) void k_round_sweep(const RoundParams p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kModeWarmPipe ? 5 : MODE == kModeWarm ? AVK_WARM_WPE : MODE == kModeFresh ? AVK_FRESH_WPE : MODE == kModeReplay ? 6 : 7))) void k_round_sweep(const RoundParams p) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave0 = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * 4u;
