@@ -348,24 +348,28 @@ class Runner:
         self.steps(pos, timed=False)
 
 
+def log_capacity(n, m, world, rank, shard):
+    """StatusUpdate log entries for one rank's engine: every update of one timed
+    segment (up to 16 rounds: C4 ~2e8 in rounds 0-2, the conflicting C4p/C4pb
+    ~1e9 over rounds 0-8) of the rank's share of the network. 36 B of device
+    memory per entry at k = 8 (singles 8, slot records 16, dense records 12 B of
+    capacity per update): 45 GB at 1M x 1000 and 77 GB for C5 on one GPU."""
+    n_loc, m_loc = n, m
+    if world > 1:
+        if shard == "targets":
+            t0, t1 = sharding.target_shard(m, world, rank)
+            m_loc = t1 - t0
+        else:
+            n_loc = -(-n // world)
+    return min(int(1.25 * n_loc * m_loc) + (1 << 20), (1 << 31) - 1)
+
+
 def measure(wl, args, world, rank, local_rank, steps, warmup):
     """This rank's shard of workload `wl`: device warm-up (one untimed epoch),
     `warmup` untimed steps, `steps` timed steps; then a second pass over the
     same steps with HIP events around every round kernel (roofline)."""
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
-    # the log holds every StatusUpdate of one timed segment (up to 16 rounds:
-    # C4 ~2e8 in rounds 0-2, the conflicting C4p/C4pb ~1e9 over rounds 0-8);
-    # 36 B of device memory per entry at k = 8 (singles 8, slot records 16, dense
-    # records 12 B of capacity per update): 45 GB at 1M x 1000, 77 GB for C5 on one
-    # GPU; a rank's log holds its shard's updates only (sized by its share)
-    n_loc, m_loc = n, m
-    if world > 1:
-        if args.shard == "targets":
-            t0, t1 = sharding.target_shard(m, world, rank)
-            m_loc = t1 - t0
-        else:
-            n_loc = -(-n // world)
-    log_cap = min(int(1.25 * n_loc * m_loc) + (1 << 20), (1 << 31) - 1)
+    log_cap = log_capacity(n, m, world, rank, args.shard)
     run = Runner(wl, args, world, rank, local_rank, log_cap)
     if run.fallback is not None:
         args.shard = "targets"

@@ -137,3 +137,16 @@ def test_line_roofline_is_compact():
         assert k in c
     assert set(c["kinds"]) == {"fresh", "storm", "klazy"}
     assert len(json.dumps(c)) < 900
+
+
+def test_log_capacity_follows_the_shard():
+    full = bench.log_capacity(1_000_000, 1000, 1, 0, "targets")
+    assert full == int(1.25 * 1_000_000 * 1000) + (1 << 20)
+    # target shards: the rank's targets (whole 32-target blocks), not the network's
+    parts = [bench.log_capacity(1_000_000, 1000, 4, r, "targets") for r in range(4)]
+    assert all(p < full / 3 for p in parts)
+    assert sum(p - (1 << 20) for p in parts) == int(1.25 * 1_000_000 * 1000)
+    # node shards: the rank's nodes
+    assert bench.log_capacity(1_000_000, 1000, 8, 3, "peers") == int(1.25 * 125_000 * 1000) + (1 << 20)
+    # capped below 2^31 entries per engine
+    assert bench.log_capacity(10_000_000, 256, 1, 0, "targets") == (1 << 31) - 1
