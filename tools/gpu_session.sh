@@ -190,6 +190,7 @@ for s in "$@"; do
     abf5) step abf5 600 bash -c 'for w in c4 c4p c4 c4p c4pb c5; do for v in w5 f5; do echo "== $w $v"; AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w > gpurun_out/rp_tmp.txt 2>/dev/null; head -1 gpurun_out/rp_tmp.txt; tail -1 gpurun_out/rp_tmp.txt; done; done' ;;
     self4s) step self4s 900 python bench.py --gpus 4 --rehearse-one-gpu --detail gpurun_out/rehearse4s_detail.json ;;
     abrun8) step abrun8 600 bash -c 'for w in c4 c4p c4 c4p c4pb; do for o in "tiles_per_wave=0 --option uni_merge=1" "tiles_per_wave=8 --option uni_merge=2" "tiles_per_wave=4 --option uni_merge=4"; do echo "== $w $o"; python tools/round_probe.py --workload $w --option $o | tail -1; done; done' ;;
+    abc5tpw) step abc5tpw 600 bash -c 'for w in c5 c5; do for o in 0 4 16; do echo "== $w tpw=$o"; python tools/round_probe.py --workload $w --option tiles_per_wave=$o | tail -1; done; done' ;;
     c2ab) step c2ab 300 bash -c 'for v in new s3; do echo "== c2 $v"; if [ $v = new ]; then python tools/fuse_probe.py; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py; fi; done' ;;
     reh2pb) step reh2pb 600 python bench.py --gpus 2 --rehearse-one-gpu --workload c4pb --shard peers --no-secondary --detail gpurun_out/rehearse2_c4pb_detail.json ;;
     reh2t) step reh2t 600 python bench.py --gpus 2 --rehearse-one-gpu --shard targets --no-secondary --detail gpurun_out/rehearse2_targets_detail.json ;;
