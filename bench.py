@@ -222,8 +222,11 @@ def cpu_baseline(wl, seed, budget_s):
     sim.close()
     return {"value": applied / dt, "unit": "vote-record updates/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "host_cpus": hc,
-            "sample_short": f"oracle C restatement, {ns} x {m}, rounds 0..{rounds - 1}, {dt:.1f}s, {threads} threads",
-            "sample": f"oracle/avalanche_oracle.c (C restatement of vote.go/processor.go, the parity oracle), "
+            "sample_short": f"oracle C restatement (branch-free bit-plane path, AVX2 target clone), {ns} x {m}, "
+                            f"rounds 0..{rounds - 1}, {dt:.1f}s, {threads} threads",
+            "sample": f"oracle/avalanche_oracle.c (C restatement of vote.go/processor.go, the parity oracle; its "
+                      f"branch-free bit-plane round, vectorised by an AVX2 target clone — not the reference's Go "
+                      f"map path, which has no toolchain here), "
                       f"{ns} nodes x {m} targets, k={k}, rounds 0..{rounds - 1} ({applied} regsiterVote "
                       f"applications, {dt:.1f}s, OpenMP over nodes, {threads} threads on {cpu_model()})"}
 
@@ -294,12 +297,14 @@ class Runner:
         else:
             self.eng.run_rounds(rounds)
 
-    def steps(self, count, timed):
+    def steps(self, count, timed, entries=None):
         """Run `count` steps from the current position. timed: every segment
         inside one epoch is bracketed by barrier + synchronize and its wall
         time summed. Untimed steps run one round at a time with the log
         emptied after each (a conflicting workload emits ~1e8 StatusUpdates
-        per round). Returns (seconds, applied, emitted, segments)."""
+        per round); `entries` (a dict) collects each untimed round's log
+        entries per kind by round of the epoch. Returns (seconds, applied,
+        emitted, segments)."""
         eng = self.eng
         elapsed, applied, emitted, segs = 0.0, 0, 0, 0
         while count > 0:
@@ -322,6 +327,11 @@ class Runner:
                 eng.replay_rounds(seg)
             else:
                 eng.run_rounds(seg)
+                if timed:
+                    # the deferred state the segment's rounds leave behind (stale vote planes, pending
+                    # count steps: DESIGN.md §3) is written back inside the timed region, so every
+                    # timed round's records are paid for (vote.go:54-75 state observable afterwards)
+                    eng.materialize()
             if timed:
                 eng.synchronize()
                 torch.cuda.synchronize()
@@ -333,6 +343,8 @@ class Runner:
             if eng.log_overflowed():
                 raise BenchFailure(f"bench: StatusUpdate log overflowed in {self.wl} steps "
                                    f"{self.pos}..{self.pos + seg - 1}: updates were not stored; no number reported")
+            if entries is not None and not timed and seg == 1:
+                entries[self.pos % EPOCH] = eng.log_entries()
             if self.on_segment is not None:
                 self.on_segment(self, self.pos, seg)
             emitted += eng.updates_count()
@@ -346,6 +358,37 @@ class Runner:
         """Untimed: bring the engine to step `pos` of a fresh chain."""
         self.reset()
         self.steps(pos, timed=False)
+
+
+ENTRY_BYTES = (8, 32, 48)  # singles, slot records, dense records (k = 8; kernels.h)
+
+
+def window_segments(warmup, steps):
+    """The timed window's segments as lists of epoch rounds (steps W..W+K-1, split at epoch starts)."""
+    segs, cur = [], []
+    for pos in range(warmup, warmup + steps):
+        if pos % EPOCH == 0 and cur:
+            segs.append(cur)
+            cur = []
+        cur.append(pos % EPOCH)
+    if cur:
+        segs.append(cur)
+    return segs
+
+
+def size_log(eng, per_round, warmup, steps):
+    """Log entries per kind for the largest timed segment (the warm-up epoch's per-round counts
+    summed over the segment's rounds, 1.3x + 64 per shard of slack), in place of the worst case per
+    update: the device log holds what one timed segment emits. Returns the log's bytes."""
+    need = [0, 0, 0]
+    for seg in window_segments(warmup, steps):
+        tot = [sum(per_round.get(r, (0, 0, 0))[k] for r in seg) for k in range(3)]
+        need = [max(a, b) for a, b in zip(need, tot)]
+    ent = [int(1.3 * v) + 64 * 1024 for v in need]
+    eng.synchronize()
+    eng.discard_updates()
+    eng.resize_log(*ent)
+    return sum(e * b for e, b in zip(ent, ENTRY_BYTES))
 
 
 def log_capacity(n, m, world, rank, shard):
@@ -369,7 +412,9 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     `warmup` untimed steps, `steps` timed steps; then a second pass over the
     same steps with HIP events around every round kernel (roofline)."""
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
-    log_cap = log_capacity(n, m, world, rank, args.shard)
+    # replay (C2) keeps the per-update worst case; the sim workloads start small and are re-sized
+    # after the warm-up epoch (size_log)
+    log_cap = log_capacity(n, m, world, rank, args.shard) if replay else 1 << 20
     run = Runner(wl, args, world, rank, local_rank, log_cap)
     if run.fallback is not None:
         args.shard = "targets"
@@ -378,20 +423,25 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     eng = run.eng
     # ---- device warm-up (untimed): after process start the GPU runs these
     # kernels up to ~15 % slower for the first ~20-30 ms of sustained load
-    # (tools/gap_probe.py --events-first): one untimed epoch
-    run.steps(EPOCH, timed=False)
+    # (tools/gap_probe.py --events-first): one untimed epoch,
+    # one round at a time in a log of one entry per lane and kind (what one
+    # round can emit at most), counting each round's entries; then the log is
+    # sized for the largest timed segment
+    log_bytes = None
+    if not replay:
+        lanes = eng.layout_info()["lanes"]
+        eng.resize_log(lanes, lanes, lanes)
+        per_round = {}
+        run.steps(EPOCH, timed=False, entries=per_round)
+        log_bytes = size_log(eng, per_round, warmup, steps)
+    else:
+        run.steps(EPOCH, timed=False)
     # ---- warmup steps (untimed), then the timed steps
     run.goto(warmup)
     elapsed, applied, emitted, segs = run.steps(steps, timed=True)
-    # ---- the deferred state the timed rounds leave behind (pending count steps, stale vote
-    # planes) written back and timed on its own: outside the window, reported beside it
+    # (the timed segments end with the deferred state's write-back, av_materialize: inside the
+    # window; the roofline pass below times it on its own as writeback_ms)
     writeback_ms = None
-    if not replay:
-        eng.set_timing(True)
-        eng.materialize()
-        ms, nl = eng.kernel_stats()
-        eng.set_timing(False)
-        writeback_ms = ms if nl else 0.0
 
     # ---- roofline pass: the same steps again, every round's kernels bracketed
     # by HIP events on the engine's stream; sim rounds one step at a time so
@@ -407,8 +457,19 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         run.goto(warmup)
         eng.set_timing(True)
         left = steps
+        wb_ms = 0.0
+
+        def writeback():
+            # the write-back that ends a timed segment, timed alone (its own launches)
+            nonlocal wb_ms
+            if replay:
+                return
+            eng.materialize()
+            wb_ms += eng.kernel_stats()[0]  # (the loop read and reset the round events already)
         while left > 0:
             rnd = run.pos % EPOCH
+            if rnd == 0 and run.pos > 0 and left < steps:
+                writeback()  # the previous epoch's segment ended here
             seg = min(EPOCH - rnd, left) if replay else 1
             b0, r0 = eng.alg_bytes(), eng.alg_bytes_reread()
             _, a, em, _ = run.steps(seg, timed=False)
@@ -423,6 +484,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
             applied2 += a
             emitted2 += em
             left -= seg
+        writeback()  # the window's last segment
+        writeback_ms = None if replay else wb_ms
         eng.set_timing(False)
         if applied2 != applied:
             raise BenchFailure(f"bench: roofline pass applied {applied2} votes, the timed pass {applied}")
@@ -444,6 +507,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     if world > 1 and args.shard in ("peers", "nodes"):
         # every rank's replica of the published preferences must be the same:
         # hash a slice of every rank's node range as this rank sees it
+        if args.shard == "peers":
+            eng.peer_sync()  # need-masked pushes leave rows no local node reads behind (collective)
         hs = hashlib.sha256()
         for r in range(world):
             a = sharding.node_shard(n, world, r)[0]
@@ -454,16 +519,23 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     info = run.info
     run.close()
 
+    # the general step: the fresh and storm rounds of the window (bench round kinds
+    # 'fresh' / 'storm', every tile through the slot network), updates over their HIP-event kernel time
+    gen = [pr for pr in per_round if round_kind(pr["round"], replay) in ("fresh", "storm")]
+    gen_applied = float(sum(pr["applied"] for pr in gen))
+    gen_ms = float(sum(pr["kernel_ms"] for pr in gen))
     if world > 1:
-        st = torch.tensor([elapsed, float(applied), float(emitted)], dtype=torch.float64,
+        st = torch.tensor([elapsed, gen_ms, float(applied), float(emitted), gen_applied], dtype=torch.float64,
                           device="cpu" if args.rehearse_one_gpu else "cuda")
-        tmax = st[0:1].clone()
+        tmax = st[0:2].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tot = st[1:3].clone()
+        tot = st[2:5].clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        elapsed, applied_all, emitted_all = float(tmax), float(tot[0]), float(tot[1])
+        elapsed, gen_ms = float(tmax[0]), float(tmax[1])
+        applied_all, emitted_all, gen_applied = float(tot[0]), float(tot[1]), float(tot[2])
     else:
         applied_all, emitted_all = applied, emitted
+    value_general = gen_applied / (gen_ms * 1e-3) if gen and gen_ms > 0 else None
     kavg_ms = kern_ms / launches if launches else None
     gen2 = k <= 8 and args.kernel != 1
     if info["capped"] and replay and gen2:
@@ -490,6 +562,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         "rounds_per_launch": steps / launches if launches else None,
         "first_round": warmup % EPOCH,
         "writeback_ms": writeback_ms, "changed": changed,
+        "value_general": value_general, "general_rounds": sorted({pr["round"] for pr in gen}),
+        "log_bytes": log_bytes,
     }
 
 
@@ -716,7 +790,8 @@ def main(argv=None):
                     continue
                 sr = measure(wl, args, world, rank, local_rank, args.steps, args.warmup)
                 rf = roofline(sr, window, world)
-                secondary[wl] = {"value": sr["value"], "ms_per_step": sr["elapsed"] / args.steps * 1e3,
+                secondary[wl] = {"value": sr["value"], "value_general": sr["value_general"],
+                                 "ms_per_step": sr["elapsed"] / args.steps * 1e3,
                                  "frac": rf["frac"] if rf else None, "binding": rf.get("binding") if rf else None}
                 if sr["writeback_ms"] is not None:
                     secondary[wl]["writeback_ms"] = sr["writeback_ms"]
@@ -739,6 +814,10 @@ def main(argv=None):
         line = {
             "metric": "vote-record updates/sec (node·target·round) at 1/2/4/8 GPU; % HBM roofline",
             "value": r["value"],
+            # updates/s of the fresh and storm rounds alone (the general step: every tile through the
+            # slot network, no settled shortcut), HIP-event kernel time; `value` is the whole window
+            "value_general": r["value_general"],
+            "general_rounds": r["general_rounds"],
             "unit": "vote-record updates/s (1 update = 1 regsiterVote on a live record; k=8 per node·target·round)",
             "n_gpus": world,
             "steps": args.steps,
@@ -759,6 +838,8 @@ def main(argv=None):
             "updates_emitted": int(r["emitted"]),
             "roofline": compact_roofline(rf),
             "writeback_ms": r["writeback_ms"],
+            # device memory of the StatusUpdate log (sized for the largest timed segment, size_log)
+            "log_gb": r["log_bytes"] / 1e9 if r["log_bytes"] else None,
             "detail": os.path.relpath(args.detail, ROOT),
         }
         if r["replicas_identical"] is not None:

@@ -55,6 +55,15 @@ hipError_t dev_alloc(T** p, size_t n) {
 
 }  // namespace
 
+struct av_engine;
+// An in-process peer group (av_peer_group_serial): the ranks of a node-sharded network as engines of
+// one process on one device, sharing one stream; its order replaces the device barrier.
+struct PeerGroup {
+  std::vector<av_engine*> members;  // by rank; nullptr once destroyed
+  hipStream_t stream = nullptr;
+  int alive = 0;
+};
+
 struct av_engine {
   av_config cfg{};
   int64_t N = 0, M = 0, n0 = 0, n1 = 0, t0 = 0, t1 = 0;
@@ -117,6 +126,9 @@ struct av_engine {
   uint32_t* node_flags = nullptr;  // capped engines: nodes k_round_node leaves to the exact pass
   uint32_t log_cap = 0;
   uint32_t log_shards = 1;
+  // allocated entries of the three log kinds (all shards together); log_cap / mlog_cap / dlog_cap are
+  // these divided by log_shards, which follows the round kernels' wave count (set_log_layout)
+  size_t log_alloc = 0, mlog_alloc = 0, dlog_alloc = 0;
   unsigned long long* applied = nullptr;
   unsigned long long* bytes = nullptr;
   unsigned long long* finalized = nullptr;
@@ -205,6 +217,27 @@ struct av_engine {
   // round of an engine without a peer exchange — the exchange's fixed cost per round without the
   // pushes and without other ranks (tools/exchange_cost.py)
   bool solo_barrier = false;
+  // sticky: solo_barrier was enabled at some point (its arrival slots were allocated and its barrier
+  // sequence advanced outside an exchange): this engine can no longer join a peer exchange
+  bool solo_used = false;
+  // in-process peer group (av_peer_group_serial): e->stream is the group's stream, own_stream this
+  // engine's (destroyed with it)
+  PeerGroup* group = nullptr;
+  hipStream_t own_stream = nullptr;
+  // need-masked exchange (option "peer_mask", default on; kernels.h RoundParams::need / stale,
+  // DESIGN.md §5): a sweep round pushes a row segment only to the peers whose nodes draw that row in
+  // the next round, and remembers per segment, buffer and peer the changes it withheld
+  bool peer_mask = true;
+  bool masked = false;             // set up by the exchange's initialisation (mask_setup)
+  uint32_t segs = 1;               // 32-word segments per row
+  uint8_t* need_mine = nullptr;    // [kNeedWin][N]: rows this rank's nodes draw in a window's rounds
+  uint8_t* needmask = nullptr;     // [kNeedWin][NL]: peers (push order) that draw each local row
+  uint8_t* stale = nullptr;        // [3][NL * segs]: per snapshot buffer, peers whose copy may differ
+  uint32_t* needin = nullptr;      // [2][world][kNeedWin][ceil(NL/32)]: the peers' drawn-row bits (IPC:
+                                   // inside the exported arrival allocation, at kNeedinOff)
+  avk::PeerPtrs peer_needin{};     // every rank's needin
+  int64_t need_ready = -1;         // window whose needmask is combined
+  int64_t need_pushed = -1;        // window whose drawn rows were pushed to the peers
   // changed published words (kernels.h RoundParams::changed): counted in every peer-push round and,
   // with option "count_changed", in every sweep round
   unsigned long long* changed = nullptr;
@@ -353,7 +386,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
 // such a round calls this first.
 int materialize_votes_only(av_engine* e) {
   if (!e->v_stale) return AV_OK;
-  AV_HIP(avk::launch_vv_materialize(round_params(e, nullptr), e->stream));
+  AV_HIP(avk::launch_materialize(round_params(e, nullptr), true, false, e->stream));
   e->v_stale = false;
   return AV_OK;
 }
@@ -363,16 +396,18 @@ int materialize_votes_only(av_engine* e) {
 // first.
 int materialize_counts(av_engine* e) {
   if (!e->k_pend) return AV_OK;
-  AV_HIP(avk::launch_kl_materialize(round_params(e, nullptr), e->stream));
+  AV_HIP(avk::launch_materialize(round_params(e, nullptr), false, true, e->stream));
   e->k_pend = false;
   return AV_OK;
 }
 
-// Both deferred forms (vote planes, count planes) written back.
+// Both deferred forms (vote planes, count planes) written back, in one pass.
 int materialize_votes(av_engine* e) {
-  int rc = materialize_votes_only(e);
-  if (rc != AV_OK) return rc;
-  return materialize_counts(e);
+  if (!e->v_stale && !e->k_pend) return AV_OK;
+  AV_HIP(avk::launch_materialize(round_params(e, nullptr), e->v_stale, e->k_pend, e->stream));
+  e->v_stale = false;
+  e->k_pend = false;
+  return AV_OK;
 }
 
 // Peer-push exchange: copy this rank's rows of snapshot buffer `b` into every
@@ -389,9 +424,74 @@ int push_own_rows(av_engine* e, int b) {
 
 // Barrier across the peer ranks, on the engine stream (kernels.h).
 int peer_barrier(av_engine* e) {
+  if (e->group) return AV_OK;  // serial group: every rank's kernels run in one stream's order
   if (!e->barrier_ticks) AV_HIP(avk::peer_timeout_ticks(e->cfg.device, e->barrier_timeout_ms, &e->barrier_ticks));
   AV_HIP(avk::launch_peer_barrier(e->peer_arrive, (uint32_t)std::max(1, e->peer_world), (uint32_t)e->peer_rank,
                                   ++e->barrier_seq, e->barrier_err, e->barrier_ticks, e->stream));
+  return AV_OK;
+}
+
+// ---- need-masked exchange (kernels.h RoundParams::need / stale) ----
+constexpr size_t kNeedinOff = 4096;  // byte offset of needin in the exported arrival allocation
+
+size_t needin_words(const av_engine* e, int world) {
+  return (size_t)2 * (size_t)world * avk::kNeedWin * ((e->NL + 31) / 32);
+}
+
+// a row's 32-word segments never straddle a wave: BL a power of two <= 32 (a node's lanes inside one
+// tile) or a multiple of 32 (32-aligned segments inside 64-aligned tiles)
+bool mask_layout_ok(const av_engine* e) {
+  return (e->BL <= 32 && (e->BL & (e->BL - 1)) == 0) || e->BL % 32 == 0;
+}
+
+// After the exchange's pointers are set (own needin allocated, peer_needin filled): buffers of the
+// masked form, every replica identical (nothing withheld).
+int mask_setup(av_engine* e) {
+  e->masked = e->peer_mask && e->peer_world >= 2 && e->peer_world <= 9 && mask_layout_ok(e) && e->needin;
+  if (!e->masked) return AV_OK;
+  e->segs = (e->BL + 31) / 32;
+  AV_HIP(dev_alloc(&e->need_mine, (size_t)avk::kNeedWin * e->N));
+  AV_HIP(dev_alloc(&e->needmask, (size_t)avk::kNeedWin * e->NL));
+  AV_HIP(dev_alloc(&e->stale, (size_t)3 * e->NL * e->segs));
+  AV_HIP(hipMemsetAsync(e->stale, 0, (size_t)3 * e->NL * e->segs, e->stream));
+  e->need_ready = e->need_pushed = -1;
+  return AV_OK;
+}
+
+// Every replica of snapshot buffer b was just given this rank's rows whole: nothing withheld.
+int stale_clear(av_engine* e, int b) {
+  if (!e->masked) return AV_OK;
+  const size_t n = (size_t)e->NL * e->segs;
+  AV_HIP(hipMemsetAsync(e->stale + (size_t)b * n, 0, n, e->stream));
+  return AV_OK;
+}
+
+// Window w = push rounds [w W, w W + W): the rows this rank's nodes draw in rounds w W + 1 .. w W + W
+// (R1's sampling), pushed to their owners; enqueued before a barrier, combined after it.
+int need_gen(av_engine* e, int64_t w) {
+  if (!e->masked || e->need_pushed == w) return AV_OK;
+  const uint32_t W = avk::kNeedWin;
+  AV_HIP(hipMemsetAsync(e->need_mine, 0, (size_t)W * e->N, e->stream));
+  AV_HIP(avk::launch_need_draw(e->cfg.seed, (uint32_t)e->N, (uint32_t)e->n0, e->NL, (uint32_t)(w * W + 1), W, e->k,
+                               e->cfg.peer_mode, e->need_mine, e->stream));
+  AV_HIP(avk::launch_need_push(e->need_mine, (uint32_t)e->N, e->NL, W, (uint32_t)e->peer_world,
+                               (uint32_t)e->peer_rank, (uint32_t)(w & 1), e->peer_needin, e->stream));
+  e->need_pushed = w;
+  return AV_OK;
+}
+
+int ref_pick(av_engine* e);
+
+// After the barrier that ordered every rank's need_gen of window w: the per-row peer masks.
+int need_combine(av_engine* e, int64_t w) {
+  if (!e->masked || e->need_ready == w || e->need_pushed != w) return AV_OK;
+  int rc = ref_pick(e);  // the reference row (uniform rows) is read by every rank
+  if (rc != AV_OK) return rc;
+  const uint32_t ref_local =
+      e->ref_node >= e->n0 && e->ref_node < e->n1 ? (uint32_t)(e->ref_node - e->n0) : 0xFFFFFFFFu;
+  AV_HIP(avk::launch_need_combine(e->needin, (uint32_t)e->peer_world, (uint32_t)e->peer_rank, (uint32_t)(w & 1),
+                                  avk::kNeedWin, e->NL, ref_local, e->needmask, e->stream));
+  e->need_ready = w;
   return AV_OK;
 }
 
@@ -464,6 +564,16 @@ int ref_pick(av_engine* e) {
 int launch_one_round(av_engine* e, const uint32_t* replay) {
   AV_CHECK(e->round - e->log_base < 4096, AV_ERR_OVERFLOW,
            "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
+  if (e->group) {
+    // serial group: round r of rank i is enqueued after round r of every lower rank and before
+    // round r of every higher one (the stream order is the exchange's barrier)
+    for (const av_engine* m : e->group->members) AV_CHECK(m, AV_ERR_UNSUPPORTED, "peer group: a rank was destroyed");
+    for (const av_engine* m : e->group->members)
+      if (m != e)
+        AV_CHECK(m->round == e->round + (m->peer_rank < e->peer_rank ? 1 : 0), AV_ERR_UNSUPPORTED,
+                 "peer group: rank %d at round %lld, rank %d at round %lld: run one round of every rank in rank "
+                 "order", e->peer_rank, (long long)e->round, m->peer_rank, (long long)m->round);
+  }
   AV_CHECK(e->NL == (uint32_t)e->N || e->comm != nullptr || e->peer_world > 1 || e->N == e->n1 - e->n0 ||
                e->unsynced_shard,
            AV_ERR_UNSUPPORTED,
@@ -519,6 +629,14 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   if (peer && sweep && !replay) {
     p.push_n = (uint32_t)e->peer_world - 1u;
     p.push_dst = e->push_tbl + (size_t)nb * avk::kMaxPeers;
+    if (e->masked) {  // need-masked pushes: this round's row masks (window of push round e->round)
+      const int64_t w = e->round / avk::kNeedWin;  // combined below (need_combine) if not yet
+      const bool have = e->need_ready == w || e->need_pushed == w;
+      p.need = have ? e->needmask + (size_t)(e->round % avk::kNeedWin) * e->NL : nullptr;
+      p.stale = e->stale + (size_t)nb * e->NL * e->segs;
+      p.segs = e->segs;
+      p.peer_all = (1u << p.push_n) - 1u;
+    }
   }
   p.count_changed = (p.push_n || e->count_changed) && sweep && !replay ? 1u : 0u;
   p.changed = e->changed;
@@ -572,6 +690,10 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     AV_HIP(hipEventCreate(&ev1));
     AV_HIP(hipEventRecord(ev0, e->stream));
   }
+  if (p.push_n && e->masked) {  // (inside the round's timing: the exchange's own work)
+    int rc = need_combine(e, e->round / avk::kNeedWin);
+    if (rc != AV_OK) return rc;
+  }
   bool refw = false;  // the round wrote reference-row flags for the snapshot it published
   if (sweep)
     AV_HIP(avk::launch_round_sweep(p, e->k, replay != nullptr, e->sweep_blocks, e->stream, &refw));
@@ -595,6 +717,11 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     e->warm_all = false;
   else if (e->c_monotone && e->k >= 8 && !e->capped && all_valid)
     e->warm_all = true;  // every live record was polled and shifted in 8 considered votes
+  if (peer) {
+    // the next push round's window drawn and pushed before the barrier (combined after it)
+    int rc = need_gen(e, (e->round + 1) / avk::kNeedWin);
+    if (rc != AV_OK) return rc;
+  }
   if (e->timing) {
     AV_HIP(hipEventRecord(ev1, e->stream));
     e->events.emplace_back(ev0, ev1);
@@ -605,6 +732,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   if (peer) {
     if (!p.push_n) {
       int rc = push_own_rows(e, nb);
+      if (rc == AV_OK) rc = stale_clear(e, nb);
       if (rc != AV_OK) return rc;
     }
     int rc = peer_barrier(e);
@@ -705,16 +833,47 @@ uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
   return (uint32_t)std::max<uint64_t>(1, (waves + 3) / 4);
 }
 
+// Waves that write the StatusUpdate log in the fewest-wave round kernel the engine may launch: every
+// writer picks shard wave % log_shards, so with more shards than writers the rest would sit empty and
+// the usable capacity shrink by that factor. Capped engines: k_round_node (one wave per node per 64
+// blocks); uncapped: the sweep grid's waves that own a run of tiles (launch_sweep_k: runs of
+// ceil(tiles / waves) tiles), never more than the tiles (the first-generation kernels: one per tile).
+uint64_t log_writer_waves(const av_engine* e) {
+  if (e->capped) return (uint64_t)e->NL * ((e->BL + 63) / 64);
+  const uint64_t tiles = e->Lpad / 64;
+  if (!e->sweep_blocks) return tiles;
+  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(e->sweep_blocks, (tiles + 3) / 4));
+  const uint64_t run = (tiles + grid * 4 - 1) / (grid * 4);
+  return std::max<uint64_t>(1, (tiles + run - 1) / run);
+}
+
+// Shard count and per-shard capacities of the (empty) log from the allocation and the writers: a
+// power of two with >= 4 writers per shard in every kernel, so that the modulo's uneven wrap (W
+// writers over S shards: some get ceil(W / S)) loads no shard more than 1.25x the mean.
+void set_log_layout(av_engine* e) {
+  const uint64_t w = log_writer_waves(e);
+  uint64_t sh = 1;
+  while (sh * 2 <= avk::kLogShards && sh * 2 * 4 <= w) sh *= 2;
+  e->log_shards = (uint32_t)sh;
+  e->log_cap = (uint32_t)std::min<size_t>(e->log_alloc / e->log_shards, 0xFFFFFFFFu);
+  e->mlog_cap = (uint32_t)std::min<size_t>(e->mlog_alloc / e->log_shards, 0xFFFFFFFFu);
+  e->dlog_cap = (uint32_t)std::min<size_t>(e->dlog_alloc / e->log_shards, 0xFFFFFFFFu);
+}
+
 
 // The arrival slots of the peer barrier (one per rank, fine-grained when peers store into them over
 // xGMI) and the barrier's timeout flag in pinned host memory (the barrier kernel stores it with
 // system scope, so the host sees it without synchronizing the stream; av_run_rounds refuses to
 // enqueue once it is set). Zeroed before any peer can see them: the exchange of handles orders the two.
+// The same allocation carries, at kNeedinOff, the table the peers' need_push stores into (sized for
+// the world of equal node shards this engine's shard implies, N / NL).
 int alloc_arrival(av_engine* e) {
+  const int world = e->N % e->NL == 0 && e->N / e->NL <= avk::kMaxPeers + 1 ? (int)(e->N / e->NL) : 1;
+  const size_t bytes = (kNeedinOff + needin_words(e, world) * 4 + (2u << 20) - 1) / (2u << 20) * (2u << 20);
   if (e->peer_fine)
-    AV_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&e->arrive), (size_t)(2u << 20), hipDeviceMallocFinegrained));
+    AV_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&e->arrive), bytes, hipDeviceMallocFinegrained));
   else
-    AV_HIP(dev_alloc(&e->arrive, (size_t)(2u << 20) / 4));
+    AV_HIP(dev_alloc(&e->arrive, bytes / 4));
   void* hp = nullptr;
   AV_HIP(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
   e->barrier_err_host = static_cast<volatile uint32_t*>(hp);
@@ -782,10 +941,20 @@ int av_destroy(av_engine* e) {
   if (e->changed) (void)hipFree(e->changed);
   if (e->push_tbl) (void)hipFree(e->push_tbl);
   if (e->marker) (void)hipEventDestroy(e->marker);
+  if (e->group) {
+    PeerGroup* g = e->group;
+    g->members[(size_t)e->peer_rank] = nullptr;
+    e->stream = e->own_stream;  // destroyed below; the group's stream with its last member
+    if (--g->alive == 0) {
+      (void)hipStreamDestroy(g->stream);
+      delete g;
+    }
+  }
   void* bufs[] = {e->planes, e->pref[0], e->pref[1], e->pref[2], e->vstale, e->kpend, e->valid, e->byz, e->log, e->log_count, e->log_overflow, e->node_flags,
                   e->readd, e->died_out, e->nopoll,
                   e->dlog, e->upd_count, e->mlog,
-                  e->applied, e->bytes, e->finalized, e->scratch_count, e->replay};
+                  e->applied, e->bytes, e->finalized, e->scratch_count, e->replay,
+                  e->need_mine, e->needmask, e->stale, e->group ? e->needin : nullptr};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -891,6 +1060,9 @@ int av_create(const av_config* cfg, av_engine** out) {
   e->mlog_cap = e->k == 8 ? std::max<uint32_t>(e->log_cap / 2, 16) : 16u;
   if ((he = dev_alloc(&e->mlog, (size_t)e->mlog_cap * e->log_shards * avk::med_rec_words())) != hipSuccess)
     return hip_fail(he, "alloc log");
+  e->log_alloc = (size_t)e->log_cap * e->log_shards;
+  e->mlog_alloc = (size_t)e->mlog_cap * e->log_shards;
+  e->dlog_alloc = (size_t)e->dlog_cap * e->log_shards;
   (void)hipMemsetAsync(e->log_count, 0, (size_t)3 * avk::kLogShards * avk::kCtrStride * 4, e->stream);
   (void)hipMemsetAsync(e->upd_count, 0, avk::kLogShards * 4, e->stream);
   if ((he = dev_alloc(&e->log_overflow, 1)) != hipSuccess) return hip_fail(he, "alloc log");
@@ -906,8 +1078,8 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = dev_alloc(&e->finalized, avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
   (void)hipMemsetAsync(e->finalized, 0, avk::kLogShards * 8, e->stream);
   if ((he = dev_alloc(&e->scratch_count, 1)) != hipSuccess) return hip_fail(he, "alloc counters");
-  if ((he = dev_alloc(&e->changed, 2 * avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
-  (void)hipMemsetAsync(e->changed, 0, 2 * avk::kLogShards * 8, e->stream);
+  if ((he = dev_alloc(&e->changed, 3 * avk::kLogShards)) != hipSuccess) return hip_fail(he, "alloc counters");
+  (void)hipMemsetAsync(e->changed, 0, 3 * avk::kLogShards * 8, e->stream);
 
   (void)hipMemsetAsync(e->log_overflow, 0, 4, e->stream);
   (void)hipMemsetAsync(e->applied, 0, avk::kLogShards * 8, e->stream);
@@ -927,6 +1099,7 @@ int av_create(const av_config* cfg, av_engine** out) {
   if ((he = avk::launch_byz(e->byz, (uint32_t)e->N, c.seed, c.byz_threshold, e->stream)) != hipSuccess)
     return hip_fail(he, "byz kernel");
   e->sweep_blocks = default_sweep_blocks(e);
+  set_log_layout(e);  // shards = the sweep grid's writers (a wave takes a run of tiles), not the tiles
   *out = e;
   rc = av_init_records(e, AV_INIT_NONE, 0);
   if (rc != AV_OK) {
@@ -978,6 +1151,8 @@ int av_init_records(av_engine* e, int32_t init_mode, uint32_t init_param) {
     // no rank's next round may read them before all ranks have pushed (collective: every rank
     // re-initialises). The other two buffers are untouched, so their replicas stay identical.
     int rc = push_own_rows(e, e->cur);
+    if (rc == AV_OK) rc = stale_clear(e, e->cur);
+    if (rc == AV_OK) rc = need_gen(e, e->round / avk::kNeedWin);
     if (rc != AV_OK) return rc;
     rc = peer_barrier(e);
     if (rc != AV_OK) return rc;
@@ -1564,6 +1739,7 @@ int clear_log(av_engine* e) {
   AV_HIP(hipMemsetAsync(e->log_overflow, 0, 4, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
   e->log_base = e->round;
+  set_log_layout(e);  // empty now: the shards follow the current sweep grid
   return AV_OK;
 }
 
@@ -1625,6 +1801,16 @@ int read_log_counts(av_engine* e, LogCounts& c) {
     c.doff[i] = (uint64_t)c.n_records;
     c.n_records += std::min<uint32_t>(c.dense[i], e->dlog_cap);
   }
+  return AV_OK;
+}
+
+// A sweep-grid option changed the number of log writers: re-shard the log now if it is empty
+// (every enqueued round has finished: read_log_counts synchronizes), else at the next clear_log.
+int relayout_log_if_empty(av_engine* e) {
+  LogCounts c;
+  int rc = read_log_counts(e, c);
+  if (rc != AV_OK) return rc;
+  if (!c.ovf && c.total == 0 && c.n_singles == 0 && c.n_med == 0 && c.n_records == 0) set_log_layout(e);
   return AV_OK;
 }
 
@@ -1794,6 +1980,60 @@ int av_discard_updates(av_engine* e) {
   return clear_log(e);
 }
 
+int av_log_entries(av_engine* e, int64_t out[3]) {
+  AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  LogCounts c;
+  int rc = read_log_counts(e, c);
+  if (rc != AV_OK) return rc;
+  out[0] = c.n_singles;
+  out[1] = c.n_med;
+  out[2] = c.n_records;
+  return AV_OK;
+}
+
+int av_resize_log(av_engine* e, const int64_t entries[3]) {
+  AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
+  AV_CHECK(entries && entries[0] >= 0 && entries[1] >= 0 && entries[2] >= 0, AV_ERR_INVALID_ARG, "bad entries");
+  LogCounts c;
+  int rc = read_log_counts(e, c);
+  if (rc != AV_OK) return rc;
+  AV_CHECK(!c.ovf && c.total == 0 && c.n_singles == 0 && c.n_med == 0 && c.n_records == 0, AV_ERR_UNSUPPORTED,
+           "av_resize_log: the log holds updates (fetch or discard them first)");
+  // every shard gets the same share: the totals rounded up to whole shards, >= 16 entries per shard
+  const uint64_t sh = avk::kLogShards;
+  auto per = [&](int64_t n) { return std::max<uint64_t>(((uint64_t)n + sh - 1) / sh, 16); };
+  const uint64_t s1 = per(entries[0]) * sh, s2 = per(entries[1]) * sh, s3 = per(entries[2]) * sh;
+  AV_CHECK(s1 / sh < (1ull << 32) && s2 / sh < (1ull << 32) && s3 / sh < (1ull << 32), AV_ERR_INVALID_ARG,
+           "log too large");
+  AV_HIP(hipStreamSynchronize(e->stream));
+  AV_HIP(hipFree(e->log));
+  AV_HIP(hipFree(e->mlog));
+  AV_HIP(hipFree(e->dlog));
+  e->log = nullptr;
+  e->mlog = nullptr;
+  e->dlog = nullptr;
+  hipError_t he = dev_alloc(&e->log, s1);
+  if (he == hipSuccess) he = dev_alloc(&e->mlog, s2 * avk::med_rec_words());
+  if (he == hipSuccess) he = dev_alloc(&e->dlog, s3 * avk::dense_words((uint32_t)e->k));
+  if (he != hipSuccess) {  // leave a usable minimal log behind
+    (void)hipGetLastError();
+    if (!e->log) (void)dev_alloc(&e->log, sh * 16);
+    if (!e->mlog) (void)dev_alloc(&e->mlog, sh * 16 * avk::med_rec_words());
+    if (!e->dlog) (void)dev_alloc(&e->dlog, sh * 16 * avk::dense_words((uint32_t)e->k));
+    e->log_alloc = e->mlog_alloc = e->dlog_alloc = sh * 16;
+    set_log_layout(e);
+    return fail(he == hipErrorOutOfMemory ? AV_ERR_OOM : AV_ERR_HIP, "av_resize_log: %s", hipGetErrorString(he));
+  }
+  e->log_alloc = s1;
+  e->mlog_alloc = s2;
+  e->dlog_alloc = s3;
+  set_log_layout(e);
+  return AV_OK;
+}
+
 namespace {
 int sum_byte_counters(av_engine* e, size_t first, int64_t* out) {
   AV_ENTER(e);
@@ -1932,6 +2172,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
       e->sweep_blocks = (uint32_t)value;
       e->sweep_blocks_explicit = true;
     }
+    AV_ENTER(e);
+    int rc = relayout_log_if_empty(e);
+    if (rc != AV_OK) return rc;
   } else if (n == "settled_fast") {
     e->settled_fast = value != 0;
   } else if (n == "replay_fast") {
@@ -1947,6 +2190,7 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
       e->peer_arrive.p[0] = e->arrive;
     }
     e->solo_barrier = value != 0;
+    e->solo_used = e->solo_used || e->solo_barrier;
   } else if (n == "dropin_fast") {
     e->dropin_fast = value != 0;
   } else if (n == "settled_lean") {
@@ -1960,6 +2204,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->tiles_per_wave = (uint32_t)value;
     // the default grid depends on the run length; an explicit sweep_blocks stays as set
     if (!e->sweep_blocks_explicit) e->sweep_blocks = default_sweep_blocks(e);
+    AV_ENTER(e);
+    int rc = relayout_log_if_empty(e);
+    if (rc != AV_OK) return rc;
   } else if (n == "unsynced_shard") {
     e->unsynced_shard = value != 0;
   } else if (n == "round_marker") {
@@ -1997,6 +2244,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->dense_min = (uint32_t)value;
   } else if (n == "fresh") {  // 0: a round after init reads every plane (A/B only)
     if (!value) e->fresh = false;
+  } else if (n == "peer_mask") {  // before the exchange is set up: need-masked pushes (default 1)
+    AV_CHECK(e->peer_world == 0, AV_ERR_INVALID_ARG, "peer_mask must be set before the exchange is set up");
+    e->peer_mask = value != 0;
   } else if (n == "peer_fine") {  // before av_peer_handles: fine-grained snapshot buffers (default 1)
     AV_CHECK(!e->arrive, AV_ERR_INVALID_ARG, "peer_fine must be set before av_peer_handles");
     e->peer_fine = value != 0;
@@ -2083,7 +2333,8 @@ int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]) {
   AV_ENTER(e);
   AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
   static_assert(sizeof(hipIpcMemHandle_t) * 4 + 64 == AV_PEER_HANDLE_BYTES, "peer handle blob size");
-  AV_CHECK(!e->solo_barrier, AV_ERR_UNSUPPORTED, "diagnostics option solo_barrier is set");
+  AV_CHECK(!e->solo_used, AV_ERR_UNSUPPORTED,
+           "diagnostics option solo_barrier was used on this engine: it cannot join a peer exchange");
   if (!e->arrive) {  // zeroed before any peer can see it: the exchange of handles orders the two
     // Snapshot buffers that peers store into over xGMI are fine-grained: this
     // device's L2 keeps such lines only within a kernel (the system-scope
@@ -2128,6 +2379,8 @@ int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handl
            AV_ERR_UNSUPPORTED, "node shards must be equal, contiguous and rank-ordered (N %% world == 0)");
   AV_CHECK(e->t0 == 0 && e->t1 == e->M, AV_ERR_UNSUPPORTED, "node sharding needs the full target range");
   AV_CHECK(e->comm == nullptr && e->peer_world == 0, AV_ERR_UNSUPPORTED, "exchange already initialised");
+  AV_CHECK(!e->solo_used, AV_ERR_UNSUPPORTED,
+           "diagnostics option solo_barrier was used on this engine: it cannot join a peer exchange");
   AV_CHECK(e->arrive != nullptr, AV_ERR_INVALID_ARG, "call av_peer_handles before av_peer_init");
   for (int r = 0; r < world; ++r) {
     void* ptrs[4] = {e->pref[0], e->pref[1], e->pref[2], e->arrive};
@@ -2159,7 +2412,9 @@ int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handl
     }
     for (int b = 0; b < 3; ++b) e->peer_pref[b][r] = static_cast<uint32_t*>(ptrs[b]);
     e->peer_arrive.p[r] = static_cast<uint32_t*>(ptrs[3]);
+    e->peer_needin.p[r] = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(ptrs[3]) + kNeedinOff);
   }
+  e->needin = e->peer_needin.p[rank];
   {
     uint32_t* tbl[3][avk::kMaxPeers] = {};
     for (int b = 0; b < 3; ++b) {
@@ -2181,10 +2436,98 @@ int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handl
       int rc = push_own_rows(e, b);
       if (rc != AV_OK) return rc;
     }
-    int rc = peer_barrier(e);
+    int rc = mask_setup(e);
+    if (rc == AV_OK) rc = need_gen(e, e->round / avk::kNeedWin);
+    if (rc != AV_OK) return rc;
+    rc = peer_barrier(e);
     if (rc != AV_OK) return rc;
   }
   return av_synchronize(e);
+}
+
+int av_peer_group_serial(av_engine** engines, int32_t world) {
+  AV_CHECK(engines && world >= 2 && world <= avk::kMaxPeers + 1, AV_ERR_INVALID_ARG,
+           "bad engines/world (2..%d ranks)", avk::kMaxPeers + 1);
+  for (int r = 0; r < world; ++r) {
+    av_engine* e = engines[r];
+    AV_CHECK(e, AV_ERR_INVALID_ARG, "null engine");
+    AV_CHECK(e->cfg.device == engines[0]->cfg.device, AV_ERR_UNSUPPORTED, "peer group: one device");
+    AV_CHECK(e->N == engines[0]->N && e->M == engines[0]->M && e->k == engines[0]->k &&
+                 e->cfg.seed == engines[0]->cfg.seed && e->cfg.byz_threshold == engines[0]->cfg.byz_threshold &&
+                 e->cfg.peer_mode == engines[0]->cfg.peer_mode && e->round == engines[0]->round &&
+                 e->cur == engines[0]->cur,
+             AV_ERR_INVALID_ARG, "peer group: engines of one network at one round");
+    AV_CHECK(e->N % world == 0 && (int64_t)e->NL * world == e->N && e->n0 == (int64_t)r * e->NL, AV_ERR_UNSUPPORTED,
+             "node shards must be equal, contiguous and rank-ordered (N %% world == 0)");
+    AV_CHECK(e->t0 == 0 && e->t1 == e->M, AV_ERR_UNSUPPORTED, "node sharding needs the full target range");
+    AV_CHECK(e->comm == nullptr && e->peer_world == 0 && !e->arrive && !e->solo_used, AV_ERR_UNSUPPORTED,
+             "exchange already initialised");
+  }
+  AV_HIP(hipSetDevice(engines[0]->cfg.device));
+  for (int r = 0; r < world; ++r) AV_HIP(hipStreamSynchronize(engines[r]->stream));
+  auto* g = new PeerGroup();
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete g;
+    return fail(AV_ERR_HIP, "hipStreamCreate failed");
+  }
+  g->members.assign(engines, engines + world);
+  g->alive = world;
+  for (int r = 0; r < world; ++r) {
+    av_engine* e = engines[r];
+    ref_invalidate(e);
+    e->group = g;
+    e->own_stream = e->stream;
+    e->stream = g->stream;
+    for (int b = 0; b < 3; ++b)
+      for (int q = 0; q < world; ++q) e->peer_pref[b][q] = engines[q]->pref[b];
+    uint32_t* tbl[3][avk::kMaxPeers] = {};
+    for (int b = 0; b < 3; ++b) {
+      int n = 0;
+      for (int q = 0; q < world; ++q)
+        if (q != r) tbl[b][n++] = e->peer_pref[b][q];
+    }
+    AV_HIP(dev_alloc(&e->push_tbl, (size_t)3 * avk::kMaxPeers));
+    AV_HIP(hipMemcpy(e->push_tbl, tbl, sizeof(tbl), hipMemcpyHostToDevice));
+    e->peer_world = world;
+    e->peer_rank = r;
+    e->world = world;
+    e->rank = r;
+  }
+  for (int r = 0; r < world; ++r) {
+    AV_HIP(dev_alloc(&engines[r]->needin, needin_words(engines[r], world)));
+    for (int q = 0; q < world; ++q) engines[q]->peer_needin.p[r] = engines[r]->needin;
+  }
+  // every replica of every snapshot buffer identical from here on
+  for (int r = 0; r < world; ++r) {
+    for (int b = 0; b < 3; ++b) {
+      int rc = push_own_rows(engines[r], b);
+      if (rc != AV_OK) return rc;
+    }
+    int rc = mask_setup(engines[r]);
+    if (rc == AV_OK) rc = need_gen(engines[r], engines[r]->round / avk::kNeedWin);
+    if (rc != AV_OK) return rc;
+  }
+  AV_HIP(hipStreamSynchronize(g->stream));
+  return AV_OK;
+}
+
+int av_peer_sync(av_engine* e) {
+  AV_ENTER(e);
+  AV_PEER_CHECK(e);
+  if (e->peer_world <= 1) return AV_OK;
+  int rc = push_own_rows(e, e->cur);
+  if (rc == AV_OK) rc = stale_clear(e, e->cur);
+  if (rc == AV_OK) rc = peer_barrier(e);
+  if (rc != AV_OK) return rc;
+  AV_HIP(hipStreamSynchronize(e->stream));
+  return peer_failed(e);
+}
+
+int av_pushed_words(av_engine* e, int64_t* out) {
+  AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
+  AV_CHECK(out, AV_ERR_INVALID_ARG, "null argument");
+  return sum_counter(e, e->changed + 2 * avk::kLogShards, out);
 }
 
 }  // extern "C"

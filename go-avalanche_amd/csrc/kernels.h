@@ -155,7 +155,21 @@ struct RoundParams {
   // (and [kLogShards + shard]: the 16-lane groups of a wave holding a changed word = 64-B row segments
   // when a wave's lanes are contiguous row words, PS == BL a multiple of 16; per-wave 16-bit sums)
   uint32_t count_changed;
-  unsigned long long* changed;  // [2 kLogShards]
+  unsigned long long* changed;  // [3 kLogShards]: changed words, changed segments, words pushed (all peers)
+  // Need-masked exchange (engine option "peer_mask"): a peer replica's copy of a row is
+  // read only by the rounds that draw that row, so a rank pushes a row segment to peer i only if one of
+  // peer i's nodes draws the row in the next round (need[nl] bit i, peer i in push_dst order; nullptr:
+  // every peer), and keeps per (row, 32-word segment) and snapshot buffer the peers whose copy may
+  // differ from its own (stale[nl * segs + seg] bit i, for pref_out's buffer): such a segment is
+  // pushed whole the next time that peer needs it. Segments never straddle a wave (BL a power of two
+  // <= 32 or a multiple of 32), so a wave's ballot decides a segment's bits alone.
+  const uint8_t* need;
+  uint8_t* stale;       // nullptr: unmasked pushes (every changed word to every peer)
+  uint32_t segs;        // 32-word segments per row: ceil(BL / 32)
+  uint32_t peer_all;    // (1 << push_n) - 1
+  // the pushes queued in LDS and stored after a wave's last tile (round_sweep.hip flush_pushes): the
+  // sweep's waves each take at most kPushQ tiles and push_n <= 8 (a byte per lane and tile)
+  uint32_t push_q;
   // Deferred count planes (`kl`, k = 8, warm sim rounds in which no record can
   // finalize): a tile all of whose polled records agreed with
   // their accepted bit on all 8 votes gains exactly +8 on every polled count
@@ -311,6 +325,23 @@ hipError_t round_sweep_occupancy(int k, bool replay, int* blocks_per_cu, int* cu
 hipError_t launch_vv_materialize(const RoundParams& p, hipStream_t s);
 // Apply the pending +8 steps of deferred count planes (p.kpend) and clear them.
 hipError_t launch_kl_materialize(const RoundParams& p, hipStream_t s);
+// Both write-backs in one pass over runs of 16 tiles per wave (do_v: launch_vv_materialize's part,
+// do_k: launch_kl_materialize's); tiles with nothing deferred are skipped with no memory access.
+hipError_t launch_materialize(const RoundParams& p, bool do_v, bool do_k, hipStream_t s);
+
+// Need-masked exchange: the rows each rank's nodes draw in the rounds of one window.
+// need_draw: mine[w][N] = 1 for every row drawn by a local node in round round0 + w (w < W).
+// need_push: the bits of mine for peer d's rows into peer d's needin[par][rank][w][NLw] (words).
+// need_combine: needmask[w][nl] = the peers (push order) whose nodes draw local row nl in round
+// round0 + w (ref_local: the reference row, read by every rank, is needed by all).
+constexpr uint32_t kNeedWin = 16;  // rounds per need window
+constexpr uint32_t kPushQ = 16;    // tiles per wave whose pushes the sweep queues in LDS
+hipError_t launch_need_draw(uint64_t seed, uint32_t n_nodes, uint32_t n0, uint32_t NL, uint32_t round0, uint32_t W,
+                            int k, int mode, uint8_t* mine, hipStream_t s);
+hipError_t launch_need_push(const uint8_t* mine, uint32_t n_nodes, uint32_t NL, uint32_t W, uint32_t world,
+                            uint32_t rank, uint32_t par, PeerPtrs needin, hipStream_t s);
+hipError_t launch_need_combine(const uint32_t* needin, uint32_t world, uint32_t rank, uint32_t par, uint32_t W,
+                               uint32_t NL, uint32_t ref_local, uint8_t* needmask, hipStream_t s);
 
 // Peer-push exchange helpers (kernels.hip). push_rows: copy words [w0, w1) of
 // a local snapshot buffer into the same range of every peer replica.

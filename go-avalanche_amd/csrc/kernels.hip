@@ -901,6 +901,65 @@ __global__ __launch_bounds__(256) void k_push_rows(const uint32_t* src, PeerPtrs
   }
 }
 
+// Need-masked exchange, step 1: the rows this rank's nodes draw (R1's peer sampling, the same
+// sample_peers the oracle restates) in the W rounds of a window, as bytes mine[w][N] (plain stores of
+// the same value: concurrent writers of one byte agree; the caller clears mine first).
+template <int K>
+__global__ __launch_bounds__(256) void k_need_draw(uint64_t seed, uint32_t n_nodes, uint32_t n0, uint32_t NL,
+                                                   uint32_t round0, uint32_t W, int mode, uint8_t* mine) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)W * NL) return;
+  const uint32_t w = (uint32_t)(i / NL), nl = (uint32_t)(i - (uint64_t)w * NL);
+  uint32_t peers[K];
+  sample_peers<K>(seed, n0 + nl, round0 + w, n_nodes, mode, peers);
+  uint8_t* row = mine + (size_t)w * n_nodes;
+#pragma unroll
+  for (int j = 0; j < K; ++j) row[peers[j]] = 1u;
+}
+
+// Step 2: rank d's slice of mine, 32 rows per word, stored into d's needin[par][rank][w][NLw]
+// (system scope: over xGMI, ordered before d reads it by the round barrier).
+__global__ __launch_bounds__(256) void k_need_push(const uint8_t* mine, uint32_t n_nodes, uint32_t NL, uint32_t W,
+                                                   uint32_t world, uint32_t rank, uint32_t par, PeerPtrs needin) {
+  const uint32_t NLw = (NL + 31u) / 32u;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)world * W * NLw) return;
+  const uint32_t d = (uint32_t)(i / ((uint64_t)W * NLw));
+  const uint32_t rem = (uint32_t)(i - (uint64_t)d * W * NLw);
+  const uint32_t w = rem / NLw, q = rem - w * NLw;
+  if (d == rank) return;
+  const uint8_t* src = mine + (size_t)w * n_nodes + (size_t)d * NL + (size_t)q * 32u;
+  const uint32_t nb = min(32u, NL - q * 32u);
+  uint32_t bits = 0u;
+  for (uint32_t j = 0; j < nb; ++j) bits |= (uint32_t)(src[j] != 0u) << j;
+  uint32_t* dst = needin.p[0];  // rank d's table, selected with static indices (SGPRs)
+#pragma unroll
+  for (int r = 1; r <= kMaxPeers; ++r)
+    if ((uint32_t)r == d) dst = needin.p[r];
+  __hip_atomic_store(dst + (((size_t)par * world + rank) * W + w) * NLw + q, bits, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Step 3 (after the barrier): per local row and round of the window, the peers (push order: ranks
+// ascending, this rank skipped) whose nodes draw it.
+__global__ __launch_bounds__(256) void k_need_combine(const uint32_t* needin, uint32_t world, uint32_t rank,
+                                                      uint32_t par, uint32_t W, uint32_t NL, uint32_t ref_local,
+                                                      uint8_t* needmask) {
+  const uint32_t NLw = (NL + 31u) / 32u;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)W * NL) return;
+  const uint32_t w = (uint32_t)(i / NL), nl = (uint32_t)(i - (uint64_t)w * NL);
+  uint32_t m = 0u, pi = 0u;
+  for (uint32_t d = 0; d < world; ++d) {
+    if (d == rank) continue;
+    const uint32_t word = needin[(((size_t)par * world + d) * W + w) * NLw + (nl >> 5)];
+    m |= ((word >> (nl & 31u)) & 1u) << pi;
+    ++pi;
+  }
+  if (nl == ref_local) m = (1u << (world - 1u)) - 1u;  // every rank reads the reference row (uniform rows)
+  needmask[(size_t)w * NL + nl] = (uint8_t)m;
+}
+
 // One wave. Lane i (< world) stores seq into rank i's arrival slot `rank`
 // (release, system scope: this rank's earlier kernels and pushes are visible
 // first), then waits for its own slot i to reach seq (acquire, system scope).
@@ -982,6 +1041,43 @@ hipError_t launch_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, u
   if (w1 <= w0 || !n_dst) return hipSuccess;
   const uint64_t blocks = std::min<uint64_t>(4096u, (w1 - w0 + 255u) / 256u);
   hipLaunchKernelGGL(k_push_rows, dim3((uint32_t)blocks), dim3(256), 0, s, src, dst, n_dst, w0, w1);
+  return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_need_draw_k(uint64_t seed, uint32_t n_nodes, uint32_t n0, uint32_t NL, uint32_t round0, uint32_t W,
+                              int mode, uint8_t* mine, hipStream_t s) {
+  const uint64_t n = (uint64_t)W * NL;
+  hipLaunchKernelGGL(k_need_draw<K>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, seed, n_nodes, n0, NL,
+                     round0, W, mode, mine);
+  return hipGetLastError();
+}
+
+hipError_t launch_need_draw(uint64_t seed, uint32_t n_nodes, uint32_t n0, uint32_t NL, uint32_t round0, uint32_t W,
+                            int k, int mode, uint8_t* mine, hipStream_t s) {
+  if (!NL || !W) return hipSuccess;
+#define AVK_NEED(K) launch_need_draw_k<K>(seed, n_nodes, n0, NL, round0, W, mode, mine, s)
+  AVK_K_SWITCH(k, AVK_NEED)
+#undef AVK_NEED
+}
+
+hipError_t launch_need_push(const uint8_t* mine, uint32_t n_nodes, uint32_t NL, uint32_t W, uint32_t world,
+                            uint32_t rank, uint32_t par, PeerPtrs needin, hipStream_t s) {
+  if (world > (uint32_t)kMaxPeers + 1u || rank >= world) return hipErrorInvalidValue;
+  const uint64_t n = (uint64_t)world * W * ((NL + 31u) / 32u);
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_need_push, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, mine, n_nodes, NL, W, world,
+                     rank, par, needin);
+  return hipGetLastError();
+}
+
+hipError_t launch_need_combine(const uint32_t* needin, uint32_t world, uint32_t rank, uint32_t par, uint32_t W,
+                               uint32_t NL, uint32_t ref_local, uint8_t* needmask, hipStream_t s) {
+  if (world < 2 || world > 9u || rank >= world) return hipErrorInvalidValue;  // <= 8 peers: a byte mask
+  const uint64_t n = (uint64_t)W * NL;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_need_combine, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, needin, world, rank, par, W,
+                     NL, ref_local, needmask);
   return hipGetLastError();
 }
 

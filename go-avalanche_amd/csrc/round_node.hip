@@ -429,6 +429,9 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
 // the next round's replayed votes are loaded while this round is computed.
 // Same round loop, hand-off to the exact pass (count >= 120), StatusUpdates,
 // published words and counters as k_replay_node.
+#ifndef AVK_REPLAY_LATE_REFILL
+#define AVK_REPLAY_LATE_REFILL 0
+#endif
 template <int K, bool NT>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_replay_fast(const RoundParams p) {
   __shared__ uint32_t wmax[2];
@@ -555,9 +558,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
     // reload round R - 1's, unused — so that the loaded registers need no merge copy, which would wait)
     // (no instruction crosses this point: the loads below are not hoisted above the buffer's last
     // reads, so the buffer and the loads' destinations can be the same registers across the loop)
-    __builtin_amdgcn_sched_barrier(0);
+    auto refill = [&]() {
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < RQ; ++i) wb[i] = pld4<true>(rq + (size_t)min(r + 2u, R - 1u) * rstride + i * 64);
+      for (int i = 0; i < RQ; ++i) wb[i] = pld4<true>(rq + (size_t)min(r + 2u, R - 1u) * rstride + i * 64);
+    };
+    if (!(K == 8 && AVK_REPLAY_LATE_REFILL)) refill();
     // the round's update masks go straight into this round's pending set (no copy)
     uint32_t alive = ~0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u, ap = 0u;
     const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
@@ -578,6 +584,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
     if constexpr (K == 8) {
       pc = emit_reserve_med<K>(p, shard, lane, Ec, 0u, upd);
+      // AVK_REPLAY_LATE_REFILL: the refill issued after this round's reserving atomic, so that the
+      // store of round r - 1's entries below (which waits for round r - 1's atomic: vmcnt counts in
+      // issue order) does not also wait for the votes of round r + 1, loaded after that atomic
+      if (AVK_REPLAY_LATE_REFILL) refill();
       if (r > 0u)
         emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Ep, Ap, 0u, pp, p.round_rel + r - 1u);
       Ac = A;

@@ -64,9 +64,15 @@ struct SweepAcc {
   uint32_t reread = 0;  // per lane: gathered preference bytes beyond the one compulsory read of each word
   uint32_t emitted_bytes = 0, updates = 0;  // wave-uniform: StatusUpdate log bytes written, updates emitted
   uint32_t umis = 0;  // per lane: some published word differed from ref_node's word of pref_in (p.uni_out)
-  // wave-uniform (p.count_changed): published words that differ from the word they overwrite (bits 0-15)
-  // and the 16-lane groups holding one (bits 16-31: 64-B row segments when PS == BL, a multiple of 16)
-  uint32_t changed = 0;
+  // wave-uniform (p.count_changed): published words that differ from the word they overwrite, and the
+  // 16-lane groups holding one (64-B row segments when PS == BL, a multiple of 16); two scalars, so
+  // that a wave walking many tiles (a small grid) cannot carry one count into the other
+  uint32_t changed = 0, changed_segs = 0;
+  uint32_t pushed = 0;  // wave-uniform: words stored into peer replicas (all peers)
+  // deferred pushes (p.push_q): the wave's queue in LDS, slot = the tile's place in the wave's tiles
+  uint32_t* qpub = nullptr;
+  uint8_t* qpm = nullptr;
+  uint32_t qslot = 0;
   uint32_t shard = 0;  // wave-uniform: this wave's log / counter shard (wave index % log_shards)
 };
 
@@ -90,22 +96,80 @@ __device__ __forceinline__ uint32_t* peer_ptr(uint32_t* const* tbl, uint32_t r) 
 // accepted plane through them, so an honest row it publishes unchanged this round equals the
 // snapshot being overwritten (written three rounds ago): no load, no push; a Byzantine row's word
 // there is the pattern of that snapshot.
+// Need-masked exchange (p.stale, kernels.h): peer i gets this lane's word if one of its nodes draws
+// the row next round (need bit i) and either the word changed or peer i's copy of the segment may
+// differ (stale bit i: a change it did not need was withheld earlier); a withheld change marks the
+// segment stale for that peer, a push to it clears the mark. The segment's bits are decided per wave
+// (any changed word of the wave: a superset, so a mark is never lost; a segment never straddles a
+// wave), so every lane of a segment stores the same byte.
+// Deferred pushes (p.push_q): the peers a lane's word goes to (bit i: peer i) and the word are queued
+// in LDS and stored after the wave's last tile (flush_pushes), so that no load of a later tile waits
+// for them (vmcnt counts loads and stores in issue order, and a system-scope store to a peer completes
+// only at the peer: pushed from inside the tile loop, every tile waited for the last one's pushes).
 template <int POL, bool CC>
 __device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uint32_t pub, uint32_t old,
-                                        uint32_t& changed, bool known = false) {
+                                        SweepAcc& acc, bool known, uint32_t nl, uint32_t slot) {
   if (CC && p.count_changed) {
     if (!known && !AVK_CC_PREFETCH) old = p.pref_out[prow];
+    uint32_t nm = 0u, st = 0u, si = 0u;
+    if (p.stale) {
+      si = nl * p.segs + ((prow - (p.n0 + nl) * p.PS) >> 5);
+      nm = p.need ? (uint32_t)p.need[nl] : p.peer_all;
+      st = p.stale[si];
+    }
     const unsigned long long m = __ballot(pub != old);
     const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
     const uint32_t groups = ((lo & 0xFFFFu) ? 1u : 0u) + ((lo >> 16) ? 1u : 0u) + ((hi & 0xFFFFu) ? 1u : 0u) + ((hi >> 16) ? 1u : 0u);
-    changed += (uint32_t)__popcll(m) + (groups << 16);
-    if (pub != old) {
-      for (uint32_t r = 0; r < p.push_n; ++r)
-        __hip_atomic_store(peer_ptr(p.push_dst, r) + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    acc.changed += (uint32_t)__popcll(m);
+    acc.changed_segs += groups;
+    if (p.push_q) {
+      const uint32_t push = p.stale ? nm & (pub != old ? p.peer_all : st) : (pub != old ? p.peer_all : 0u);
+      const uint32_t lane = __lane_id();
+      acc.qpm[slot * 64u + lane] = (uint8_t)push;
+      acc.qpub[slot * 64u + lane] = pub;
+      for (uint32_t r = 0; r < p.push_n; ++r) acc.pushed += (uint32_t)__popcll(__ballot((push >> r) & 1u));
+      if (p.stale) {
+        const uint32_t nst = (st | (m ? p.peer_all : 0u)) & ~nm;
+        if (nst != st) p.stale[si] = (uint8_t)nst;
+      }
+    } else if (p.stale) {
+      const uint32_t push = nm & (pub != old ? p.peer_all : st);
+      for (uint32_t r = 0; r < p.push_n; ++r) {
+        const bool go = (push >> r) & 1u;
+        if (go) __hip_atomic_store(peer_ptr(p.push_dst, r) + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        acc.pushed += (uint32_t)__popcll(__ballot(go));
+      }
+      const uint32_t nst = (st | (m ? p.peer_all : 0u)) & ~nm;
+      if (nst != st) p.stale[si] = (uint8_t)nst;
+    } else {
+      if (pub != old)
+        for (uint32_t r = 0; r < p.push_n; ++r)
+          __hip_atomic_store(peer_ptr(p.push_dst, r) + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      acc.pushed += (uint32_t)__popcll(m) * p.push_n;
     }
   }
   const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc(p.pref_out, 0, (int)0xFFFFFFFFu, kRsrcWord3);
   st1<POL>(pr, p.pref_out + prow, prow * 4u, pub);
+}
+
+// The queued pushes of a wave's tiles (p.push_q): tile first + s * step for queue slot s < n. The peer
+// pointers are read once; the stores are the wave's last memory instructions, back to back.
+__device__ __forceinline__ void flush_pushes(const RoundParams& p, uint32_t lane, uint32_t first, uint32_t step,
+                                             uint32_t n, const uint32_t* qpub, const uint8_t* qpm) {
+  uint32_t* dst[8];
+#pragma unroll
+  for (uint32_t r = 0; r < 8u; ++r) dst[r] = r < p.push_n ? peer_ptr(p.push_dst, r) : nullptr;
+  for (uint32_t s = 0; s < n; ++s) {
+    const uint32_t g = (first + s * step) * 64u + lane;
+    const uint32_t pm = g < p.L ? (uint32_t)qpm[s * 64u + lane] : 0u;
+    if (pm == 0u) continue;
+    const uint32_t pub = qpub[s * 64u + lane];
+    const uint32_t nl = div_bl(p, g);
+    const uint32_t prow = (p.n0 + nl) * p.PS + (g - nl * p.BL);
+#pragma unroll
+    for (uint32_t r = 0; r < 8u; ++r)
+      if ((pm >> r) & 1u) __hip_atomic_store(dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3, kModeWarmPipe = 4, kModeFresh = 5 };
@@ -548,8 +612,8 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     const uint32_t pub = nbyz ? byz_pattern(p.round + 1u) : A;
     if (p.uni_out) acc.umis |= pub != in.uref ? 1u : 0u;  // uniform rows (kernels.h)
     const bool known = AVK_CC_PREFETCH || (kdefer && pend >= 2u);  // (publish)
-    publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? in.old : (nbyz ? byz_pattern(p.round - 2u) : pub), acc.changed,
-                     known);
+    publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? in.old : (nbyz ? byz_pattern(p.round - 2u) : pub), acc,
+                     known, node - p.n0, acc.qslot);
     // a record deleted this round keeps the vote/consider planes stored
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them
@@ -679,7 +743,7 @@ __device__ __forceinline__ bool settled_tile(const RoundParams& p, uint32_t tile
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
     const bool known = AVK_CC_PREFETCH || (kw & 0xFFu) >= 2u;  // (publish)
     publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? old : (is_byz(p.byz, node) ? byz_pattern(p.round - 2u) : pub),
-                     acc.changed, known);
+                     acc, known, nl, acc.qslot);
   }
   if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, p.pref_in[p.ref_node * p.PS + (active ? b : 0u)]);
   if (lane == 0) p.kpend[tile] = ((kw & 0xFFu) + 1u) | kPendAllLive | (kw & kHiVirt);
@@ -784,7 +848,7 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
       const bool known = AVK_CC_PREFETCH || (m & 0xFFu) >= 2u;  // (publish)
       publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? old : (((byzm >> rel) & 1ull) ? byz_pattern(p.round - 2u) : pub),
-                       acc.changed, known);
+                       acc, known, nl, i);
     }
     if (REF && p.rflag_out) ref_flag_store(p, lane, active, b, node, pub, rin);
     done |= 1u << i;
@@ -920,7 +984,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
       const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, (int)i);
       const bool known = AVK_CC_PREFETCH || (m & 0xFFu) >= 2u;
       const uint32_t old = AVK_CC_PREFETCH ? Ov[i] : (((byzm >> (nl - nlA)) & 1ull) ? byz_pattern(p.round - 2u) : pub);
-      publish<POL, CC>(p, prow, pub, old, acc.changed, known);
+      publish<POL, CC>(p, prow, pub, old, acc, known, nl, i);
     }
     done |= 1u << i;
     applied += 8u * (uint32_t)__popc(P0);
@@ -963,6 +1027,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   const uint32_t tiles = p.Lpad >> 6;
   SweepAcc acc;
   acc.shard = wave0 % p.log_shards;  // once per wave (a runtime modulo is a ~20-instruction sequence)
+  if constexpr (CC) {  // deferred pushes: the wave's queue (dynamic LDS, launched only with p.push_q)
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
+    const uint32_t w = threadIdx.x >> 6;
+    acc.qpub = reinterpret_cast<uint32_t*>(s_dyn) + w * (kPushQ * 64u);
+    acc.qpm = s_dyn + 4u * 4u * kPushQ * 64u + w * (kPushQ * 64u);
+  }
   // uniform rows (kernels.h): no rank's slot of pref_in carries this round's tag
   bool uniform = p.uni_in != nullptr;
   if (uniform)
@@ -1077,8 +1147,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         lean_ran = true;
       }
     }
+    const uint32_t qfirst = tile, qstep = stride;  // deferred pushes: slot s = tile qfirst + s * qstep
+    uint32_t qn = 0;
     for (; tile < tile_end; tile += stride) {
       constexpr bool AB = MODE == kModeAblate;
+      if constexpr (CC) acc.qslot = qn++;
       if constexpr (MODE == kModeWarm) {
         if constexpr (K == 8) {
           if (lean_done && ((lean_done >> (tile - wd.t0)) & 1u)) continue;
@@ -1119,6 +1192,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         }
       }
     }
+    if constexpr (CC) {
+      if (p.push_q && qn) flush_pushes(p, lane, qfirst, qstep, qn, acc.qpub, acc.qpm);
+    }
   }
   // one flush per wave (shard = wave index); 32-bit sums: a wave's lanes
   // accumulate < 2^32 over the tiles a grid gives it (the engine's grids
@@ -1136,9 +1212,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     if (acc.updates) atomicAdd(&p.upd_count[shard], acc.updates);
   }
   if (p.count_changed && lane == 0 && acc.changed) {
-    atomicAdd(&p.changed[acc.shard], (unsigned long long)(acc.changed & 0xFFFFu));
-    atomicAdd(&p.changed[kLogShards + acc.shard], (unsigned long long)(acc.changed >> 16));
+    atomicAdd(&p.changed[acc.shard], (unsigned long long)acc.changed);
+    atomicAdd(&p.changed[kLogShards + acc.shard], (unsigned long long)acc.changed_segs);
   }
+  if (p.count_changed && lane == 0 && acc.pushed) atomicAdd(&p.changed[2 * kLogShards + acc.shard], (unsigned long long)acc.pushed);
   if (p.uni_out && __ballot(acc.umis != 0u) != 0ull && lane == 0) {
     // some word this wave published differs from the reference row: tag the output snapshot's slot
     // of this rank in every replica (read by the next round, after the barrier in a peer exchange)
@@ -1149,29 +1226,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   }
 }
 
+// dynamic LDS of a sweep launch: the deferred-push queue of its 4 waves (p.push_q)
+constexpr uint32_t kPushQBytes = 4u * kPushQ * 64u * 5u;
+
 template <int K, int MODE, bool CC>
 hipError_t launch_mode_cc(const RoundParams& p, uint32_t grid, hipStream_t s) {
+  const uint32_t shm = CC && p.push_q ? kPushQBytes : 0u;
   // write-through store policies are built for k = 8 only (the measured workloads)
   const uint32_t pol = (K == 8 && p.store_policy >= 2) ? p.store_policy : (p.plane_nt ? 1u : 0u);
   if constexpr (K == 8 && MODE == kModeWarm) {
     // reference rows (kernels.h): the walking warm mode writes the flags and settled tiles read them
     if (p.rflag_out) {
       if (pol == 1)
-        hipLaunchKernelGGL((k_round_sweep<K, MODE, 1, true, CC>), dim3(grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((k_round_sweep<K, MODE, 1, true, CC>), dim3(grid), dim3(256), shm, s, p);
       else
-        hipLaunchKernelGGL((k_round_sweep<K, MODE, 0, true, CC>), dim3(grid), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((k_round_sweep<K, MODE, 0, true, CC>), dim3(grid), dim3(256), shm, s, p);
       return hipGetLastError();
     }
   }
   switch (pol) {
-    case 0: hipLaunchKernelGGL((k_round_sweep<K, MODE, 0, false, CC>), dim3(grid), dim3(256), 0, s, p); break;
-    case 1: hipLaunchKernelGGL((k_round_sweep<K, MODE, 1, false, CC>), dim3(grid), dim3(256), 0, s, p); break;
+    case 0: hipLaunchKernelGGL((k_round_sweep<K, MODE, 0, false, CC>), dim3(grid), dim3(256), shm, s, p); break;
+    case 1: hipLaunchKernelGGL((k_round_sweep<K, MODE, 1, false, CC>), dim3(grid), dim3(256), shm, s, p); break;
     default:
       if constexpr (K == 8) {
         if (pol == 2)
-          hipLaunchKernelGGL((k_round_sweep<K, MODE, 2, false, CC>), dim3(grid), dim3(256), 0, s, p);
+          hipLaunchKernelGGL((k_round_sweep<K, MODE, 2, false, CC>), dim3(grid), dim3(256), shm, s, p);
         else
-          hipLaunchKernelGGL((k_round_sweep<K, MODE, 3, false, CC>), dim3(grid), dim3(256), 0, s, p);
+          hipLaunchKernelGGL((k_round_sweep<K, MODE, 3, false, CC>), dim3(grid), dim3(256), shm, s, p);
       }
   }
   return hipGetLastError();
@@ -1195,6 +1276,13 @@ hipError_t launch_sweep_k(const RoundParams& p_in, bool replay, uint32_t blocks,
   const uint32_t grid = std::max(1u, blocks ? std::min(blocks, need) : need);
   RoundParams p = p_in;
   p.tpw = 0u;
+  // deferred pushes: every wave of the grid takes at most kPushQ tiles (a run, or a grid stride over
+  // <= kPushQ tiles) and at most 8 peers (the queue's byte per lane); the resident pipelined grid and
+  // larger worlds push from the tile loop
+  {
+    const uint32_t waves = grid * 4u, tiles = p.Lpad / 64u;
+    p.push_q = p.push_n && p.push_n <= 8u && (tiles + waves - 1u) / waves <= kPushQ ? 1u : 0u;
+  }
   if (p_in.tpw && K == 8 && !replay && !p.ablate_gather && !p.fresh && p.warm_skip && p.warm_all) {
     // p_in.tpw = enabled: each wave takes a run of consecutive tiles
     const uint32_t tiles = p.Lpad / 64u, waves = grid * 4u;
@@ -1210,9 +1298,13 @@ hipError_t launch_sweep_k(const RoundParams& p_in, bool replay, uint32_t blocks,
   if (replay) return launch_mode<K, kModeReplay>(p, grid, s);
   if (p.ablate_gather) return launch_mode<K, kModeAblate>(p, grid, s);
   if (p.fresh) return launch_mode<K, kModeFresh>(p, grid, s);
-  if (p.warm_skip && p.warm_all)  // a resident grid walks several tiles per wave: pipeline them
-    return blocks && grid < need && !p.nopipe ? launch_mode<K, kModeWarmPipe>(p, grid, s)
-                                              : launch_mode<K, kModeWarm>(p, grid, s);
+  if (p.warm_skip && p.warm_all) {  // a resident grid walks several tiles per wave: pipeline them
+    if (blocks && grid < need && !p.nopipe) {
+      p.push_q = 0u;
+      return launch_mode<K, kModeWarmPipe>(p, grid, s);
+    }
+    return launch_mode<K, kModeWarm>(p, grid, s);
+  }
   return launch_mode<K, kModeCheck>(p, grid, s);
 }
 
@@ -1301,6 +1393,93 @@ __global__ __launch_bounds__(256) void k_kl_materialize(const RoundParams p) {
   if (lane == 0) p.kpend[tile] = 0u;
 }
 
+// Both deferred forms written back in one pass (do_v: stale vote planes and unstored consider planes,
+// as k_vv_materialize; do_k: pending count steps and virtual K4..K7 groups, as k_kl_materialize), a
+// wave walking a run of `run` consecutive tiles: the run's tile words are loaded one lane per tile and
+// tested with v_readlane, so a wave pays its set-up once per run and a tile with nothing deferred costs
+// no memory access (one wave per tile left most waves with nothing to do but their launch).
+__global__ __launch_bounds__(256) void k_materialize(const RoundParams p, uint32_t run, uint32_t do_v, uint32_t do_k) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
+  const uint32_t tiles = p.Lpad >> 6;
+  const uint32_t t0 = wave * run;
+  if (t0 >= tiles) return;
+  const uint32_t n = min(run, tiles - t0);
+  const uint32_t ti = t0 + lane;
+  const uint32_t stw = do_v && lane < n ? p.vstale[ti] : 0u;
+  const uint32_t kww = do_k && lane < n ? p.kpend[ti] : 0u;
+  if (__ballot(stw != 0u || kww != 0u) == 0ull) return;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t raw = (uint32_t)__builtin_amdgcn_readlane((int)stw, (int)i);
+    const uint32_t kw = (uint32_t)__builtin_amdgcn_readlane((int)kww, (int)i);
+    if (raw == 0u && kw == 0u) continue;
+    const uint32_t tile = t0 + i;
+    const LaneIdx x = lane_idx(p, tile, lane);
+    uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
+    u32x4* const grp = reinterpret_cast<u32x4*>(tp) + lane;
+    if (raw) {
+      const uint32_t st = raw & kVMask;
+      if ((raw & kCAll) && x.active) {  // consider planes: all-ones
+#pragma unroll
+        for (int c = 0; c < 8; ++c) tp[1024u + (uint32_t)c * 64u + lane] = ~0u;
+      }
+      if (st) {
+        u32x4 o0, o1;
+        if (st == kVUniform) {  // V_i = A on every polled record
+          const uint32_t A = tp[1536u + lane];
+          o0 = o1 = u32x4{A, A, A, A};
+        } else {  // the last round's 8 gathered votes, V_i = slot 7 - i
+          const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
+          uint32_t pp[8];
+          draw_peers<8>(p, p.round - 1u, x.node, x.nl, nlA, nn, lane, pp);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            o0[c] = p.pref_prev[pp[7 - c] * p.PS + x.b];
+            o1[c] = p.pref_prev[pp[3 - c] * p.PS + x.b];
+          }
+        }
+        if (x.active) {
+          grp[0] = o0;
+          grp[64] = o1;
+        }
+      }
+    }
+    const uint32_t pend = kw & 0xFFu;
+    if ((pend || (kw & kHiVirt)) && x.active) {  // + 8 * pend on the polled records' counts
+      const u32x4 k0 = grp[128];
+      const u32x4 k1 = kw & kHiVirt ? u32x4{0u, 0u, 0u, ~real_mask(p.tn, x.b)} : grp[192];  // kernels.h kHiVirt
+      uint32_t Kp[8];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        Kp[c] = k0[c];
+        Kp[4 + c] = k1[c];
+      }
+      const uint32_t P0 = ~Kp[7] & p.valid[x.b];
+      uint32_t cy = 0u;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {  // + pend on count bits 3..6
+        const uint32_t bi = ((pend >> c) & 1u) ? P0 : 0u;
+        const uint32_t t = Kp[3 + c] ^ bi;
+        const uint32_t si = t ^ cy;
+        cy = (t & cy) | (Kp[3 + c] & bi);
+        Kp[3 + c] = si;
+      }
+      u32x4 o2, o3;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        o2[c] = Kp[c];
+        o3[c] = Kp[4 + c];
+      }
+      grp[128] = o2;
+      grp[192] = o3;
+    }
+  }
+  if (lane < n) {
+    if (stw) p.vstale[ti] = 0u;
+    if (kww) p.kpend[ti] = 0u;
+  }
+}
+
 template <int K>
 hipError_t occupancy_k(bool replay, int* bpc) {
   return replay ? hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, k_round_sweep<K, kModeReplay, 1>, 256, 0)
@@ -1333,6 +1512,16 @@ hipError_t launch_vv_materialize(const RoundParams& p, hipStream_t s) {
   if (!p.vstale || !p.pref_prev) return hipErrorInvalidValue;
   const uint32_t tiles = p.Lpad / 64u;
   hipLaunchKernelGGL(k_vv_materialize, dim3((tiles + 3u) / 4u), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_materialize(const RoundParams& p, bool do_v, bool do_k, hipStream_t s) {
+  if ((do_v && (!p.vstale || !p.pref_prev)) || (do_k && !p.kpend)) return hipErrorInvalidValue;
+  if (!do_v && !do_k) return hipSuccess;
+  constexpr uint32_t run = 16u;
+  const uint32_t tiles = p.Lpad / 64u;
+  const uint32_t waves = (tiles + run - 1u) / run;
+  hipLaunchKernelGGL(k_materialize, dim3((waves + 3u) / 4u), dim3(256), 0, s, p, run, do_v ? 1u : 0u, do_k ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -82,7 +82,8 @@ EXPORTED = [
     "av_set_option", "av_set_timing", "av_kernel_stats", "av_layout_info", "av_comm_unique_id", "av_comm_init",
     "av_peer_handles", "av_peer_init", "av_get_round", "av_set_round", "av_log_base_round", "av_updates_digest",
     "av_updates_digest_range", "av_read_pref_words", "av_set_polling",
-    "av_register_votes_batch", "av_changed_words", "av_materialize",
+    "av_register_votes_batch", "av_changed_words", "av_materialize", "av_peer_group_serial", "av_peer_sync",
+    "av_pushed_words", "av_log_entries", "av_resize_log",
 ]
 
 _lib = None
@@ -150,6 +151,11 @@ def lib():
         "av_read_pref_words": (i32, [_vp, i64, i64, _vp]),
         "av_set_polling": (i32, [_vp, i64, i32]),
         "av_register_votes_batch": (i32, [_vp, i64, _vp, _vp, _vp, _vp, _vp]),
+        "av_peer_group_serial": (i32, [_vp, i32]),
+        "av_peer_sync": (i32, [_vp]),
+        "av_pushed_words": (i32, [_vp, P(i64)]),
+        "av_log_entries": (i32, [_vp, _vp]),
+        "av_resize_log": (i32, [_vp, _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -192,6 +198,23 @@ def comm_unique_id() -> bytes:
     buf = (C.c_uint8 * 128)()
     _check(lib().av_comm_unique_id(C.cast(buf, _vp)))
     return bytes(buf)
+
+
+def peer_group_serial(engines):
+    """Make the node-shard engines of one network (rank order) one in-process
+    peer group on one device (av_peer_group_serial): every rank's round pushes
+    into the others' buffers; run round r of every rank in rank order."""
+    arr = (_vp * len(engines))(*[e._h for e in engines])
+    _check(lib().av_peer_group_serial(C.cast(arr, _vp), len(engines)))
+    for e in engines:
+        e._group = engines  # destroyed together (Engine.close closes the whole group)
+
+
+def run_group_rounds(engines, rounds=1):
+    """`rounds` synchronous rounds of a serial peer group: round r of rank 0, 1, .."""
+    for _ in range(rounds):
+        for e in engines:
+            e.run_rounds(1)
 
 
 class Engine:
@@ -423,6 +446,27 @@ class Engine:
         w, g = C.c_int64(0), C.c_int64(0)
         _check(lib().av_changed_words(self._h, C.byref(w), C.byref(g)))
         return w.value, g.value
+
+    def log_entries(self):
+        """Pending log entries per kind: (singles, slot records, dense records)."""
+        out = np.zeros(3, np.int64)
+        _check(lib().av_log_entries(self._h, _ptr(out)))
+        return tuple(int(v) for v in out)
+
+    def resize_log(self, singles, slots, dense):
+        """Re-allocate the empty device log for that many entries of each kind."""
+        v = np.array([singles, slots, dense], np.int64)
+        _check(lib().av_resize_log(self._h, _ptr(v)))
+
+    def pushed_words(self):
+        """Words stored into peer replicas by sweep rounds (all peers together)."""
+        out = C.c_int64(0)
+        _check(lib().av_pushed_words(self._h, C.byref(out)))
+        return out.value
+
+    def peer_sync(self):
+        """Collective: every rank's own rows pushed whole (replicas complete for reads)."""
+        _check(lib().av_peer_sync(self._h))
 
     def materialize(self):
         """Write back the deferred state (stale vote planes, pending count steps) now."""

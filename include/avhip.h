@@ -222,6 +222,15 @@ int av_finalized_count(av_engine* e, int64_t* out);
 int av_live_records(av_engine* e, int32_t honest_only, int64_t* out);
 /* Drop pending StatusUpdates without copying them (long convergence runs). */
 int av_discard_updates(av_engine* e);
+/* Log entries pending, per kind: out = {single updates, slot records (2-4
+ * slots of one 32-record lane), dense records (a lane's whole round)}; a
+ * lane's updates of one round are one entry. Sizing input for av_resize_log. */
+int av_log_entries(av_engine* e, int64_t out[3]);
+/* Re-allocate the (empty: AV_ERR_UNSUPPORTED otherwise) device log for
+ * entries[k] entries of each kind (8, 32 and 48 B each at k = 8), instead of
+ * av_config.update_log_capacity's worst case per update (36 B per update).
+ * One round never needs more than one entry per lane of each kind. */
+int av_resize_log(av_engine* e, const int64_t entries[3]);
 /* Algorithmic bytes moved by the round kernels since creation: state planes
  * read/written, gathered vote words, published words, 8 B per StatusUpdate
  * (DESIGN.md §3). */
@@ -323,6 +332,31 @@ int av_comm_init(av_engine* e, int32_t world, int32_t rank, const uint8_t id[128
 int av_peer_handles(av_engine* e, uint8_t out[AV_PEER_HANDLE_BYTES]);
 /* handles: world * AV_PEER_HANDLE_BYTES bytes, rank-ordered (this rank's own blob is ignored) */
 int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handles);
+/* One-device rehearsal and measurement harness of the peer-push exchange: the
+ * `world` node-shard engines of one network (engines[r] = rank r, created in
+ * this process on one device, same configuration, same round) become one peer
+ * group sharing one stream. Each rank's round kernel pushes into the others'
+ * buffers exactly as over IPC; the stream's order (round r of every rank in
+ * rank order, then round r + 1) replaces the device barrier, so per-rank
+ * kernel times are those of a rank alone on the device. A rank may run a round
+ * only when every lower rank has run it and no higher rank has
+ * (AV_ERR_UNSUPPORTED otherwise). Destroy the group's engines together. */
+int av_peer_group_serial(av_engine** engines, int32_t world);
+/* Need-masked exchange (option "peer_mask", default on for 2..9 ranks when a
+ * row's 32-word segments never straddle a wave: BL a power of two <= 32 or a
+ * multiple of 32): a round sends a changed row segment only to
+ * the ranks whose nodes draw that row in the next round (R1's sampling is a
+ * function of (seed, node, round), so every rank draws its own nodes' rows of
+ * a 16-round window ahead and tells their owners), and later sends whatever it
+ * withheld once that rank needs the row. Every result is the same as with full
+ * pushes; a rank's replica of another rank's rows can then hold rows no local
+ * node reads: av_read_pref / av_read_pref_words of another rank's rows are
+ * current only after av_peer_sync. Collective: every rank's own rows of the
+ * current snapshot pushed whole to every replica, then a barrier. */
+int av_peer_sync(av_engine* e);
+/* Words stored into peer replicas by sweep rounds since creation, summed over
+ * the peers (the exchange's volume; diagnostics, no reference counterpart). */
+int av_pushed_words(av_engine* e, int64_t* out);
 
 #ifdef __cplusplus
 }

@@ -150,3 +150,13 @@ def test_log_capacity_follows_the_shard():
     assert bench.log_capacity(1_000_000, 1000, 8, 3, "peers") == int(1.25 * 125_000 * 1000) + (1 << 20)
     # capped below 2^31 entries per engine
     assert bench.log_capacity(10_000_000, 256, 1, 0, "targets") == (1 << 31) - 1
+
+
+def test_window_segments_split_at_epochs():
+    """The timed window's segments (the log is sized for the largest): steps
+    W..W+K-1 are rounds p % 16 of fresh epochs, split where an epoch starts."""
+    import bench
+    assert bench.window_segments(5, 20) == [list(range(5, 16)), list(range(0, 9))]
+    assert bench.window_segments(0, 16) == [list(range(16))]
+    assert bench.window_segments(16, 3) == [[0, 1, 2]]
+    assert bench.window_segments(15, 2) == [[15], [0]]

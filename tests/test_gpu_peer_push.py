@@ -29,6 +29,9 @@ CASES = {
     "byz_pairs_reinit": (256, 200, 8, BYZ20, 4, 0, 20, {"_reinit": 7}),
     # uniform rows on / off across ranks (mismatch slots pushed to the replicas)
     "c4_shape_uniform_off": (512, 1000, 8, 0, 3, P80, 22, {"uniform_rows": 0}),
+    # the need-masked exchange (default on where the layout allows it: here BL 32 and 8) and off
+    "c4_shape_unmasked": (512, 1000, 8, 0, 3, P80, 22, {"peer_mask": 0}),
+    "pairs_bl8_masked": (512, 256, 8, BYZ20, 4, 0, 24, {}),
 }
 
 
@@ -77,6 +80,8 @@ def _rank_main(case, world, rank, d, q):
         e.synchronize()
         np.save(os.path.join(d, f"rec{rank}.npy"), e.read_records())
         np.save(os.path.join(d, f"upd{rank}.npy"), e.fetch_updates())
+        # need-masked pushes leave rows no local node reads behind: complete every replica first
+        e.peer_sync()
         np.save(os.path.join(d, f"pref{rank}.npy"), e.read_pref())
         e.close()
         q.put((rank, "ok"))

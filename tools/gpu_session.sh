@@ -30,6 +30,13 @@ for s in "$@"; do
     smoke) step smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step pytest_gpu 1080 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testsnew) step pytest_new 1200 python -u -m pytest tests/test_gpu_delivery.py tests/test_gpu_fullsize.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    testslog) step pytest_log 600 python -u -m pytest tests/test_gpu_log_layout.py tests/test_gpu_peer_group.py tests/test_gpu_bench_protocol.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    peers) step pytest_peers 900 python -u -m pytest tests/test_gpu_peer_group.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    gm_c4) step gm_c4 900 python tools/group_model.py --workload c4 --json $OUT/group_model_c4.json ;;
+    gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --json $OUT/group_model_c4p.json ;;
+    gm_c4pb) step gm_c4pb 900 python tools/group_model.py --workload c4pb --json $OUT/group_model_c4pb.json ;;
+    ab_c2late) step ab_c2late 600 bash -c 'for i in 1 2 3; do for v in default late; do echo "== $v"; if [ $v = default ]; then python tools/fuse_probe.py | head -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_late.so python tools/fuse_probe.py | head -1; fi; done; done' ;;
+    pmclist) step pmclist 120 rocprofv3 -L ;;
     testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py ;;
     rccl2) step rccl2 240 python tools/rccl_two_rank_probe.py ;;
