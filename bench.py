@@ -60,6 +60,8 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402  (device plumbing + torch.distributed only)
 import torch.distributed as dist  # noqa: E402
 
+import numpy as np  # noqa: E402
+
 import avhip  # noqa: E402
 from avhip import sharding  # noqa: E402
 
@@ -443,6 +445,38 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     # window; the roofline pass below times it on its own as writeback_ms)
     writeback_ms = None
 
+    # ---- delivery (one GPU, sim workloads; detail only): rounds 0-3 of a fresh epoch (the fresh and
+    # storm rounds, the most updates) one at a time, each followed by av_fetch_updates of its whole
+    # update stream into pageable host memory: the reference's *[]StatusUpdate out-parameter
+    # (processor.go:61,111) filled every round
+    delivery = None
+    if world == 1 and not replay and not args.no_roofline_pass:  # (before the roofline pass, which
+        # must stay the process's last round-kernel dispatches for tools/pmc_bench.py)
+        run.goto(0)
+        rows = []
+        buf = None
+        a0 = eng.applied_votes()
+        for _ in range(4):
+            rnd = run.pos % EPOCH
+            eng.synchronize()
+            t0 = time.perf_counter()
+            eng.run_rounds(1)
+            eng.synchronize()
+            t1 = time.perf_counter()
+            nu = eng.updates_count()
+            if buf is None or buf.size < nu:
+                buf = np.empty(max(nu, 1), np.uint64)
+            got = eng.fetch_into(buf)
+            t2 = time.perf_counter()
+            run.pos += 1
+            rows.append({"round": rnd, "updates": got, "round_ms": (t1 - t0) * 1e3, "fetch_ms": (t2 - t1) * 1e3})
+        upd = sum(r["updates"] for r in rows)
+        ms = sum(r["round_ms"] + r["fetch_ms"] for r in rows)
+        delivery = {"rounds": rows, "updates": upd, "ms": ms,
+                    "delivered_updates_per_s": (eng.applied_votes() - a0) / (ms * 1e-3),
+                    "status_updates_per_s": upd / (sum(r["fetch_ms"] for r in rows) * 1e-3),
+                    "note": "round + av_fetch_updates (device expansion, canonical radix sort, copy into pageable "
+                            "host memory through pinned staging) per round, wall clock"}
     # ---- roofline pass: the same steps again, every round's kernels bracketed
     # by HIP events on the engine's stream; sim rounds one step at a time so
     # that every round's kernel time, model bytes and re-read bytes are known
@@ -563,7 +597,7 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         "first_round": warmup % EPOCH,
         "writeback_ms": writeback_ms, "changed": changed,
         "value_general": value_general, "general_rounds": sorted({pr["round"] for pr in gen}),
-        "log_bytes": log_bytes,
+        "log_bytes": log_bytes, "delivery": delivery,
     }
 
 
@@ -797,7 +831,7 @@ def main(argv=None):
                     secondary[wl]["writeback_ms"] = sr["writeback_ms"]
                 if world > 1:
                     secondary[wl]["replicas_identical"] = sr["replicas_identical"]
-                detail["workloads"][wl] = {"workload": sr["desc"], "value": sr["value"],
+                detail["workloads"][wl] = {"workload": sr["desc"], "value": sr["value"], "delivery": sr["delivery"],
                                            "ms_per_step": sr["elapsed"] / args.steps * 1e3,
                                            "updates_emitted": int(sr["emitted"]), "roofline": rf,
                                            "per_round": sr["per_round"], "writeback_ms": sr["writeback_ms"],
@@ -848,7 +882,7 @@ def main(argv=None):
             line["config"]["shard_fallback"] = "peer exchange unavailable: " + args.shard_fallback
         if secondary:
             line["secondary"] = secondary
-        detail["workloads"][args.workload] = {"workload": r["desc"], "value": r["value"],
+        detail["workloads"][args.workload] = {"workload": r["desc"], "value": r["value"], "delivery": r["delivery"],
                                               "ms_per_step": r["elapsed"] / args.steps * 1e3,
                                               "updates_emitted": int(r["emitted"]), "roofline": rf,
                                               "per_round": r["per_round"], "writeback_ms": r["writeback_ms"],

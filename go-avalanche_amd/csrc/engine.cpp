@@ -228,6 +228,8 @@ struct av_engine {
   // DESIGN.md §5): a sweep round pushes a row segment only to the peers whose nodes draw that row in
   // the next round, and remembers per segment, buffer and peer the changes it withheld
   bool peer_mask = true;
+  bool push_defer = true;          // option "push_defer": sweep pushes queued per wave (RoundParams::push_q)
+  uint32_t push_store = 1;         // option "push_store" (RoundParams::push_store)
   bool masked = false;             // set up by the exchange's initialisation (mask_setup)
   uint32_t segs = 1;               // 32-word segments per row
   uint8_t* need_mine = nullptr;    // [kNeedWin][N]: rows this rank's nodes draw in a window's rounds
@@ -266,6 +268,9 @@ struct av_engine {
   // sort-grouped general path, A/B and tests)
   void* dropin_host = nullptr;
   size_t dropin_host_bytes = 0;
+  // StatusUpdate delivery into pageable caller memory: two pinned staging chunks (copy_out)
+  void* stage[2] = {nullptr, nullptr};
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
   bool dropin_fast = true;
 
   size_t round_replay_words() const { return avk::replay_words(Lpad, k); }
@@ -423,11 +428,25 @@ int push_own_rows(av_engine* e, int b) {
 }
 
 // Barrier across the peer ranks, on the engine stream (kernels.h).
-int peer_barrier(av_engine* e) {
-  if (e->group) return AV_OK;  // serial group: every rank's kernels run in one stream's order
+// slot_buf >= 0: the barrier kernel first copies this rank's uniform-rows mismatch slot of snapshot
+// buffer slot_buf into every peer's replica (the round kernel writes only its own copy, RoundParams::
+// uni_post). A serial group has no barrier: the copy alone runs.
+int peer_barrier(av_engine* e, int slot_buf = -1) {
+  const uint32_t* slot = nullptr;
+  avk::PeerPtrs sd{};
+  if (slot_buf >= 0 && e->peer_world > 1) {
+    slot = e->pref[slot_buf] + e->uni_off + e->peer_rank;
+    for (int r = 0; r < e->peer_world; ++r) sd.p[r] = e->peer_pref[slot_buf][r] + e->uni_off + e->peer_rank;
+  }
+  if (e->group) {  // serial group: every rank's kernels run in one stream's order
+    if (slot)
+      AV_HIP(avk::launch_peer_barrier(e->peer_arrive, (uint32_t)e->peer_world, (uint32_t)e->peer_rank, 0u, nullptr,
+                                      0u, e->stream, slot, sd, 0u));
+    return AV_OK;
+  }
   if (!e->barrier_ticks) AV_HIP(avk::peer_timeout_ticks(e->cfg.device, e->barrier_timeout_ms, &e->barrier_ticks));
   AV_HIP(avk::launch_peer_barrier(e->peer_arrive, (uint32_t)std::max(1, e->peer_world), (uint32_t)e->peer_rank,
-                                  ++e->barrier_seq, e->barrier_err, e->barrier_ticks, e->stream));
+                                  ++e->barrier_seq, e->barrier_err, e->barrier_ticks, e->stream, slot, sd, 1u));
   return AV_OK;
 }
 
@@ -635,8 +654,10 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
       p.need = have ? e->needmask + (size_t)(e->round % avk::kNeedWin) * e->NL : nullptr;
       p.stale = e->stale + (size_t)nb * e->NL * e->segs;
       p.segs = e->segs;
-      p.peer_all = (1u << p.push_n) - 1u;
     }
+    p.peer_all = (1u << std::min<uint32_t>(p.push_n, 31u)) - 1u;
+    p.push_defer = e->push_defer ? 1u : 0u;
+    p.push_store = e->push_store;
   }
   p.count_changed = (p.push_n || e->count_changed) && sweep && !replay ? 1u : 0u;
   p.changed = e->changed;
@@ -683,6 +704,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     p.uni_out = e->pref[nb] + e->uni_off;
     p.uni_in = e->uni_ok[e->cur] ? e->pref[e->cur] + e->uni_off : nullptr;
     p.uni_merge = e->uni_merge;
+    p.uni_post = peer && sweep && !replay ? 1u : 0u;  // the slot reaches the peers in the barrier kernel
   }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   if (e->timing) {
@@ -735,7 +757,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
       if (rc == AV_OK) rc = stale_clear(e, nb);
       if (rc != AV_OK) return rc;
     }
-    int rc = peer_barrier(e);
+    int rc = peer_barrier(e, p.uni_post ? nb : -1);
     if (rc != AV_OK) return rc;
   } else if (e->solo_barrier) {
     int rc = peer_barrier(e);
@@ -937,6 +959,10 @@ int av_destroy(av_engine* e) {
   if (e->barrier_err_host) (void)hipHostFree(const_cast<uint32_t*>(e->barrier_err_host));
   if (e->fetch_scratch) (void)hipFree(e->fetch_scratch);
   if (e->dropin_host) (void)hipHostFree(e->dropin_host);
+  for (int i = 0; i < 2; ++i) {
+    if (e->stage[i]) (void)hipHostFree(e->stage[i]);
+    if (e->stage_ev[i]) (void)hipEventDestroy(e->stage_ev[i]);
+  }
   if (e->digest) (void)hipFree(e->digest);
   if (e->changed) (void)hipFree(e->changed);
   if (e->push_tbl) (void)hipFree(e->push_tbl);
@@ -1814,6 +1840,51 @@ int relayout_log_if_empty(av_engine* e) {
   return AV_OK;
 }
 
+// n words from device memory into the caller's host buffer. Pinned caller memory: one DMA. Pageable
+// memory: chunks through two pinned staging buffers, the DMA of chunk i + 1 in flight while host
+// threads copy chunk i out (a hipMemcpy into pageable memory is staged by the runtime at ~14.5 GB/s,
+// DESIGN.md §4 delivery).
+int copy_out(av_engine* e, uint64_t* out, const uint64_t* dev, size_t n) {
+  if (!n) return AV_OK;
+  hipPointerAttribute_t at{};
+  bool pinned = false;
+  if (hipPointerGetAttributes(&at, out) == hipSuccess) pinned = at.type == hipMemoryTypeHost;
+  (void)hipGetLastError();
+  constexpr size_t kChunk = (size_t)8 << 20;  // words (64 MiB)
+  if (pinned || n <= (size_t)1 << 19) {
+    AV_HIP(hipMemcpyAsync(out, dev, n * 8, hipMemcpyDeviceToHost, e->stream));
+    AV_HIP(hipStreamSynchronize(e->stream));
+    return AV_OK;
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (!e->stage[i]) AV_HIP(hipHostMalloc(&e->stage[i], kChunk * 8, hipHostMallocDefault));
+    if (!e->stage_ev[i]) AV_HIP(hipEventCreateWithFlags(&e->stage_ev[i], hipEventDisableTiming));
+  }
+  const size_t chunks = (n + kChunk - 1) / kChunk;
+  auto dma = [&](size_t c) -> int {
+    const size_t w = std::min(kChunk, n - c * kChunk);
+    AV_HIP(hipMemcpyAsync(e->stage[c & 1], dev + c * kChunk, w * 8, hipMemcpyDeviceToHost, e->stream));
+    AV_HIP(hipEventRecord(e->stage_ev[c & 1], e->stream));
+    return AV_OK;
+  };
+  int rc = dma(0);
+  if (rc != AV_OK) return rc;
+  for (size_t c = 0; c < chunks; ++c) {
+    if (c + 1 < chunks) {
+      rc = dma(c + 1);  // its staging buffer's previous chunk (c - 1) was copied out already
+      if (rc != AV_OK) return rc;
+    }
+    AV_HIP(hipEventSynchronize(e->stage_ev[c & 1]));
+    const size_t w = std::min(kChunk, n - c * kChunk);
+    const uint64_t* src = static_cast<const uint64_t*>(e->stage[c & 1]);
+    uint64_t* dst = out + c * kChunk;
+    parallel_chunks((int64_t)w, 1 << 18, [&](int, int64_t a, int64_t b) {
+      std::memcpy(dst + a, src + a, (size_t)(b - a) * 8);
+    });
+  }
+  return AV_OK;
+}
+
 int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
   AV_ENTER(e);
   AV_PEER_SYNC_CHECK(e);
@@ -1906,8 +1977,8 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
     AV_CHECK(singles + n_med + n_dense == total, AV_ERR_HIP, "StatusUpdate log inconsistent (%lld of %lld)",
              (long long)(singles + n_med + n_dense), (long long)total);
     AV_HIP(avk::launch_sort_updates(sort_tmp, &sort_bytes, words, sorted, (uint64_t)total, 2, end_bit, e->stream));
-    AV_HIP(hipMemcpyAsync(out, sorted, (size_t)total * 8, hipMemcpyDeviceToHost, e->stream));
-    AV_HIP(hipStreamSynchronize(e->stream));
+    rc = copy_out(e, out, sorted, (size_t)total);
+    if (rc != AV_OK) return rc;
   }
   return clear_log(e);
 }
@@ -2244,6 +2315,11 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     e->dense_min = (uint32_t)value;
   } else if (n == "fresh") {  // 0: a round after init reads every plane (A/B only)
     if (!value) e->fresh = false;
+  } else if (n == "push_defer") {  // A/B: 0 = every push stored from the tile loop
+    e->push_defer = value != 0;
+  } else if (n == "push_store") {  // A/B: 1 = plain stores (default), 0 = system scope, 2 = none (results invalid)
+    AV_CHECK(value >= 0 && value <= 2, AV_ERR_INVALID_ARG, "push_store must be 0, 1 or 2");
+    e->push_store = (uint32_t)value;
   } else if (n == "peer_mask") {  // before the exchange is set up: need-masked pushes (default 1)
     AV_CHECK(e->peer_world == 0, AV_ERR_INVALID_ARG, "peer_mask must be set before the exchange is set up");
     e->peer_mask = value != 0;

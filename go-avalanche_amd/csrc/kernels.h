@@ -170,6 +170,8 @@ struct RoundParams {
   // the pushes queued in LDS and stored after a wave's last tile (round_sweep.hip flush_pushes): the
   // sweep's waves each take at most kPushQ tiles and push_n <= 8 (a byte per lane and tile)
   uint32_t push_q;
+  uint32_t push_defer;  // engine option "push_defer" (default 1): the sweep may queue its pushes (push_q)
+  uint32_t push_store;  // engine option "push_store": 1 = plain stores (default), 0 = system scope, 2 = none (diagnostics)
   // Deferred count planes (`kl`, k = 8, warm sim rounds in which no record can
   // finalize): a tile all of whose polled records agreed with
   // their accepted bit on all 8 votes gains exactly +8 on every polled count
@@ -209,6 +211,7 @@ struct RoundParams {
   const uint32_t* uni_in;
   uint32_t uni_world, uni_rank, uni_off;
   uint32_t uni_merge;  // a round with a uniform input: every uni_merge-th wave takes uni_merge runs (1: off)
+  uint32_t uni_post;   // peer-push rounds: the rank's slot reaches the peers after the round (launch_peer_barrier)
 
   // fresh: the round right after av_init_records: every record is a
   // NewVoteRecord (votes = consider = 0, count 0, vote.go:33-35), so the
@@ -352,7 +355,11 @@ hipError_t launch_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, u
 // waits until every slot of its own array (arrive[rank]) has reached `seq`.
 // Gives up after timeout_ticks of the wall clock and sets *err (later barriers then return at once).
 hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
-                               uint64_t timeout_ticks, hipStream_t s);
+                               uint64_t timeout_ticks, hipStream_t s, const uint32_t* slot = nullptr,
+                               PeerPtrs slot_dst = PeerPtrs{}, uint32_t wait = 1u);
+// (slot: this rank's uniform-rows mismatch slot of the snapshot the round wrote, copied into every
+// peer's replica (slot_dst.p[i]: rank i's copy) before the arrival; wait = 0: no arrival and no wait
+// (the serial peer group, whose stream order is the barrier))
 // Wall-clock ticks of a timeout (the device's wall clock rate; queried once per engine).
 hipError_t peer_timeout_ticks(int device, uint32_t timeout_ms, uint64_t* ticks);
 

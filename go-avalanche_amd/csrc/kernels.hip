@@ -968,8 +968,17 @@ __global__ __launch_bounds__(256) void k_need_combine(const uint32_t* needin, ui
 // waiting; the host refuses further rounds and results (engine.cpp
 // peer_failed, AV_ERR_PEER).
 __global__ __launch_bounds__(64) void k_peer_barrier(PeerPtrs arrive, const uint32_t* own, uint32_t world,
-                                                     uint32_t rank, uint32_t seq, uint32_t* err, uint64_t ticks) {
+                                                     uint32_t rank, uint32_t seq, uint32_t* err, uint64_t ticks,
+                                                     const uint32_t* uslot, PeerPtrs slot_dst, uint32_t wait) {
   const uint32_t i = threadIdx.x;
+  if (uslot && i < world && i != rank) {  // this rank's uniform-rows slot into rank i's replica (before arriving)
+    uint32_t* d = slot_dst.p[0];
+#pragma unroll
+    for (int r = 1; r <= kMaxPeers; ++r)
+      if ((uint32_t)r == i) d = slot_dst.p[r];
+    __hip_atomic_store(d, *uslot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (!wait) return;
   uint32_t* mine = arrive.p[0];  // lane i's rank-i array, selected with static indices
 #pragma unroll
   for (int r = 1; r <= kMaxPeers; ++r)
@@ -1090,10 +1099,11 @@ hipError_t peer_timeout_ticks(int device, uint32_t timeout_ms, uint64_t* ticks) 
 }
 
 hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, uint32_t seq, uint32_t* err,
-                               uint64_t timeout_ticks, hipStream_t s) {
+                               uint64_t timeout_ticks, hipStream_t s, const uint32_t* slot, PeerPtrs slot_dst,
+                               uint32_t wait) {
   if (world > (uint32_t)kMaxPeers + 1u || rank >= world) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, s, arrive, arrive.p[rank], world, rank, seq, err,
-                     timeout_ticks);
+                     timeout_ticks, slot, slot_dst, wait);
   return hipGetLastError();
 }
 

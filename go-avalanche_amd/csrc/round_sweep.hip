@@ -85,6 +85,17 @@ __device__ __forceinline__ uint32_t* peer_ptr(uint32_t* const* tbl, uint32_t r) 
   return reinterpret_cast<uint32_t*>(t[__builtin_amdgcn_readfirstlane((int)r)]);
 }
 
+// One word into a peer's replica (p.push_store): 1 = a plain store (default: the round kernel's
+// completion releases it at system scope before the barrier kernel that follows it on the stream runs,
+// which orders it for the peer; measured far cheaper to issue than the scoped form), 0 = a system-scope
+// store (the first form), 2 = none (diagnostics: the exchange's stores ablated, results invalid).
+__device__ __forceinline__ void push_word(const RoundParams& p, uint32_t* dst, uint32_t v) {
+  if (p.push_store == 1u)
+    *dst = v;
+  else if (p.push_store == 0u)
+    __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The published word of one lane into pref_out. In a peer-push round the word being overwritten is
 // what every peer replica holds (kernels.h), so only a changed word is stored into each replica
 // (system-scope write-through stores over xGMI; the barrier after the round orders them before any
@@ -136,7 +147,7 @@ __device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uin
       const uint32_t push = nm & (pub != old ? p.peer_all : st);
       for (uint32_t r = 0; r < p.push_n; ++r) {
         const bool go = (push >> r) & 1u;
-        if (go) __hip_atomic_store(peer_ptr(p.push_dst, r) + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (go) push_word(p, peer_ptr(p.push_dst, r) + prow, pub);
         acc.pushed += (uint32_t)__popcll(__ballot(go));
       }
       const uint32_t nst = (st | (m ? p.peer_all : 0u)) & ~nm;
@@ -144,7 +155,7 @@ __device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uin
     } else {
       if (pub != old)
         for (uint32_t r = 0; r < p.push_n; ++r)
-          __hip_atomic_store(peer_ptr(p.push_dst, r) + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          push_word(p, peer_ptr(p.push_dst, r) + prow, pub);
       acc.pushed += (uint32_t)__popcll(m) * p.push_n;
     }
   }
@@ -168,7 +179,7 @@ __device__ __forceinline__ void flush_pushes(const RoundParams& p, uint32_t lane
     const uint32_t prow = (p.n0 + nl) * p.PS + (g - nl * p.BL);
 #pragma unroll
     for (uint32_t r = 0; r < 8u; ++r)
-      if ((pm >> r) & 1u) __hip_atomic_store(dst[r] + prow, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((pm >> r) & 1u) push_word(p, dst[r] + prow, pub);
   }
 }
 
@@ -1219,10 +1230,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   if (p.uni_out && __ballot(acc.umis != 0u) != 0ull && lane == 0) {
     // some word this wave published differs from the reference row: tag the output snapshot's slot
     // of this rank in every replica (read by the next round, after the barrier in a peer exchange)
+    // (p.uni_post: the engine copies the slot to the peers once after the round, in the barrier
+    // kernel: every wave of a storm round tags, and 7 system-scope stores per wave into the same 7
+    // words serialised the whole round, 0.13 -> 0.6 ms per rank at 8 ranks)
     const uint32_t tag = p.round + 1u;
     p.uni_out[p.uni_rank] = tag;
-    for (uint32_t r = 0; r < p.push_n; ++r)
-      __hip_atomic_store(peer_ptr(p.push_dst, r) + p.uni_off + p.uni_rank, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!p.uni_post)
+      for (uint32_t r = 0; r < p.push_n; ++r)
+        __hip_atomic_store(peer_ptr(p.push_dst, r) + p.uni_off + p.uni_rank, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1281,7 +1296,7 @@ hipError_t launch_sweep_k(const RoundParams& p_in, bool replay, uint32_t blocks,
   // larger worlds push from the tile loop
   {
     const uint32_t waves = grid * 4u, tiles = p.Lpad / 64u;
-    p.push_q = p.push_n && p.push_n <= 8u && (tiles + waves - 1u) / waves <= kPushQ ? 1u : 0u;
+    p.push_q = p.push_defer && p.push_n && p.push_n <= 8u && (tiles + waves - 1u) / waves <= kPushQ ? 1u : 0u;
   }
   if (p_in.tpw && K == 8 && !replay && !p.ablate_gather && !p.fresh && p.warm_skip && p.warm_all) {
     // p_in.tpw = enabled: each wave takes a run of consecutive tiles

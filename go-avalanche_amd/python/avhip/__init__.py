@@ -388,6 +388,14 @@ class Engine:
         buf = buf[: got.value]
         return decode_updates(buf, base) if decode else buf
 
+    def fetch_into(self, buf):
+        """All pending StatusUpdates, packed and sorted canonical, into the caller's uint64 buffer
+        (av_fetch_updates); returns how many."""
+        assert buf.dtype == np.uint64 and buf.flags.c_contiguous
+        got = C.c_int64(0)
+        _check(lib().av_fetch_updates(self._h, _ptr(buf), buf.size, C.byref(got)))
+        return got.value
+
     def updates_digest(self, n0=None, n1=None):
         """(count, sum, xor) of splitmix64 over the pending packed updates (not
         cleared), of nodes [n0, n1) if given."""

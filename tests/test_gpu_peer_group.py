@@ -73,11 +73,15 @@ def oracle_run(oracle, case):
     return sim, exp[np.lexsort(exp.T[::-1])]
 
 
-@pytest.mark.parametrize("mask", [1, 0], ids=["masked", "full"])
+@pytest.mark.parametrize("mode", ["masked", "full", "direct"])
 @pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("case", sorted(CASES))
-def test_peer_group_vs_oracle(oracle, case, world, mask):
-    rec, upd, own = run_case(case, world, extra=(("peer_mask", mask),))
+def test_peer_group_vs_oracle(oracle, case, world, mode):
+    # masked: need-masked pushes (where the layout allows), queued per wave; full: every changed word to
+    # every peer, queued; direct: every changed word stored from the tile loop (push_defer 0)
+    extra = {"masked": (("peer_mask", 1),), "full": (("peer_mask", 0),),
+             "direct": (("peer_mask", 0), ("push_defer", 0))}[mode]
+    rec, upd, own = run_case(case, world, extra=extra)
     sim, exp = oracle_run(oracle, case)
     assert np.array_equal(rec, sim.dump()), "VoteRecord state differs from the oracle"
     assert np.array_equal(upd, exp), "StatusUpdate stream differs from the oracle"

@@ -36,6 +36,16 @@ for s in "$@"; do
     gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --json $OUT/group_model_c4p.json ;;
     gm_c4pb) step gm_c4pb 900 python tools/group_model.py --workload c4pb --json $OUT/group_model_c4pb.json ;;
     ab_c2late) step ab_c2late 600 bash -c 'for i in 1 2 3; do for v in default late; do echo "== $v"; if [ $v = default ]; then python tools/fuse_probe.py | head -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_late.so python tools/fuse_probe.py | head -1; fi; done; done' ;;
+    gm_ab) step gm_ab 900 python tools/group_model.py --workload c4p --ranks 8 --kinds targets,masked --variant scoped:push_store=0 --variant ablate:push_store=2 --variant direct:push_defer=0 --variant nomask_abl:peer_mask=0,push_store=2 --variant nomask:peer_mask=0 --json $OUT/group_model_c4p_ab.json ;;
+    gm_trace) step gm_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/gm_trace -o gm -- \
+            python3 tools/group_model.py --workload c4p --ranks 8 --kinds masked --steps 6 ;;
+    ns_probe) step ns_probe 600 bash -c 'for o in "count_changed=0" "count_changed=1"; do python tools/node_shard_probe.py --workload c4p --shards 1,8 --kinds nodes --rounds 6 --option $o; done' ;;
+    gm_merge) step gm_merge 900 python tools/group_model.py --workload c4 --kinds targets --target-option uni_merge=4 --json $OUT/group_model_c4_merge4.json ;;
+    pmcea_req) step pmcea_req_${WL:-c5} 600 timeout -s KILL 500 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum \
+            --output-format csv -d $OUT/pmcea_req_${WL:-c5} -o bench -- python3 bench.py --workload ${WL:-c5} --no-cpu-baseline --no-secondary --no-exchange-pass ;;
+    pmcea_dram) step pmcea_dram_${WL:-c5} 600 timeout -s KILL 500 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum GRBM_GUI_ACTIVE \
+            --output-format csv -d $OUT/pmcea_dram_${WL:-c5} -o bench -- python3 bench.py --workload ${WL:-c5} --no-cpu-baseline --no-secondary --no-exchange-pass ;;
+    pmcea_sum) step pmcea_sum_${WL:-c5} 120 python tools/pmc_ea.py --req $OUT/pmcea_req_${WL:-c5} --dram $OUT/pmcea_dram_${WL:-c5} --out $OUT/pmc_ea_${WL:-c5}.json ;;
     pmclist) step pmclist 120 rocprofv3 -L ;;
     testsall) step pytest_gpu 1500 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py ;;

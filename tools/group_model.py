@@ -91,9 +91,11 @@ def window(engs, init, warmup, steps, on_round):
         e.set_timing(False)
 
 
-def run_single(n, m, k, byz, init, warmup, steps, **kw):
+def run_single(n, m, k, byz, init, warmup, steps, options=(), **kw):
     e = avhip.Engine(n, m, k=k, seed=SEED, byz_threshold=byz, log_capacity=log_cap(kw.get("nl", n), m), **{
         k2: v for k2, v in kw.items() if k2 != "nl"})
+    for name, v in options:
+        e.set_option(name, v)
     rows = []
     window([e], init, warmup, steps, lambda r, ms, pw: None)  # device warm-up
     window([e], init, warmup, steps, lambda r, ms, pw: rows.append({"round": r, "ms": ms[0]}))
@@ -101,7 +103,7 @@ def run_single(n, m, k, byz, init, warmup, steps, **kw):
     return rows
 
 
-def run_group(n, m, k, byz, init, warmup, steps, g, mask, t_range=None):
+def run_group(n, m, k, byz, init, warmup, steps, g, mask, t_range=None, options=()):
     per = n // g
     engs = []
     for r in range(g):
@@ -112,6 +114,8 @@ def run_group(n, m, k, byz, init, warmup, steps, g, mask, t_range=None):
         engs.append(avhip.Engine(n, mm, k=k, seed=SEED, byz_threshold=byz, log_capacity=log_cap(per, mm), **kw))
     for e in engs:
         e.set_option("peer_mask", mask)
+        for name, v in options:
+            e.set_option(name, v)
         e.init_records(*init)
     avhip.peer_group_serial(engs)
     rows = []
@@ -145,8 +149,13 @@ def main():
     ap.add_argument("--ranks", default="2,4,8")
     ap.add_argument("--kinds", default="targets,nodes,masked,2d")
     ap.add_argument("--barrier-us", type=float, default=6.0)
+    ap.add_argument("--target-option", action="append", default=[],
+                    help="name=value on the target-shard engines (an extra 'targets+' row)")
+    ap.add_argument("--variant", action="append", default=[],
+                    help="name:opt=v,opt=v -- an extra masked node-shard row with engine options (A/B)")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
+    topts = [(o.split("=")[0], int(o.split("=")[1])) for o in args.target_option]
     N, M, K, init_mode, init_param, byz, replay, desc = WORKLOADS[args.workload]
     assert not replay, "sim workloads only"
     init = (init_mode, init_param)
@@ -177,10 +186,21 @@ def main():
             rows = run_single(N, M, K, byz, init, args.warmup, args.steps,
                               target_range=sharding.target_shard(M, g, 0))
             record(g, "targets", [{"round": r["round"], "ms": r["ms"], "kernel_ms_max": r["ms"]} for r in rows])
+            if topts:
+                rows = run_single(N, M, K, byz, init, args.warmup, args.steps, options=topts,
+                                  target_range=sharding.target_shard(M, g, 0))
+                record(g, "targets+" + ",".join(args.target_option),
+                       [{"round": r["round"], "ms": r["ms"], "kernel_ms_max": r["ms"]} for r in rows])
         for name, mask in (("nodes", 0), ("masked", 1)):
             if name in kinds and N % g == 0:
                 rows = run_group(N, M, K, byz, init, args.warmup, args.steps, g, mask)
                 record(g, name, project(rows, g - 1, args.barrier_us))
+        for var in args.variant:
+            vname, vopts = var.split(":")
+            opts = [(o.split("=")[0], int(o.split("=")[1])) for o in vopts.split(",") if o]
+            if N % g == 0:
+                rows = run_group(N, M, K, byz, init, args.warmup, args.steps, g, 1, options=opts)
+                record(g, "masked+" + vname, project(rows, g - 1, args.barrier_us))
         if "2d" in kinds and g >= 4:
             for gn in (2, 4) if g == 8 else (2,):
                 gt = g // gn
