@@ -240,6 +240,11 @@ struct av_engine {
   avk::PeerPtrs peer_needin{};     // every rank's needin
   int64_t need_ready = -1;         // window whose needmask is combined
   int64_t need_pushed = -1;        // window whose drawn rows were pushed to the peers
+  // the next window's rows are drawn on a side stream while the current window's rounds run
+  // (need_draw_ahead): need_free = the last push that read need_mine, need_drawn = the draw done
+  hipStream_t need_stream = nullptr;
+  hipEvent_t need_free = nullptr, need_drawn = nullptr;
+  int64_t need_drawn_w = -1;       // window whose rows the side stream drew (or is drawing)
   // changed published words (kernels.h RoundParams::changed): counted in every peer-push round and,
   // with option "count_changed", in every sweep round
   unsigned long long* changed = nullptr;
@@ -465,7 +470,19 @@ bool mask_layout_ok(const av_engine* e) {
 
 // After the exchange's pointers are set (own needin allocated, peer_needin filled): buffers of the
 // masked form, every replica identical (nothing withheld).
+uint32_t default_sweep_blocks(const av_engine* e, bool force);
+extern "C" int relayout_log_if_empty(av_engine* e);
+
 int mask_setup(av_engine* e) {
+  // node shards of an exchange: runs of up to 16 tiles per wave (the longest the shared draw holds,
+  // BL >= 16) unless set: the single-GPU rule (>= 15000 waves) gave 4 at 8 ranks of C4, whose settled
+  // rounds then paid 4x the per-wave set-up (tools/group_model.py)
+  if (!e->tiles_per_wave && !e->sweep_blocks_explicit && e->BL >= 16 && e->peer_world >= 4) {
+    e->tiles_per_wave = 16;
+    e->sweep_blocks = default_sweep_blocks(e, false);
+    int rc = relayout_log_if_empty(e);  // fewer writer waves
+    if (rc != AV_OK) return rc;
+  }
   e->masked = e->peer_mask && e->peer_world >= 2 && e->peer_world <= 9 && mask_layout_ok(e) && e->needin;
   if (!e->masked) return AV_OK;
   e->segs = (e->BL + 31) / 32;
@@ -473,7 +490,10 @@ int mask_setup(av_engine* e) {
   AV_HIP(dev_alloc(&e->needmask, (size_t)avk::kNeedWin * e->NL));
   AV_HIP(dev_alloc(&e->stale, (size_t)3 * e->NL * e->segs));
   AV_HIP(hipMemsetAsync(e->stale, 0, (size_t)3 * e->NL * e->segs, e->stream));
-  e->need_ready = e->need_pushed = -1;
+  AV_HIP(hipStreamCreateWithFlags(&e->need_stream, hipStreamNonBlocking));
+  AV_HIP(hipEventCreateWithFlags(&e->need_free, hipEventDisableTiming));
+  AV_HIP(hipEventCreateWithFlags(&e->need_drawn, hipEventDisableTiming));
+  e->need_ready = e->need_pushed = e->need_drawn_w = -1;
   return AV_OK;
 }
 
@@ -487,15 +507,41 @@ int stale_clear(av_engine* e, int b) {
 
 // Window w = push rounds [w W, w W + W): the rows this rank's nodes draw in rounds w W + 1 .. w W + W
 // (R1's sampling), pushed to their owners; enqueued before a barrier, combined after it.
+int need_draw(av_engine* e, int64_t w, hipStream_t s) {
+  const uint32_t W = avk::kNeedWin;
+  AV_HIP(hipMemsetAsync(e->need_mine, 0, (size_t)W * e->N, s));
+  AV_HIP(avk::launch_need_draw(e->cfg.seed, (uint32_t)e->N, (uint32_t)e->n0, e->NL, (uint32_t)(w * W + 1), W, e->k,
+                               e->cfg.peer_mode, e->need_mine, s));
+  return AV_OK;
+}
+
 int need_gen(av_engine* e, int64_t w) {
   if (!e->masked || e->need_pushed == w) return AV_OK;
-  const uint32_t W = avk::kNeedWin;
-  AV_HIP(hipMemsetAsync(e->need_mine, 0, (size_t)W * e->N, e->stream));
-  AV_HIP(avk::launch_need_draw(e->cfg.seed, (uint32_t)e->N, (uint32_t)e->n0, e->NL, (uint32_t)(w * W + 1), W, e->k,
-                               e->cfg.peer_mode, e->need_mine, e->stream));
-  AV_HIP(avk::launch_need_push(e->need_mine, (uint32_t)e->N, e->NL, W, (uint32_t)e->peer_world,
+  if (e->need_drawn_w == w) {
+    AV_HIP(hipStreamWaitEvent(e->stream, e->need_drawn, 0));  // drawn ahead on the side stream
+  } else {
+    int rc = need_draw(e, w, e->stream);
+    if (rc != AV_OK) return rc;
+  }
+  AV_HIP(avk::launch_need_push(e->need_mine, (uint32_t)e->N, e->NL, avk::kNeedWin, (uint32_t)e->peer_world,
                                (uint32_t)e->peer_rank, (uint32_t)(w & 1), e->peer_needin, e->stream));
+  AV_HIP(hipEventRecord(e->need_free, e->stream));
   e->need_pushed = w;
+  e->need_drawn_w = -1;
+  return AV_OK;
+}
+
+// Window w + 1's rows drawn on the side stream while window w's rounds run (after window w's push
+// released need_mine); need_gen at the end of window w waits for it.
+// (not in a serial peer group: there every rank's side stream would run beside the other ranks'
+// rounds on the one device, which a rank of a real run never sees; the group draws inline)
+int need_draw_ahead(av_engine* e, int64_t w) {
+  if (!e->masked || e->group || e->need_drawn_w == w || e->need_pushed >= w) return AV_OK;
+  AV_HIP(hipStreamWaitEvent(e->need_stream, e->need_free, 0));
+  int rc = need_draw(e, w, e->need_stream);
+  if (rc != AV_OK) return rc;
+  AV_HIP(hipEventRecord(e->need_drawn, e->need_stream));
+  e->need_drawn_w = w;
   return AV_OK;
 }
 
@@ -714,6 +760,7 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
   }
   if (p.push_n && e->masked) {  // (inside the round's timing: the exchange's own work)
     int rc = need_combine(e, e->round / avk::kNeedWin);
+    if (rc == AV_OK) rc = need_draw_ahead(e, e->round / avk::kNeedWin + 1);
     if (rc != AV_OK) return rc;
   }
   bool refw = false;  // the round wrote reference-row flags for the snapshot it published
@@ -967,6 +1014,12 @@ int av_destroy(av_engine* e) {
   if (e->changed) (void)hipFree(e->changed);
   if (e->push_tbl) (void)hipFree(e->push_tbl);
   if (e->marker) (void)hipEventDestroy(e->marker);
+  if (e->need_stream) {
+    (void)hipStreamSynchronize(e->need_stream);
+    (void)hipStreamDestroy(e->need_stream);
+  }
+  if (e->need_free) (void)hipEventDestroy(e->need_free);
+  if (e->need_drawn) (void)hipEventDestroy(e->need_drawn);
   if (e->group) {
     PeerGroup* g = e->group;
     g->members[(size_t)e->peer_rank] = nullptr;

@@ -122,11 +122,13 @@ __device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uin
                                         SweepAcc& acc, bool known, uint32_t nl, uint32_t slot) {
   if (CC && p.count_changed) {
     if (!known && !AVK_CC_PREFETCH) old = p.pref_out[prow];
-    uint32_t nm = 0u, st = 0u, si = 0u;
+    uint32_t nm = p.peer_all, st = 0u, si = 0u;
     if (p.stale) {
       si = nl * p.segs + ((prow - (p.n0 + nl) * p.PS) >> 5);
-      nm = p.need ? (uint32_t)p.need[nl] : p.peer_all;
       st = p.stale[si];
+      // a word known unchanged (a settled tile) goes out only where a change was withheld: the need
+      // mask is read only then (settled rounds after the catch-up read one byte per lane, not two)
+      if (p.need && (!known || __ballot(st != 0u) != 0ull)) nm = (uint32_t)p.need[nl];
     }
     const unsigned long long m = __ballot(pub != old);
     const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
@@ -137,8 +139,7 @@ __device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uin
       const uint32_t push = p.stale ? nm & (pub != old ? p.peer_all : st) : (pub != old ? p.peer_all : 0u);
       const uint32_t lane = __lane_id();
       acc.qpm[slot * 64u + lane] = (uint8_t)push;
-      acc.qpub[slot * 64u + lane] = pub;
-      for (uint32_t r = 0; r < p.push_n; ++r) acc.pushed += (uint32_t)__popcll(__ballot((push >> r) & 1u));
+      if (push) acc.qpub[slot * 64u + lane] = pub;  // (read only where pm != 0; counted by flush_pushes)
       if (p.stale) {
         const uint32_t nst = (st | (m ? p.peer_all : 0u)) & ~nm;
         if (nst != st) p.stale[si] = (uint8_t)nst;
@@ -165,14 +166,16 @@ __device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uin
 
 // The queued pushes of a wave's tiles (p.push_q): tile first + s * step for queue slot s < n. The peer
 // pointers are read once; the stores are the wave's last memory instructions, back to back.
-__device__ __forceinline__ void flush_pushes(const RoundParams& p, uint32_t lane, uint32_t first, uint32_t step,
-                                             uint32_t n, const uint32_t* qpub, const uint8_t* qpm) {
+__device__ __forceinline__ uint32_t flush_pushes(const RoundParams& p, uint32_t lane, uint32_t first, uint32_t step,
+                                                 uint32_t n, const uint32_t* qpub, const uint8_t* qpm) {
   uint32_t* dst[8];
 #pragma unroll
   for (uint32_t r = 0; r < 8u; ++r) dst[r] = r < p.push_n ? peer_ptr(p.push_dst, r) : nullptr;
+  uint32_t words = 0u;  // this lane's pushed words (returned: the caller sums the wave once)
   for (uint32_t s = 0; s < n; ++s) {
     const uint32_t g = (first + s * step) * 64u + lane;
     const uint32_t pm = g < p.L ? (uint32_t)qpm[s * 64u + lane] : 0u;
+    words += (uint32_t)__popc(pm);
     if (pm == 0u) continue;
     const uint32_t pub = qpub[s * 64u + lane];
     const uint32_t nl = div_bl(p, g);
@@ -181,6 +184,7 @@ __device__ __forceinline__ void flush_pushes(const RoundParams& p, uint32_t lane
     for (uint32_t r = 0; r < 8u; ++r)
       if ((pm >> r) & 1u) push_word(p, dst[r] + prow, pub);
   }
+  return words;
 }
 
 enum : int { kModeWarm = 0, kModeCheck = 1, kModeReplay = 2, kModeAblate = 3, kModeWarmPipe = 4, kModeFresh = 5 };
@@ -1204,7 +1208,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
       }
     }
     if constexpr (CC) {
-      if (p.push_q && qn) flush_pushes(p, lane, qfirst, qstep, qn, acc.qpub, acc.qpm);
+      if (p.push_q && qn) acc.pushed += (uint32_t)wave_sum(flush_pushes(p, lane, qfirst, qstep, qn, acc.qpub, acc.qpm));
     }
   }
   // one flush per wave (shard = wave index); 32-bit sums: a wave's lanes

@@ -32,13 +32,15 @@ for s in "$@"; do
     testsnew) step pytest_new 1200 python -u -m pytest tests/test_gpu_delivery.py tests/test_gpu_fullsize.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testslog) step pytest_log 600 python -u -m pytest tests/test_gpu_log_layout.py tests/test_gpu_peer_group.py tests/test_gpu_bench_protocol.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     peers) step pytest_peers 900 python -u -m pytest tests/test_gpu_peer_group.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    gm_c4) step gm_c4 900 python tools/group_model.py --workload c4 --json $OUT/group_model_c4.json ;;
-    gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --json $OUT/group_model_c4p.json ;;
-    gm_c4pb) step gm_c4pb 900 python tools/group_model.py --workload c4pb --json $OUT/group_model_c4pb.json ;;
+    gm_c4) step gm_c4 900 python tools/group_model.py --workload c4 --variant nomask:peer_mask=0 --variant tpw16:tiles_per_wave=16 --variant nomask_tpw16:peer_mask=0,tiles_per_wave=16 --json $OUT/group_model_c4.json ;;
+    gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --variant nomask:peer_mask=0 --json $OUT/group_model_c4p.json ;;
+    gm_c4pb) step gm_c4pb 900 python tools/group_model.py --workload c4pb --variant nomask:peer_mask=0 --json $OUT/group_model_c4pb.json ;;
     ab_c2late) step ab_c2late 600 bash -c 'for i in 1 2 3; do for v in default late; do echo "== $v"; if [ $v = default ]; then python tools/fuse_probe.py | head -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_late.so python tools/fuse_probe.py | head -1; fi; done; done' ;;
     gm_ab) step gm_ab 900 python tools/group_model.py --workload c4p --ranks 8 --kinds targets,masked --variant scoped:push_store=0 --variant ablate:push_store=2 --variant direct:push_defer=0 --variant nomask_abl:peer_mask=0,push_store=2 --variant nomask:peer_mask=0 --json $OUT/group_model_c4p_ab.json ;;
     gm_trace) step gm_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/gm_trace -o gm -- \
-            python3 tools/group_model.py --workload c4p --ranks 8 --kinds masked --steps 6 ;;
+            python3 tools/group_model.py --workload c4p --ranks 8 --kinds masked --json $OUT/gm_trace.json ;;
+    gm_tpw) step gm_tpw 900 python tools/group_model.py --workload c4p --ranks 8 --kinds masked --variant nomask:peer_mask=0 --variant tpw8:tiles_per_wave=8 --variant tpw16:tiles_per_wave=16 --variant nomask_tpw8:peer_mask=0,tiles_per_wave=8 --json $OUT/group_model_c4p_tpw.json ;;
+    gm_c4m) step gm_c4m 900 python tools/group_model.py --workload c4 --ranks 8 --kinds targets,masked --target-option uni_merge=4 --variant merge4:uni_merge=4 --variant nomask:peer_mask=0 --variant nomask_merge4:peer_mask=0,uni_merge=4 --json $OUT/group_model_c4_merge.json ;;
     ns_probe) step ns_probe 600 bash -c 'for o in "count_changed=0" "count_changed=1"; do python tools/node_shard_probe.py --workload c4p --shards 1,8 --kinds nodes --rounds 6 --option $o; done' ;;
     gm_merge) step gm_merge 900 python tools/group_model.py --workload c4 --kinds targets --target-option uni_merge=4 --json $OUT/group_model_c4_merge4.json ;;
     pmcea_req) step pmcea_req_${WL:-c5} 600 timeout -s KILL 500 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_sum \
