@@ -90,6 +90,20 @@ WORKLOADS = {
              "C4pb: 1M nodes x 500 double-spend pairs, k=8, 20% Byzantine flip-flop voters"),
 }
 
+# --shard auto (the default): the decomposition tools/group_model.py measured best per workload and
+# rank count (profiles/r05/s7): target shards, except the conflicting workloads at 8
+# ranks, whose rounds all change their rows: node shards with the need-masked peer push
+AUTO_SHARD = {8: {"c4p": "peers", "c4pb": "peers"}}
+
+
+def shard_for(wl, world, requested):
+    if requested != "auto":
+        return requested
+    if world <= 1:
+        return "targets"
+    return AUTO_SHARD.get(world, {}).get(wl, "targets")
+
+
 PARALLELISM = {
     "peers": "node-sharded, changed preference words pushed to peers over xGMI + device barrier per round",
     "nodes": "node-sharded, RCCL all-gather of preference rows per round",
@@ -114,7 +128,7 @@ def parse(argv=None):
     # targets: target shards, no exchange (default: DESIGN.md §5 measures it ahead of the node
     # shards at G = 2 and 4, even at 8); peers: node shards + peer-push exchange; nodes: node
     # shards + RCCL all-gather of the preference rows
-    ap.add_argument("--shard", default="targets", choices=["peers", "targets", "nodes"])
+    ap.add_argument("--shard", default="auto", choices=["auto", "peers", "targets", "nodes"])
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xA7A1A9C4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
@@ -414,6 +428,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     `warmup` untimed steps, `steps` timed steps; then a second pass over the
     same steps with HIP events around every round kernel (roofline)."""
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
+    args = argparse.Namespace(**vars(args))  # this workload's copy (its decomposition)
+    args.shard = shard_for(wl, world, args.shard)
     # replay (C2) keeps the per-update worst case; the sim workloads start small and are re-sized
     # after the warm-up epoch (size_log)
     log_cap = log_capacity(n, m, world, rank, args.shard) if replay else 1 << 20
@@ -597,7 +613,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         "first_round": warmup % EPOCH,
         "writeback_ms": writeback_ms, "changed": changed,
         "value_general": value_general, "general_rounds": sorted({pr["round"] for pr in gen}),
-        "log_bytes": log_bytes, "delivery": delivery,
+        "log_bytes": log_bytes, "delivery": delivery, "shard": args.shard,
+        "shard_fallback": getattr(args, "shard_fallback", None),
     }
 
 
@@ -621,7 +638,7 @@ def allgather_probe(world, local_rank, total_bytes=1_000_000 * 128, reps=5):
             "note": "C4 node-sharded round exchange (1M x 1000 bits), torch.distributed all_gather_into_tensor"}
 
 
-PMC_DIR = os.path.join(ROOT, "profiles", "r04")
+PMC_DIR = os.path.join(ROOT, "profiles", "r05")
 
 
 def load_pmc(wl, window, world):
@@ -822,7 +839,11 @@ def main(argv=None):
             for wl in others:
                 if wl == args.workload:
                     continue
-                sr = measure(wl, args, world, rank, local_rank, args.steps, args.warmup)
+                try:
+                    sr = measure(wl, args, world, rank, local_rank, args.steps, args.warmup)
+                except avhip.AvError as ex:  # a secondary workload's failure leaves the headline's line
+                    secondary[wl] = {"error": repr(ex)[:300]}
+                    continue
                 rf = roofline(sr, window, world)
                 secondary[wl] = {"value": sr["value"], "value_general": sr["value_general"],
                                  "ms_per_step": sr["elapsed"] / args.steps * 1e3,
@@ -831,6 +852,7 @@ def main(argv=None):
                     secondary[wl]["writeback_ms"] = sr["writeback_ms"]
                 if world > 1:
                     secondary[wl]["replicas_identical"] = sr["replicas_identical"]
+                    secondary[wl]["shard"] = sr["shard"]
                 detail["workloads"][wl] = {"workload": sr["desc"], "value": sr["value"], "delivery": sr["delivery"],
                                            "ms_per_step": sr["elapsed"] / args.steps * 1e3,
                                            "updates_emitted": int(sr["emitted"]), "roofline": rf,
@@ -867,7 +889,7 @@ def main(argv=None):
                 "n_nodes": r["n"], "n_targets": r["m"], "k": r["k"],
                 "rounds": f"step p = round p % 16 of a fresh network (all records live), timed from round {first}, "
                           f"{r['segments']} segment(s)",
-                "parallelism": (PARALLELISM[args.shard] + f" x{world}") if world > 1 else "single GPU",
+                "parallelism": (PARALLELISM[r["shard"]] + f" x{world}") if world > 1 else "single GPU",
             },
             "updates_emitted": int(r["emitted"]),
             "roofline": compact_roofline(rf),
@@ -878,8 +900,8 @@ def main(argv=None):
         }
         if r["replicas_identical"] is not None:
             line["config"]["replicas_identical"] = r["replicas_identical"]
-        if getattr(args, "shard_fallback", None):
-            line["config"]["shard_fallback"] = "peer exchange unavailable: " + args.shard_fallback
+        if r.get("shard_fallback"):
+            line["config"]["shard_fallback"] = "peer exchange unavailable: " + r["shard_fallback"]
         if secondary:
             line["secondary"] = secondary
         detail["workloads"][args.workload] = {"workload": r["desc"], "value": r["value"], "delivery": r["delivery"],

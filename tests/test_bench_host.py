@@ -160,3 +160,15 @@ def test_window_segments_split_at_epochs():
     assert bench.window_segments(0, 16) == [list(range(16))]
     assert bench.window_segments(16, 3) == [[0, 1, 2]]
     assert bench.window_segments(15, 2) == [[15], [0]]
+
+
+def test_shard_auto_per_workload():
+    """--shard auto: target shards except the conflicting workloads at 8 ranks
+    (node shards with the need-masked push), as measured."""
+    import bench
+    assert bench.shard_for("c4", 1, "auto") == "targets"
+    assert bench.shard_for("c4", 8, "auto") == "targets"
+    assert bench.shard_for("c4p", 8, "auto") == "peers"
+    assert bench.shard_for("c4pb", 8, "auto") == "peers"
+    assert bench.shard_for("c4p", 4, "auto") == "targets"
+    assert bench.shard_for("c4p", 8, "nodes") == "nodes"
