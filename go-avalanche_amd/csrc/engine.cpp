@@ -919,11 +919,14 @@ uint64_t log_writer_waves(const av_engine* e) {
 // Shard count and per-shard capacities of the (empty) log from the allocation and the writers: a
 // power of two with >= 4 writers per shard in every kernel, so that the modulo's uneven wrap (W
 // writers over S shards: some get ceil(W / S)) loads no shard more than 1.25x the mean.
-void set_log_layout(av_engine* e) {
-  const uint64_t w = log_writer_waves(e);
+uint64_t log_shards_for(uint64_t w) {
   uint64_t sh = 1;
   while (sh * 2 <= avk::kLogShards && sh * 2 * 4 <= w) sh *= 2;
-  e->log_shards = (uint32_t)sh;
+  return sh;
+}
+
+void set_log_layout(av_engine* e) {
+  e->log_shards = (uint32_t)log_shards_for(log_writer_waves(e));
   e->log_cap = (uint32_t)std::min<size_t>(e->log_alloc / e->log_shards, 0xFFFFFFFFu);
   e->mlog_cap = (uint32_t)std::min<size_t>(e->mlog_alloc / e->log_shards, 0xFFFFFFFFu);
   e->dlog_cap = (uint32_t)std::min<size_t>(e->dlog_alloc / e->log_shards, 0xFFFFFFFFu);
@@ -2126,9 +2129,17 @@ int av_resize_log(av_engine* e, const int64_t entries[3]) {
   if (rc != AV_OK) return rc;
   AV_CHECK(!c.ovf && c.total == 0 && c.n_singles == 0 && c.n_med == 0 && c.n_records == 0, AV_ERR_UNSUPPORTED,
            "av_resize_log: the log holds updates (fetch or discard them first)");
-  // every shard gets the same share: the totals rounded up to whole shards, >= 16 entries per shard
+  // sized for the current grid's writer waves (log_writer_waves): a shard takes every sh-th writer, so
+  // with w writers one shard serves up to ceil(w / sh) of them; each writer gets ceil(n / w) + 1 entries
+  // (a writer owns one run of lanes, at most one more than the lanes' mean: "one entry per lane" holds
+  // any round), >= 16 per shard. The allocation is that per-shard share times kLogShards, so that a
+  // later re-layout to more shards keeps the total.
   const uint64_t sh = avk::kLogShards;
-  auto per = [&](int64_t n) { return std::max<uint64_t>(((uint64_t)n + sh - 1) / sh, 16); };
+  const uint64_t w = std::max<uint64_t>(log_writer_waves(e), 1), lsh = log_shards_for(w);
+  auto per = [&](int64_t n) {
+    const uint64_t shard = (((uint64_t)n + w - 1) / w + 1) * ((w + lsh - 1) / lsh);
+    return std::max<uint64_t>((shard * lsh + sh - 1) / sh, 16);
+  };
   const uint64_t s1 = per(entries[0]) * sh, s2 = per(entries[1]) * sh, s3 = per(entries[2]) * sh;
   AV_CHECK(s1 / sh < (1ull << 32) && s2 / sh < (1ull << 32) && s3 / sh < (1ull << 32), AV_ERR_INVALID_ARG,
            "log too large");

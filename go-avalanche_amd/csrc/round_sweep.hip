@@ -896,6 +896,13 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
 // general path.
 constexpr uint32_t kUniRun = 16;  // longest run settled_run_uni takes (p.tpw <= 16)
 
+// bit rel of the 256-bit set bm (rel per lane: a select chain, no scratch-indexed array)
+__device__ __forceinline__ bool byz_bit(const unsigned long long (&bm)[4], uint32_t rel) {
+  const uint32_t q = rel >> 6;
+  const unsigned long long w = q == 0u ? bm[0] : q == 1u ? bm[1] : q == 2u ? bm[2] : bm[3];
+  return (w >> (rel & 63u)) & 1ull;
+}
+
 template <int POL, bool CC>
 __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32_t lane, uint32_t t0,
                                                     uint32_t tile_end, uint32_t meta, uint32_t nlA, uint32_t nn,
@@ -905,7 +912,12 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
   const uint32_t vw = at_byte(p.valid, bo);
   const uint32_t refp = at_byte(p.pref_prev, p.ref_node * p.PS * 4u + bo);  // every vote word this round
   const uint32_t rin = p.uni_out ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
-  const unsigned long long byzm = __ballot(lane < nn && is_byz(p.byz, p.n0 + nlA + lane));
+  // the run's Byzantine bits, node nlA + rel at bit rel & 63 of byzm[rel >> 6]: up to 256 nodes (runs of
+  // 16 tiles at BL >= 4, the merged runs of uni_merge on target shards)
+  unsigned long long byzm[4];
+#pragma unroll
+  for (uint32_t j = 0; j < 4u; ++j)
+    byzm[j] = __ballot(lane + 64u * j < nn && is_byz(p.byz, p.n0 + nlA + lane + 64u * j));
   const uint32_t bpat = byz_pattern(p.round + 1u);
   const __amdgpu_buffer_rsrc_t ta =
       __builtin_amdgcn_make_buffer_rsrc(p.planes + (size_t)t0 * (kPlanes * 64u), 0, (int)(ntiles * kPlanes * 64u * 4u),
@@ -960,7 +972,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
       const uint32_t A = Av[i];
       const uint32_t mis = __ballot((refp ^ A) & P0) != 0ull ? 1u : 0u;  // always evaluated: no branch
       const bool ok = (((cand >> i) & 1u) & (mis ^ 1u)) != 0u;             // wave-uniform
-      const uint32_t pub = ((byzm >> (rel & 63u)) & 1ull) ? bpat : A;
+      const uint32_t pub = byz_bit(byzm, rel) ? bpat : A;
       const bool st = ok && active;
       __builtin_amdgcn_raw_buffer_store_b32(pub, prb, st ? prow * 4u : 0xFFFFFFFCu, 0, POL == 1 ? 2 : 0);  // (table < 4 GiB: 0xFFFFFFFC is past it)
       umis |= (st & (pub != rin)) ? 1u : 0u;
@@ -990,7 +1002,8 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
     const uint32_t P0 = active ? vw : 0u;  // polled = live (kPendAllLive) and valid
     if (__ballot((refp ^ A) & P0) != 0ull) continue;
     const uint32_t node = p.n0 + nl;
-    const uint32_t pub = ((byzm >> (nl - nlA)) & 1ull) ? bpat : A;
+    const bool bz = byz_bit(byzm, nl - nlA);
+    const uint32_t pub = bz ? bpat : A;
     if (active) {
       umis |= pub != rin ? 1u : 0u;
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
@@ -998,7 +1011,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
       // overwritten (publish): honest rows publish that word again, Byzantine rows its pattern's
       const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, (int)i);
       const bool known = AVK_CC_PREFETCH || (m & 0xFFu) >= 2u;
-      const uint32_t old = AVK_CC_PREFETCH ? Ov[i] : (((byzm >> (nl - nlA)) & 1ull) ? byz_pattern(p.round - 2u) : pub);
+      const uint32_t old = AVK_CC_PREFETCH ? Ov[i] : (bz ? byz_pattern(p.round - 2u) : pub);
       publish<POL, CC>(p, prow, pub, old, acc, known, nl, i);
     }
     done |= 1u << i;
@@ -1107,7 +1120,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           wd.nn = nn;
           // uniform rows: the run's settled candidates first, with no draw; the draw only if a tile is left
           const uint32_t all_tiles = (uint32_t)((1ull << (tile_end - tile)) - 1ull);
-          if (uniform && p.lean && p.settled_fast && p.klazy && p.vv && nn <= 64u && tile_end - tile <= kUniRun) {
+          if (uniform && p.lean && p.settled_fast && p.klazy && p.vv && nn <= 256u && tile_end - tile <= kUniRun) {
             uni_done = settled_run_uni<POL, CC>(p, lane, tile, tile_end, wd.meta, nlA, nn, acc);
             uni_ran = true;
           }

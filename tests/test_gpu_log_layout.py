@@ -165,12 +165,14 @@ def test_solo_barrier_is_sticky():
     e.close()
 
 
-def test_resize_log_one_entry_per_lane():
+@pytest.mark.parametrize("n,m", [(6000, 1000), (5000, 2000)], ids=["even", "uneven_writers"])
+def test_resize_log_one_entry_per_lane(n, m):
     """A log of one entry per lane and kind holds any single round (a lane's
     updates of a round are one entry), here the storm round of conflicting
     pairs; av_log_entries counts them by kind; a log holding updates is not
-    re-sized."""
-    n, m = 6000, 1000
+    re-sized. 5000 x 2000 (BL 63: 1231 writer waves over 256 shards) gives
+    some shards one writer more than others: the sizing serves the fullest
+    shard (C3's bench log overflowed at one entry per lane before)."""
     e = avhip.Engine(n, m, k=8, seed=9, log_capacity=1 << 20)
     lanes = e.layout_info()["lanes"]
     e.resize_log(lanes, lanes, lanes)

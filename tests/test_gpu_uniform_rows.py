@@ -107,13 +107,14 @@ def test_uniform_rows_add_targets_midrun(oracle):
     eng.close()
 
 
-@pytest.mark.parametrize("tpw,merge", [(4, 4), (8, 2)])
-def test_uni_merge_on_off_identical(tpw, merge):
+@pytest.mark.parametrize("tpw,merge,m", [(4, 4, 1000), (8, 2, 1000), (4, 4, 125), (8, 2, 250), (2, 8, 125)])
+def test_uni_merge_on_off_identical(tpw, merge, m):
     """Option uni_merge > 1 (a round with a uniform input: every merge-th wave takes its
     neighbours' runs, the others end at once) changes only the work split, never a result:
     digests, records and published rows equal to uni_merge = 1 at runs of tpw tiles (so that
-    tpw * merge <= 16 and the merge really happens)."""
-    n, m = 20_000, 1000
+    tpw * merge <= 16 and the merge really happens). m = 125 / 250 are C4's target
+    shards at 8 / 4 ranks (BL 4 / 8): a merged run of 16 tiles holds 256 / 128 nodes."""
+    n = 20_000
     out = []
     for um in (1, merge):
         eng = avhip.Engine(n, m, k=8, seed=7, log_capacity=1 << 26)

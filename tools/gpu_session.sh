@@ -31,6 +31,10 @@ for s in "$@"; do
     tests) step pytest_gpu 1080 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testsnew) step pytest_new 1200 python -u -m pytest tests/test_gpu_delivery.py tests/test_gpu_fullsize.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     testslog) step pytest_log 600 python -u -m pytest tests/test_gpu_log_layout.py tests/test_gpu_peer_group.py tests/test_gpu_bench_protocol.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    testsuni) step pytest_uni 600 python -u -m pytest tests/test_gpu_log_layout.py tests/test_gpu_uniform_rows.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    gm_um) step gm_um4 600 python tools/group_model.py --workload c4 --ranks 4 --kinds targets --target-option uni_merge=2 --json $OUT/group_model_c4_um4.json && \
+           step gm_um8 600 python tools/group_model.py --workload c4 --ranks 8 --kinds targets --target-option uni_merge=4 --json $OUT/group_model_c4_um8.json && \
+           step gm_um8t16 600 python tools/group_model.py --workload c4 --ranks 8 --kinds targets --target-option tiles_per_wave=16 --json $OUT/group_model_c4_t16.json ;;
     peers) step pytest_peers 900 python -u -m pytest tests/test_gpu_peer_group.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gm_c4) step gm_c4 900 python tools/group_model.py --workload c4 --variant nomask:peer_mask=0 --variant tpw16:tiles_per_wave=16 --variant nomask_tpw16:peer_mask=0,tiles_per_wave=16 --json $OUT/group_model_c4.json ;;
     gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --variant nomask:peer_mask=0 --json $OUT/group_model_c4p.json ;;
