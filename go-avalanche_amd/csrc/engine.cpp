@@ -230,6 +230,7 @@ struct av_engine {
   bool peer_mask = true;
   bool push_defer = true;          // option "push_defer": sweep pushes queued per wave (RoundParams::push_q)
   uint32_t push_store = 1;         // option "push_store" (RoundParams::push_store)
+  uint32_t mat_run = 1;            // option "materialize_run" (RoundParams::mat_run, A/B)
   bool masked = false;             // set up by the exchange's initialisation (mask_setup)
   uint32_t segs = 1;               // 32-word segments per row
   uint8_t* need_mine = nullptr;    // [kNeedWin][N]: rows this rank's nodes draw in a window's rounds
@@ -353,6 +354,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.ablate_emit = (uint32_t)e->ablate_emit;
   p.ablate_phase = e->ablate_phase;
   p.ablate_node = e->ablate_node;
+  p.mat_run = e->mat_run;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
   p.log_shards = e->log_shards;
@@ -2381,6 +2383,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     if (!value) e->fresh = false;
   } else if (n == "push_defer") {  // A/B: 0 = every push stored from the tile loop
     e->push_defer = value != 0;
+  } else if (n == "materialize_run") {  // A/B: tiles per wave of the deferred state's write-back
+    AV_CHECK(value >= 1 && value <= 64, AV_ERR_INVALID_ARG, "materialize_run must be 1..64");
+    e->mat_run = (uint32_t)value;
   } else if (n == "push_store") {  // A/B: 1 = plain stores (default), 0 = system scope, 2 = none (results invalid)
     AV_CHECK(value >= 0 && value <= 2, AV_ERR_INVALID_ARG, "push_store must be 0, 1 or 2");
     e->push_store = (uint32_t)value;

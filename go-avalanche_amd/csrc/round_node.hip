@@ -432,6 +432,13 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
 #ifndef AVK_REPLAY_LATE_REFILL
 #define AVK_REPLAY_LATE_REFILL 0
 #endif
+// A/B knob: the StatusUpdate pipeline's depth (k = 8): 1 = round r's entries stored in round r + 1
+// (two pending sets), 2 = in round r + 2 (four sets, loop unrolled four times), so that the wait for
+// the reserving atomic's result (vmcnt counts in issue order: also every load and store issued before
+// it) is for operations two rounds old
+#ifndef AVK_REPLAY_EMIT_DEPTH
+#define AVK_REPLAY_EMIT_DEPTH 1
+#endif
 template <int K, bool NT>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_replay_fast(const RoundParams p) {
   __shared__ uint32_t wmax[2];
@@ -588,8 +595,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       // store of round r - 1's entries below (which waits for round r - 1's atomic: vmcnt counts in
       // issue order) does not also wait for the votes of round r + 1, loaded after that atomic
       if (AVK_REPLAY_LATE_REFILL) refill();
-      if (r > 0u)
-        emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Ep, Ap, 0u, pp, p.round_rel + r - 1u);
+      if (r >= (uint32_t)AVK_REPLAY_EMIT_DEPTH)
+        emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Ep, Ap, 0u, pp,
+                                     p.round_rel + r - (uint32_t)AVK_REPLAY_EMIT_DEPTH);
       Ac = A;
     } else {
       (void)pc;
@@ -601,6 +609,28 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
     return true;
   };
+#if AVK_REPLAY_EMIT_DEPTH == 2
+  // four pending sets: round r reserves into set r % 4 and stores set (r - 2) % 4; the replayed-vote
+  // buffers keep alternating (r % 2)
+  EmitRes pendC{}, pendD{};
+  uint32_t EpC[K], EpD[K], ApC = 0u, ApD = 0u;
+  for (uint32_t r = 0; r < R; r += 4u) {
+    if (!step(r, wb0, pendA, EpA, ApA, pendC, EpC, ApC)) break;
+    if (r + 1u >= R || !step(r + 1u, wb1, pendB, EpB, ApB, pendD, EpD, ApD)) break;
+    if (r + 2u >= R || !step(r + 2u, wb0, pendC, EpC, ApC, pendA, EpA, ApA)) break;
+    if (r + 3u >= R || !step(r + 3u, wb1, pendD, EpD, ApD, pendB, EpB, ApB)) break;
+  }
+  if constexpr (K == 8) {  // the last two rounds run's entries (rounds done - 2, done - 1)
+    for (uint32_t q = done >= 2u ? done - 2u : 0u; q < done; ++q) {
+      const uint32_t sset = q & 3u;
+      const uint32_t rk = p.round_rel + q;
+      if (sset == 0u) emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpA, ApA, 0u, pendA, rk);
+      else if (sset == 1u) emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpB, ApB, 0u, pendB, rk);
+      else if (sset == 2u) emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpC, ApC, 0u, pendC, rk);
+      else emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpD, ApD, 0u, pendD, rk);
+    }
+  }
+#else
   for (uint32_t r = 0; r < R; r += 2u) {
     if (!step(r, wb0, pendA, EpA, ApA, pendB, EpB, ApB)) break;
     if (r + 1u >= R || !step(r + 1u, wb1, pendB, EpB, ApB, pendA, EpA, ApA)) break;
@@ -612,6 +642,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
                      : emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpA, ApA, 0u, pendA, p.round_rel + done - 1u);
     }
   }
+#endif
   if (done < R && b == 0) p.node_flags[nl] = done + 1u;  // the exact pass takes rounds done..R-1
   if (done > 0u) {
     pst4<NT>(grp, u32x4{V[0], V[1], V[2], V[3]});

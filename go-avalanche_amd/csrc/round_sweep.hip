@@ -1426,14 +1426,94 @@ __global__ __launch_bounds__(256) void k_kl_materialize(const RoundParams p) {
 }
 
 // Both deferred forms written back in one pass (do_v: stale vote planes and unstored consider planes,
-// as k_vv_materialize; do_k: pending count steps and virtual K4..K7 groups, as k_kl_materialize), a
-// wave walking a run of `run` consecutive tiles: the run's tile words are loaded one lane per tile and
-// tested with v_readlane, so a wave pays its set-up once per run and a tile with nothing deferred costs
-// no memory access (one wave per tile left most waves with nothing to do but their launch).
+// as k_vv_materialize; do_k: pending count steps and virtual K4..K7 groups, as k_kl_materialize).
+// Per tile every load (A for a uniform vote register, the K groups, a stale tile's peer rows) is issued
+// before any store: vmcnt counts loads and stores in issue order, so a load issued after the tile's
+// consider-plane stores waited for their write acknowledgements too (round 5's walking version paid
+// that per tile, 16 tiles in a row per wave: ~5 TB/s at C4's segment end). A wave takes `run`
+// consecutive tiles (default 1: the memory system hides each tile's round trip behind other waves').
+__device__ __forceinline__ void materialize_tile(const RoundParams& p, uint32_t tile, uint32_t lane, uint32_t raw,
+                                                 uint32_t kw) {
+  const LaneIdx x = lane_idx(p, tile, lane);
+  uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
+  u32x4* const grp = reinterpret_cast<u32x4*>(tp) + lane;
+  const uint32_t st = raw & kVMask;
+  const uint32_t pend = kw & 0xFFu;
+  const bool dok = (pend || (kw & kHiVirt)) && x.active;
+  // ---- loads
+  u32x4 o0, o1, k0, k1;
+  if (st == kVUniform) {  // V_i = A on every polled record
+    const uint32_t A = tp[1536u + lane];
+    o0 = o1 = u32x4{A, A, A, A};
+  } else if (st) {  // the last round's 8 gathered votes, V_i = slot 7 - i
+    const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
+    uint32_t pp[8];
+    draw_peers<8>(p, p.round - 1u, x.node, x.nl, nlA, nn, lane, pp);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      o0[c] = p.pref_prev[pp[7 - c] * p.PS + x.b];
+      o1[c] = p.pref_prev[pp[3 - c] * p.PS + x.b];
+    }
+  }
+  uint32_t vb = 0u;
+  if (dok) {
+    k0 = grp[128];
+    k1 = kw & kHiVirt ? u32x4{0u, 0u, 0u, ~real_mask(p.tn, x.b)} : grp[192];  // kernels.h kHiVirt
+    vb = p.valid[x.b];
+  }
+  // ---- stores
+  if ((raw & kCAll) && x.active) {  // consider planes: all-ones
+#pragma unroll
+    for (int c = 0; c < 8; ++c) tp[1024u + (uint32_t)c * 64u + lane] = ~0u;
+  }
+  if (st && x.active) {
+    grp[0] = o0;
+    grp[64] = o1;
+  }
+  if (dok) {  // + 8 * pend on the polled records' counts
+    uint32_t Kp[8];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      Kp[c] = k0[c];
+      Kp[4 + c] = k1[c];
+    }
+    const uint32_t P0 = ~Kp[7] & vb;
+    uint32_t cy = 0u;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {  // + pend on count bits 3..6
+      const uint32_t bi = ((pend >> c) & 1u) ? P0 : 0u;
+      const uint32_t t = Kp[3 + c] ^ bi;
+      const uint32_t si = t ^ cy;
+      cy = (t & cy) | (Kp[3 + c] & bi);
+      Kp[3 + c] = si;
+    }
+    u32x4 o2, o3;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      o2[c] = Kp[c];
+      o3[c] = Kp[4 + c];
+    }
+    grp[128] = o2;
+    grp[192] = o3;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_materialize(const RoundParams p, uint32_t run, uint32_t do_v, uint32_t do_k) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = uni(blockIdx.x * 4u + (threadIdx.x >> 6));
   const uint32_t tiles = p.Lpad >> 6;
+  if (run == 1u) {  // the tile words as scalar loads (the tile index is wave-uniform)
+    if (wave >= tiles) return;
+    const uint32_t raw = do_v ? uni(p.vstale[wave]) : 0u;
+    const uint32_t kw = do_k ? uni(p.kpend[wave]) : 0u;
+    if (raw == 0u && kw == 0u) return;
+    materialize_tile(p, wave, lane, raw, kw);
+    if (lane == 0) {
+      if (raw) p.vstale[wave] = 0u;
+      if (kw) p.kpend[wave] = 0u;
+    }
+    return;
+  }
   const uint32_t t0 = wave * run;
   if (t0 >= tiles) return;
   const uint32_t n = min(run, tiles - t0);
@@ -1445,66 +1525,7 @@ __global__ __launch_bounds__(256) void k_materialize(const RoundParams p, uint32
     const uint32_t raw = (uint32_t)__builtin_amdgcn_readlane((int)stw, (int)i);
     const uint32_t kw = (uint32_t)__builtin_amdgcn_readlane((int)kww, (int)i);
     if (raw == 0u && kw == 0u) continue;
-    const uint32_t tile = t0 + i;
-    const LaneIdx x = lane_idx(p, tile, lane);
-    uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
-    u32x4* const grp = reinterpret_cast<u32x4*>(tp) + lane;
-    if (raw) {
-      const uint32_t st = raw & kVMask;
-      if ((raw & kCAll) && x.active) {  // consider planes: all-ones
-#pragma unroll
-        for (int c = 0; c < 8; ++c) tp[1024u + (uint32_t)c * 64u + lane] = ~0u;
-      }
-      if (st) {
-        u32x4 o0, o1;
-        if (st == kVUniform) {  // V_i = A on every polled record
-          const uint32_t A = tp[1536u + lane];
-          o0 = o1 = u32x4{A, A, A, A};
-        } else {  // the last round's 8 gathered votes, V_i = slot 7 - i
-          const uint32_t nlA = uni(x.nl), nn = (uint32_t)__builtin_amdgcn_readlane((int)x.nl, 63) - nlA + 1u;
-          uint32_t pp[8];
-          draw_peers<8>(p, p.round - 1u, x.node, x.nl, nlA, nn, lane, pp);
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            o0[c] = p.pref_prev[pp[7 - c] * p.PS + x.b];
-            o1[c] = p.pref_prev[pp[3 - c] * p.PS + x.b];
-          }
-        }
-        if (x.active) {
-          grp[0] = o0;
-          grp[64] = o1;
-        }
-      }
-    }
-    const uint32_t pend = kw & 0xFFu;
-    if ((pend || (kw & kHiVirt)) && x.active) {  // + 8 * pend on the polled records' counts
-      const u32x4 k0 = grp[128];
-      const u32x4 k1 = kw & kHiVirt ? u32x4{0u, 0u, 0u, ~real_mask(p.tn, x.b)} : grp[192];  // kernels.h kHiVirt
-      uint32_t Kp[8];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        Kp[c] = k0[c];
-        Kp[4 + c] = k1[c];
-      }
-      const uint32_t P0 = ~Kp[7] & p.valid[x.b];
-      uint32_t cy = 0u;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {  // + pend on count bits 3..6
-        const uint32_t bi = ((pend >> c) & 1u) ? P0 : 0u;
-        const uint32_t t = Kp[3 + c] ^ bi;
-        const uint32_t si = t ^ cy;
-        cy = (t & cy) | (Kp[3 + c] & bi);
-        Kp[3 + c] = si;
-      }
-      u32x4 o2, o3;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        o2[c] = Kp[c];
-        o3[c] = Kp[4 + c];
-      }
-      grp[128] = o2;
-      grp[192] = o3;
-    }
+    materialize_tile(p, t0 + i, lane, raw, kw);
   }
   if (lane < n) {
     if (stw) p.vstale[ti] = 0u;
@@ -1550,7 +1571,7 @@ hipError_t launch_vv_materialize(const RoundParams& p, hipStream_t s) {
 hipError_t launch_materialize(const RoundParams& p, bool do_v, bool do_k, hipStream_t s) {
   if ((do_v && (!p.vstale || !p.pref_prev)) || (do_k && !p.kpend)) return hipErrorInvalidValue;
   if (!do_v && !do_k) return hipSuccess;
-  constexpr uint32_t run = 16u;
+  const uint32_t run = p.mat_run ? p.mat_run : 1u;
   const uint32_t tiles = p.Lpad / 64u;
   const uint32_t waves = (tiles + run - 1u) / run;
   hipLaunchKernelGGL(k_materialize, dim3((waves + 3u) / 4u), dim3(256), 0, s, p, run, do_v ? 1u : 0u, do_k ? 1u : 0u);

@@ -119,12 +119,15 @@ def test_changed_words_match_host_diff(case):
     e.close()
 
 
-def test_materialize_leaves_results_unchanged(oracle):
+@pytest.mark.parametrize("run", [1, 4, 16])
+def test_materialize_leaves_results_unchanged(oracle, run):
     """av_materialize in the middle of a deferred stretch (stale vote planes,
     pending count steps): records, digests and every later round identical to
-    an engine that never wrote back, and to the oracle."""
+    an engine that never wrote back, and to the oracle; k_materialize taking 1,
+    4 or 16 tiles per wave (option materialize_run)."""
     n, m = 2000, 1000
     a = avhip.Engine(n, m, k=8, seed=5, log_capacity=1 << 24)
+    a.set_option("materialize_run", run)
     b = avhip.Engine(n, m, k=8, seed=5, log_capacity=1 << 24)
     sim = oracle.Sim(n, m, 8, seed=5, init_mode=avhip.INIT_BERNOULLI, init_param=P80)
     for x in (a, b):

@@ -35,6 +35,11 @@ for s in "$@"; do
     gm_um) step gm_um4 600 python tools/group_model.py --workload c4 --ranks 4 --kinds targets --target-option uni_merge=2 --json $OUT/group_model_c4_um4.json && \
            step gm_um8 600 python tools/group_model.py --workload c4 --ranks 8 --kinds targets --target-option uni_merge=4 --json $OUT/group_model_c4_um8.json && \
            step gm_um8t16 600 python tools/group_model.py --workload c4 --ranks 8 --kinds targets --target-option tiles_per_wave=16 --json $OUT/group_model_c4_t16.json ;;
+    wbprobe) step wbprobe 600 python tools/wb_probe.py --json $OUT/wb_probe.json ;;
+    ab_c2emit) step ab_c2emit 600 bash -c 'for i in 1 2 3; do for v in default late emit2 emit2late; do echo "== $v"; if [ $v = default ]; then python tools/fuse_probe.py | head -1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py | head -1; fi; done; done' ;;
+    gm_t16) step gm_t16_c4 600 python tools/group_model.py --workload c4 --ranks 4,8 --kinds targets --target-option tiles_per_wave=16 --json $OUT/gm_t16_c4.json && \
+            step gm_t16_c4p 600 python tools/group_model.py --workload c4p --ranks 4,8 --kinds targets --target-option tiles_per_wave=16 --json $OUT/gm_t16_c4p.json && \
+            step gm_t16_c4pb 600 python tools/group_model.py --workload c4pb --ranks 4,8 --kinds targets --target-option tiles_per_wave=16 --json $OUT/gm_t16_c4pb.json ;;
     peers) step pytest_peers 900 python -u -m pytest tests/test_gpu_peer_group.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gm_c4) step gm_c4 900 python tools/group_model.py --workload c4 --variant nomask:peer_mask=0 --variant tpw16:tiles_per_wave=16 --variant nomask_tpw16:peer_mask=0,tiles_per_wave=16 --json $OUT/group_model_c4.json ;;
     gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --variant nomask:peer_mask=0 --json $OUT/group_model_c4p.json ;;
