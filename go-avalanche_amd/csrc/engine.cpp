@@ -230,6 +230,7 @@ struct av_engine {
   bool peer_mask = true;
   bool push_defer = true;          // option "push_defer": sweep pushes queued per wave (RoundParams::push_q)
   uint32_t push_store = 1;         // option "push_store" (RoundParams::push_store)
+  uint32_t tile_draw = 1;          // option "tile_draw" (RoundParams::tile_draw, A/B)
   uint32_t mat_run = 1;            // option "materialize_run" (RoundParams::mat_run, A/B)
   bool masked = false;             // set up by the exchange's initialisation (mask_setup)
   uint32_t segs = 1;               // 32-word segments per row
@@ -355,6 +356,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.ablate_phase = e->ablate_phase;
   p.ablate_node = e->ablate_node;
   p.mat_run = e->mat_run;
+  p.tile_draw = e->tile_draw;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
   p.log_shards = e->log_shards;
@@ -2383,6 +2385,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     if (!value) e->fresh = false;
   } else if (n == "push_defer") {  // A/B: 0 = every push stored from the tile loop
     e->push_defer = value != 0;
+  } else if (n == "tile_draw") {  // A/B: per-tile shared peer draws in runs whose nodes overflow the run's draw
+    AV_CHECK(value == 0 || value == 1, AV_ERR_INVALID_ARG, "tile_draw must be 0 or 1");
+    e->tile_draw = (uint32_t)value;
   } else if (n == "materialize_run") {  // A/B: tiles per wave of the deferred state's write-back
     AV_CHECK(value >= 1 && value <= 64, AV_ERR_INVALID_ARG, "materialize_run must be 1..64");
     e->mat_run = (uint32_t)value;

@@ -171,6 +171,7 @@ struct RoundParams {
   // sweep's waves each take at most kPushQ tiles and push_n <= 8 (a byte per lane and tile)
   uint32_t push_q;
   uint32_t push_defer;  // engine option "push_defer" (default 1): the sweep may queue its pushes (push_q)
+  uint32_t tile_draw;   // engine option "tile_draw": per-tile shared draws in runs that overflow the run's draw
   uint32_t mat_run;     // engine option "materialize_run": tiles per wave of k_materialize (0 = 1)
   uint32_t push_store;  // engine option "push_store": 1 = plain stores (default), 0 = system scope, 2 = none (diagnostics)
   // Deferred count planes (`kl`, k = 8, warm sim rounds in which no record can

@@ -1092,6 +1092,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     wd.fofs = 0u;
     uint32_t uni_done = 0u;  // uniform rows: run tiles settled with no draw (settled_run_uni)
     bool uni_ran = false;
+    __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][512];
+    uint32_t* const sd = s_draw[threadIdx.x >> 6];
     if constexpr (MODE == kModeWarm && K == 8) {
       if (p.tpw) {
         // a run of p.tpw consecutive tiles per wave; one Philox pass draws the
@@ -1125,8 +1127,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
             uni_ran = true;
           }
           const bool any_stale = __ballot((st & kVMask) == kVStale) != 0ull;
-          __shared__ __attribute__((aligned(16))) uint32_t s_draw[4][512];
-          uint32_t* const sd = s_draw[threadIdx.x >> 6];
           if (uni_done != all_tiles) {
             wd.pair = any_stale;
             wd.flagok = 0ull;
@@ -1177,12 +1177,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     }
     const uint32_t qfirst = tile, qstep = stride;  // deferred pushes: slot s = tile qfirst + s * qstep
     uint32_t qn = 0;
+    // tile draws (p.tile_draw): a run whose nodes overflow the run's draw (narrow rows: at BL <= 16 a
+    // 16-tile run holds 64-256 nodes) still shares one Philox pass per tile, 2 producer lanes per
+    // node (a tile's 64 / BL nodes fit: BL >= 2, or >= 4 with a stale tile's paired draw), instead of
+    // every lane drawing its node's 8 peers alone (4-16 lanes per node repeating the same draw)
+    const bool tdraw = MODE == kModeWarm && K == 8 && p.tile_draw && p.tpw && !wd.ok && tile < tile_end;
     for (; tile < tile_end; tile += stride) {
       constexpr bool AB = MODE == kModeAblate;
       if constexpr (CC) acc.qslot = qn++;
       if constexpr (MODE == kModeWarm) {
         if constexpr (K == 8) {
           if (lean_done && ((lean_done >> (tile - wd.t0)) & 1u)) continue;
+          if (tdraw) {
+            const uint32_t tnlA = uni(div_bl(p, tile * 64u));
+            const uint32_t tnn = uni(div_bl(p, min(tile * 64u + 64u, p.L) - 1u)) - tnlA + 1u;
+            const bool tst = ((meta_of(wd, tile) >> 8) & kVMask) == kVStale;  // wave-uniform
+            const PairDraw d = tst ? pair_draw(p, p.round, tnlA, tnn, lane) : single_draw(p, p.round, tnlA, tnn, lane);
+            wd.ok = !d.fallback;
+            if (wd.ok) {
+              park_draw(d, sd, lane, p.PS * 4u);
+              wd.nlA = tnlA;
+              wd.nn = tnn;
+              wd.pair = tst;
+              wd.sdp = sd;
+              wd.sdc = tst ? sd + 128 : sd;
+              wd.badp = d.bad & 0xFFFFFFFFull;
+              wd.badc = tst ? d.bad >> 32 : d.bad;
+              wd.fofs = tst ? 32u : 0u;
+              wd.flagok = 0ull;
+            }
+          }
           if (wd.ok && p.settled_fast && p.klazy && p.vv && !lean_ran) {
             const uint32_t m = meta_of(wd, tile);
             if (((m >> 8) & kVMask) == kVUniform && (m & kPendAllLive) &&

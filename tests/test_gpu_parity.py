@@ -495,12 +495,14 @@ def test_target_shard_identity_8way():
     assert full.finalized_count() == sum(p.finalized_count() for p in parts) > 0
 
 
-@pytest.mark.parametrize("g", [2, 4, 8])
-def test_target_shard_runs(g):
+@pytest.mark.parametrize("g,tpw,tile_draw", [(2, 16, 1), (4, 8, 1), (8, 4, 1), (4, 16, 1), (8, 16, 1), (8, 16, 0),
+                                              (2, 16, 0)])
+def test_target_shard_runs(g, tpw, tile_draw):
     """G target shards of a C4-shaped network (BL = 16 / 8 / 4 lanes per node)
-    with the tiles-per-wave the engine picks for that BL at full size
-    (engine.cpp default_sweep_blocks: 16 / 8 / 4, one 64-lane draw per run) ==
-    one engine, bit for bit, through the settled rounds and finalization."""
+    with runs of tpw tiles per wave (a run of 64 * tpw / BL nodes: past 32 the
+    run's draw falls back to per-tile draws, shared by 2 producer lanes per node
+    with option tile_draw, else one draw per lane) == one engine, bit for bit,
+    through the settled rounds and finalization."""
     n, m, k, R = 20_000, 1000, 8, 20
     full = avhip.Engine(n, m, k=k, seed=77, log_capacity=1 << 24)
     full.init_records(avhip.INIT_BERNOULLI, P80)
@@ -508,7 +510,8 @@ def test_target_shard_runs(g):
     parts = []
     for r in range(g):
         p = avhip.Engine(n, m, k=k, seed=77, target_range=sharding.target_shard(m, g, r), log_capacity=1 << 23)
-        p.set_option("tiles_per_wave", {2: 16, 4: 8, 8: 4}[g])
+        p.set_option("tiles_per_wave", tpw)
+        p.set_option("tile_draw", tile_draw)
         p.init_records(avhip.INIT_BERNOULLI, P80)
         parts.append(p)
     for r in range(R):

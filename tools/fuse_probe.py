@@ -46,20 +46,25 @@ def main():
     ap.add_argument("--rounds", type=int, default=11)
     ap.add_argument("--first", type=int, default=5, help="untimed rounds before the timed batch")
     ap.add_argument("--option", action="append", default=[])
+    ap.add_argument("--repeat", type=int, default=1, help="measured batches (the median is reported)")
+    ap.add_argument("--fuse", default="16,0", help="replay_fuse values")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[args.workload]
     out = []
-    for fuse in (16, 0):
+    for fuse in [int(x) for x in args.fuse.split(",")]:
         e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4, byz_threshold=byz, log_capacity=min(n * m // 2 + (1 << 20), 1 << 31))
         e.set_option("replay_fuse", fuse)
         for o in args.option:
             name, v = o.split("=")
             e.set_option(name, int(v))
         epoch(e, init_mode, init_param, args.rounds, args.first)  # warm-up
-        r = epoch(e, init_mode, init_param, args.rounds, args.first)
-        r.update({"fuse": fuse, "options": args.option, "rounds": args.rounds,
-                  "kernel_ms_per_round": r["kernel_ms"] / args.rounds})
+        reps = [epoch(e, init_mode, init_param, args.rounds, args.first) for _ in range(args.repeat)]
+        reps.sort(key=lambda x: x["kernel_ms"])
+        r = dict(reps[len(reps) // 2])  # the median batch
+        r.update({"fuse": fuse, "options": args.option, "rounds": args.rounds, "repeat": args.repeat,
+                  "kernel_ms_per_round": r["kernel_ms"] / args.rounds,
+                  "kernel_ms_per_round_all": [x["kernel_ms"] / args.rounds for x in reps]})
         print(json.dumps(r), flush=True)
         out.append(r)
         e.close()
