@@ -392,6 +392,15 @@ def window_segments(warmup, steps):
     return segs
 
 
+def compact_delivery(d):
+    """The delivery measurement in the line: StatusUpdates per second consumed on the device
+    (av_updates_digest) and fetched to the host (pageable / pinned destination), and the vote-record
+    updates per second of rounds 0-3 with every round's updates fetched into pinned memory."""
+    return {"digest_updates_per_s": d["digest_updates_per_s"],
+            "fetch_updates_per_s": {"pageable": d["pageable"]["updates_per_s"], "pinned": d["pinned"]["updates_per_s"]},
+            "votes_per_s_with_fetch": d["pinned"]["delivered_votes_per_s"]}
+
+
 def size_log(eng, per_round, warmup, steps):
     """Log entries per kind for the largest timed segment (the warm-up epoch's per-round counts
     summed over the segment's rounds, 1.3x + 64 per shard of slack), in place of the worst case per
@@ -468,31 +477,53 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     delivery = None
     if world == 1 and not replay and not args.no_roofline_pass:  # (before the roofline pass, which
         # must stay the process's last round-kernel dispatches for tools/pmc_bench.py)
-        run.goto(0)
         rows = []
-        buf = None
-        a0 = eng.applied_votes()
-        for _ in range(4):
-            rnd = run.pos % EPOCH
-            eng.synchronize()
-            t0 = time.perf_counter()
-            eng.run_rounds(1)
-            eng.synchronize()
-            t1 = time.perf_counter()
-            nu = eng.updates_count()
-            if buf is None or buf.size < nu:
-                buf = np.empty(max(nu, 1), np.uint64)
-            got = eng.fetch_into(buf)
-            t2 = time.perf_counter()
-            run.pos += 1
-            rows.append({"round": rnd, "updates": got, "round_ms": (t1 - t0) * 1e3, "fetch_ms": (t2 - t1) * 1e3})
-        upd = sum(r["updates"] for r in rows)
-        ms = sum(r["round_ms"] + r["fetch_ms"] for r in rows)
-        delivery = {"rounds": rows, "updates": upd, "ms": ms,
-                    "delivered_updates_per_s": (eng.applied_votes() - a0) / (ms * 1e-3),
-                    "status_updates_per_s": upd / (sum(r["fetch_ms"] for r in rows) * 1e-3),
-                    "note": "round + av_fetch_updates (device expansion, canonical radix sort, copy into pageable "
-                            "host memory through pinned staging) per round, wall clock"}
+        for dest in ("pageable", "pinned"):
+            run.goto(0)
+            buf = None
+            for _ in range(4):
+                rnd = run.pos % EPOCH
+                eng.synchronize()
+                a0 = eng.applied_votes()
+                t0 = time.perf_counter()
+                eng.run_rounds(1)
+                eng.synchronize()
+                t1 = time.perf_counter()
+                nu = eng.updates_count()
+                # the on-device consumer: av_updates_digest folds every pending update (all three
+                # record kinds) in device memory, nothing crosses PCIe
+                eng.updates_digest()
+                t1d = time.perf_counter()
+                if buf is None or buf.size < nu:
+                    if dest == "pinned":
+                        buf = torch.empty(max(nu, 1), dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
+                    else:
+                        buf = np.empty(max(nu, 1), np.uint64)
+                got = eng.fetch_into(buf)
+                t2 = time.perf_counter()
+                run.pos += 1
+                rows.append({"dest": dest, "round": rnd, "updates": got, "applied": eng.applied_votes() - a0,
+                             "round_ms": (t1 - t0) * 1e3,
+                             "digest_ms": (t1d - t1) * 1e3, "fetch_ms": (t2 - t1d) * 1e3})
+            buf = None
+
+        def rate(dest):
+            rs = [r for r in rows if r["dest"] == dest]
+            upd = sum(r["updates"] for r in rs)
+            ms = sum(r["round_ms"] + r["fetch_ms"] for r in rs)
+            return {"updates": upd, "ms": ms, "updates_per_s": upd / (sum(r["fetch_ms"] for r in rs) * 1e-3),
+                    "GB_per_s": 8.0 * upd / (sum(r["fetch_ms"] for r in rs) * 1e-3) / 1e9,
+                    "delivered_votes_per_s": sum(r["applied"] for r in rs) / (ms * 1e-3)}
+        pg, pn = rate("pageable"), rate("pinned")
+        dg = [r for r in rows if r["dest"] == "pageable"]
+        delivery = {"rounds": rows, "pageable": pg, "pinned": pn,
+                    "delivered_updates_per_s": pg["delivered_votes_per_s"],
+                    "status_updates_per_s": pg["updates_per_s"],
+                    "digest_updates_per_s": sum(r["updates"] for r in dg) / (sum(r["digest_ms"] for r in dg) * 1e-3),
+                    "note": "per round (rounds 0-3 of a fresh epoch), wall clock: the round; av_updates_digest (the "
+                            "on-device consumer); av_fetch_updates (device expansion, canonical radix sort, copy "
+                            "to the host: 8 B per update) into pageable memory (through pinned staging) or "
+                            "straight into a pinned buffer (one DMA)"}
     # ---- roofline pass: the same steps again, every round's kernels bracketed
     # by HIP events on the engine's stream; sim rounds one step at a time so
     # that every round's kernel time, model bytes and re-read bytes are known
@@ -850,6 +881,8 @@ def main(argv=None):
                                  "frac": rf["frac"] if rf else None, "binding": rf.get("binding") if rf else None}
                 if sr["writeback_ms"] is not None:
                     secondary[wl]["writeback_ms"] = sr["writeback_ms"]
+                if sr["delivery"]:
+                    secondary[wl]["delivery"] = compact_delivery(sr["delivery"])
                 if world > 1:
                     secondary[wl]["replicas_identical"] = sr["replicas_identical"]
                     secondary[wl]["shard"] = sr["shard"]
@@ -898,6 +931,8 @@ def main(argv=None):
             "log_gb": r["log_bytes"] / 1e9 if r["log_bytes"] else None,
             "detail": os.path.relpath(args.detail, ROOT),
         }
+        if r["delivery"]:
+            line["delivery"] = compact_delivery(r["delivery"])
         if r["replicas_identical"] is not None:
             line["config"]["replicas_identical"] = r["replicas_identical"]
         if r.get("shard_fallback"):

@@ -230,7 +230,7 @@ struct av_engine {
   bool peer_mask = true;
   bool push_defer = true;          // option "push_defer": sweep pushes queued per wave (RoundParams::push_q)
   uint32_t push_store = 1;         // option "push_store" (RoundParams::push_store)
-  uint32_t tile_draw = 1;          // option "tile_draw" (RoundParams::tile_draw, A/B)
+  uint32_t tile_draw = 0;          // option "tile_draw" (RoundParams::tile_draw, A/B)
   uint32_t mat_run = 1;            // option "materialize_run" (RoundParams::mat_run, A/B)
   bool masked = false;             // set up by the exchange's initialisation (mask_setup)
   uint32_t segs = 1;               // 32-word segments per row
@@ -897,7 +897,14 @@ uint32_t default_sweep_blocks(const av_engine* e, bool force = false) {
   // (tools/shard_model.py, profiles/r04/tshard_c4_*.json, rank 0's settled rounds): BL 16 (G = 2)
   // 0.083 ms at 4 tiles per wave, 0.038 at 16; BL 8 (G = 4) 0.046 at 4, 0.031 at 8, 0.166 at 16 (the
   // run's nodes overflow the draw); BL 4 (G = 8) 0.027 at 4, 0.124 at 8.
+  // Narrow rows (BL <= 8: C5, the target shards of C4 at 4 and 8 ranks): a run's nodes overflow the
+  // draw at any length >= BL / 2, so every tile draws its own peers whatever the run, and the longest
+  // run pays the per-wave set-up least; the uniform settled runs take up to 256 nodes (settled_run_uni).
+  // Round 5 (tools/group_model.py, profiles/r05/s11/gm_td16_*.log; tools/round_probe.py, ab_c5td.log):
+  // C4 rank 0 at G = 8 window 1.545 -> 1.309 ms, G = 4 2.078 -> 1.955, C5 epoch 17.2 -> 16.2 ms, C4p /
+  // C4pb within 1 %.
   uint64_t tpw = e->tiles_per_wave;
+  if (!tpw && e->BL <= 8) tpw = 16;
   if (!tpw) {
     tpw = 16;
     while (tpw > 4 && (tpw > (uint64_t)e->BL || tiles / tpw < 15000)) tpw /= 2;

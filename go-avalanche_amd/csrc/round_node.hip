@@ -436,8 +436,20 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
 // (two pending sets), 2 = in round r + 2 (four sets, loop unrolled four times), so that the wait for
 // the reserving atomic's result (vmcnt counts in issue order: also every load and store issued before
 // it) is for operations two rounds old
+// A/B knob: the near-finalization check (a workgroup barrier) every round instead of from round J on
+#ifndef AVK_REPLAY_ALWAYS_CHECK
+#define AVK_REPLAY_ALWAYS_CHECK 0
+#endif
+#ifndef AVK_REPLAY_VMWAIT
+#define AVK_REPLAY_VMWAIT 0
+#endif
+#ifndef AVK_REPLAY_BUF3
+#define AVK_REPLAY_BUF3 0
+#endif
+// (round 5, tools/fuse_probe.py --repeat 15, three alternations on one box: depth 2 3.52-3.53 us per
+// round against 3.69-3.73 at depth 1; profiles/r05/s11/ab_c2e.log)
 #ifndef AVK_REPLAY_EMIT_DEPTH
-#define AVK_REPLAY_EMIT_DEPTH 1
+#define AVK_REPLAY_EMIT_DEPTH 2
 #endif
 template <int K, bool NT>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_replay_fast(const RoundParams p) {
@@ -527,9 +539,11 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   EmitRes pendA{}, pendB{};
   uint32_t EpA[K], EpB[K], ApA = 0u, ApB = 0u;
   const uint32_t shard = wave_id % p.log_shards;  // once (a runtime modulo is a long sequence)
-  auto step = [&](uint32_t r, u32x4 (&wb)[RQ], EmitRes& pc, uint32_t (&Ec)[K], uint32_t& Ac,
+  // wb: this round's replayed votes; nb: the buffer refilled with round r + 2's (wb itself with two
+  // buffers; with three (AVK_REPLAY_BUF3) the one read last round, whose registers are free)
+  auto step = [&](uint32_t r, u32x4 (&wb)[RQ], u32x4 (&nb)[RQ], EmitRes& pc, uint32_t (&Ec)[K], uint32_t& Ac,
                   const EmitRes& pp, const uint32_t (&Ep)[K], uint32_t Ap) -> bool {
-    if (r >= J) {  // a record with count >= 120 may finalize (and leave the poll set) this round
+    if (AVK_REPLAY_ALWAYS_CHECK || r >= J) {  // a record with count >= 120 may finalize (and leave the poll set) this round
       const uint32_t nearfin = Kp[6] & Kp[5] & Kp[4] & Kp[3];
       if (__syncthreads_or(nearfin != 0u)) {  // workgroup-uniform
         done = r;
@@ -537,6 +551,15 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       }
     }
     uint32_t ys[7 + K], ns[7 + K], cv[K];
+#if AVK_REPLAY_VMWAIT
+    // this round's votes were loaded two rounds ago, and at least the RQ loads of last round's refill
+    // were issued after them: vmcnt(RQ) retires them (vmcnt counts in issue order). The compiler's own
+    // wait, which merges the loop's paths (stores and atomics in lane-conditional blocks), asked for
+    // vmcnt(0) here, i.e. for the refill just issued too: one memory latency per round
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt((RQ & 15) | (7 << 4) | (15 << 8) | ((RQ >> 4) << 14));
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const uint32_t wj = wb[j >> 1][(j & 1) * 2];
@@ -568,7 +591,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
     auto refill = [&]() {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < RQ; ++i) wb[i] = pld4<true>(rq + (size_t)min(r + 2u, R - 1u) * rstride + i * 64);
+      for (int i = 0; i < RQ; ++i) nb[i] = pld4<true>(rq + (size_t)min(r + 2u, R - 1u) * rstride + i * 64);
     };
     if (!(K == 8 && AVK_REPLAY_LATE_REFILL)) refill();
     // the round's update masks go straight into this round's pending set (no copy)
@@ -609,16 +632,43 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
     return true;
   };
-#if AVK_REPLAY_EMIT_DEPTH == 2
+#if AVK_REPLAY_BUF3
+  // three replayed-vote buffers and three pending sets, the loop unrolled three times: round r reads
+  // buffer r % 3 and refills buffer (r + 2) % 3 (read in round r - 1: its registers are dead, so the
+  // loads need no copy into the loop header's registers, which waited for them); it reserves into set
+  // r % 3 and stores set (r - depth) % 3
+  u32x4 wb2[RQ];
+  EmitRes pendC{};
+  uint32_t EpC[K], ApC = 0u;
+  constexpr bool D2 = AVK_REPLAY_EMIT_DEPTH == 2;
+  for (uint32_t r = 0; r < R; r += 3u) {
+    if (!(D2 ? step(r, wb0, wb2, pendA, EpA, ApA, pendB, EpB, ApB) : step(r, wb0, wb2, pendA, EpA, ApA, pendC, EpC, ApC))) break;
+    if (r + 1u >= R ||
+        !(D2 ? step(r + 1u, wb1, wb0, pendB, EpB, ApB, pendC, EpC, ApC) : step(r + 1u, wb1, wb0, pendB, EpB, ApB, pendA, EpA, ApA)))
+      break;
+    if (r + 2u >= R ||
+        !(D2 ? step(r + 2u, wb2, wb1, pendC, EpC, ApC, pendA, EpA, ApA) : step(r + 2u, wb2, wb1, pendC, EpC, ApC, pendB, EpB, ApB)))
+      break;
+  }
+  if constexpr (K == 8) {  // the last rounds run's entries (rounds done - depth .. done - 1)
+    for (uint32_t q = done >= (uint32_t)AVK_REPLAY_EMIT_DEPTH ? done - (uint32_t)AVK_REPLAY_EMIT_DEPTH : 0u; q < done; ++q) {
+      const uint32_t sset = q % 3u;
+      const uint32_t rk = p.round_rel + q;
+      if (sset == 0u) emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpA, ApA, 0u, pendA, rk);
+      else if (sset == 1u) emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpB, ApB, 0u, pendB, rk);
+      else emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpC, ApC, 0u, pendC, rk);
+    }
+  }
+#elif AVK_REPLAY_EMIT_DEPTH == 2
   // four pending sets: round r reserves into set r % 4 and stores set (r - 2) % 4; the replayed-vote
   // buffers keep alternating (r % 2)
   EmitRes pendC{}, pendD{};
   uint32_t EpC[K], EpD[K], ApC = 0u, ApD = 0u;
   for (uint32_t r = 0; r < R; r += 4u) {
-    if (!step(r, wb0, pendA, EpA, ApA, pendC, EpC, ApC)) break;
-    if (r + 1u >= R || !step(r + 1u, wb1, pendB, EpB, ApB, pendD, EpD, ApD)) break;
-    if (r + 2u >= R || !step(r + 2u, wb0, pendC, EpC, ApC, pendA, EpA, ApA)) break;
-    if (r + 3u >= R || !step(r + 3u, wb1, pendD, EpD, ApD, pendB, EpB, ApB)) break;
+    if (!step(r, wb0, wb0, pendA, EpA, ApA, pendC, EpC, ApC)) break;
+    if (r + 1u >= R || !step(r + 1u, wb1, wb1, pendB, EpB, ApB, pendD, EpD, ApD)) break;
+    if (r + 2u >= R || !step(r + 2u, wb0, wb0, pendC, EpC, ApC, pendA, EpA, ApA)) break;
+    if (r + 3u >= R || !step(r + 3u, wb1, wb1, pendD, EpD, ApD, pendB, EpB, ApB)) break;
   }
   if constexpr (K == 8) {  // the last two rounds run's entries (rounds done - 2, done - 1)
     for (uint32_t q = done >= 2u ? done - 2u : 0u; q < done; ++q) {
@@ -632,8 +682,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 #else
   for (uint32_t r = 0; r < R; r += 2u) {
-    if (!step(r, wb0, pendA, EpA, ApA, pendB, EpB, ApB)) break;
-    if (r + 1u >= R || !step(r + 1u, wb1, pendB, EpB, ApB, pendA, EpA, ApA)) break;
+    if (!step(r, wb0, wb0, pendA, EpA, ApA, pendB, EpB, ApB)) break;
+    if (r + 1u >= R || !step(r + 1u, wb1, wb1, pendB, EpB, ApB, pendA, EpA, ApA)) break;
   }
   if constexpr (K == 8) {  // the last round run's entries (round done - 1)
     if (done > 0u) {
