@@ -481,6 +481,9 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         for dest in ("pageable", "pinned"):
             run.goto(0)
             buf = None
+            if dest == "pinned":  # allocated before the rounds (page-locking 0.8 GB takes ~70 ms)
+                most = max(r["updates"] for r in rows) + (1 << 20)
+                buf = torch.empty(most, dtype=torch.int64, pin_memory=True).numpy().view(np.uint64)
             for _ in range(4):
                 rnd = run.pos % EPOCH
                 eng.synchronize()
