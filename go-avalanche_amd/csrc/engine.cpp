@@ -205,6 +205,7 @@ struct av_engine {
   uint32_t* barrier_err = nullptr;                   // device view of barrier_err_host
   volatile uint32_t* barrier_err_host = nullptr;
   bool failed = false;                               // sticky: a peer barrier timed out
+  bool pref_uncached = false;  // option "pref_uncached": snapshot buffers in uncached device memory (A/B)
   bool peer_fine = true;  // option "peer_fine": snapshot buffers fine-grained once exported (xGMI coherence)
   size_t pref_alloc_words = 0;
   uint32_t barrier_seq = 0;
@@ -2404,6 +2405,23 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
   } else if (n == "peer_mask") {  // before the exchange is set up: need-masked pushes (default 1)
     AV_CHECK(e->peer_world == 0, AV_ERR_INVALID_ARG, "peer_mask must be set before the exchange is set up");
     e->peer_mask = value != 0;
+  } else if (n == "pref_uncached") {
+    // A/B: the three snapshot buffers re-allocated uncached (hipDeviceMallocUncached: the L2 does not
+    // keep their lines, a gather reads the bytes it asks for instead of a 128-B line fill) or back
+    AV_CHECK(value == 0 || value == 1, AV_ERR_INVALID_ARG, "pref_uncached must be 0 or 1");
+    AV_CHECK(!e->arrive && !e->group, AV_ERR_UNSUPPORTED, "pref_uncached: not with a peer exchange");
+    if ((value != 0) != e->pref_uncached) {
+      AV_HIP(hipStreamSynchronize(e->stream));
+      for (int b = 0; b < 3; ++b) {
+        uint32_t* nb = nullptr;
+        AV_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&nb), e->pref_alloc_words * 4,
+                                     value ? hipDeviceMallocUncached : hipDeviceMallocDefault));
+        AV_HIP(hipMemcpy(nb, e->pref[b], e->pref_alloc_words * 4, hipMemcpyDeviceToDevice));
+        AV_HIP(hipFree(e->pref[b]));
+        e->pref[b] = nb;
+      }
+      e->pref_uncached = value != 0;
+    }
   } else if (n == "peer_fine") {  // before av_peer_handles: fine-grained snapshot buffers (default 1)
     AV_CHECK(!e->arrive, AV_ERR_INVALID_ARG, "peer_fine must be set before av_peer_handles");
     e->peer_fine = value != 0;

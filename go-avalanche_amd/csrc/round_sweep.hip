@@ -903,28 +903,51 @@ __device__ __forceinline__ bool byz_bit(const unsigned long long (&bm)[4], uint3
   return (w >> (rel & 63u)) & 1ull;
 }
 
-template <int POL, bool CC>
-__device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32_t lane, uint32_t t0,
-                                                    uint32_t tile_end, uint32_t meta, uint32_t nlA, uint32_t nn,
-                                                    SweepAcc& acc) {
-  const uint32_t ntiles = tile_end - t0;
-  const uint32_t b = lane & (p.BL - 1u), bo = b * 4u;
-  const uint32_t vw = at_byte(p.valid, bo);
-  const uint32_t refp = at_byte(p.pref_prev, p.ref_node * p.PS * 4u + bo);  // every vote word this round
-  const uint32_t rin = p.uni_out ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
-  // the run's Byzantine bits, node nlA + rel at bit rel & 63 of byzm[rel >> 6]: up to 256 nodes (runs of
-  // 16 tiles at BL >= 4, the merged runs of uni_merge on target shards)
+// Everything settled_run_uni reads that depends on no other load (the run's A planes, the validity
+// word, the reference row's words, the Byzantine bits), requested at the start of the wave's run,
+// before the uniform test's slot words and the run's tile words are waited for: the settled wave
+// then waits for one memory latency instead of three in a row (slot words -> tile words -> A).
+#ifndef AVK_UNI_PREFETCH
+#define AVK_UNI_PREFETCH 1
+#endif
+struct UniPre {
+  uint32_t Av[kUniRun];
+  uint32_t vw, refp, rin;
   unsigned long long byzm[4];
-#pragma unroll
-  for (uint32_t j = 0; j < 4u; ++j)
-    byzm[j] = __ballot(lane + 64u * j < nn && is_byz(p.byz, p.n0 + nlA + lane + 64u * j));
-  const uint32_t bpat = byz_pattern(p.round + 1u);
+};
+
+template <int POL>
+__device__ __forceinline__ void uni_prefetch(const RoundParams& p, uint32_t lane, uint32_t t0, uint32_t tile_end,
+                                             uint32_t nlA, uint32_t nn, UniPre& u) {
+  const uint32_t ntiles = tile_end - t0;
+  const uint32_t bo = (lane & (p.BL - 1u)) * 4u;
   const __amdgpu_buffer_rsrc_t ta =
       __builtin_amdgcn_make_buffer_rsrc(p.planes + (size_t)t0 * (kPlanes * 64u), 0, (int)(ntiles * kPlanes * 64u * 4u),
                                         kRsrcWord3);
   const uint32_t aoff = (1536u + lane) * 4u;
-  // the candidates' A planes are all loaded before the first test: up to kUniRun loads in flight
-  // per wave instead of one load latency per tile
+#pragma unroll
+  for (uint32_t i = 0; i < kUniRun; ++i)  // tiles past the run: offset past the resource (reads 0, no access)
+    u.Av[i] = __builtin_amdgcn_raw_buffer_load_b32(ta, i < ntiles ? aoff + i * (kPlanes * 64u * 4u) : 0x80000000u, 0,
+                                                   POL > 0 ? 2 : 0);
+  u.vw = at_byte(p.valid, bo);
+  u.refp = at_byte(p.pref_prev, p.ref_node * p.PS * 4u + bo);  // every vote word this round
+  u.rin = p.uni_out ? at_byte(p.pref_in, p.ref_node * p.PS * 4u + bo) : 0u;
+  // the run's Byzantine bits, node nlA + rel at bit rel & 63 of byzm[rel >> 6]: up to 256 nodes (runs of
+  // 16 tiles at BL >= 4, the merged runs of uni_merge on target shards)
+#pragma unroll
+  for (uint32_t j = 0; j < 4u; ++j)
+    u.byzm[j] = __ballot(lane + 64u * j < nn && is_byz(p.byz, p.n0 + nlA + lane + 64u * j));
+}
+
+template <int POL, bool CC>
+__device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32_t lane, uint32_t t0,
+                                                    uint32_t tile_end, uint32_t meta, uint32_t nlA, uint32_t nn,
+                                                    const UniPre& u, SweepAcc& acc) {
+  const uint32_t ntiles = tile_end - t0;
+  const uint32_t b = lane & (p.BL - 1u);
+  const uint32_t vw = u.vw, refp = u.refp, rin = u.rin;
+  const unsigned long long(&byzm)[4] = u.byzm;
+  const uint32_t bpat = byz_pattern(p.round + 1u);
   uint32_t cand = 0u;
   for (uint32_t i = 0; i < ntiles; ++i) {
     const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, (int)i);
@@ -932,15 +955,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
   }
   uint32_t Av[kUniRun], Ov[kUniRun];
 #pragma unroll
-  for (uint32_t i = 0; i < kUniRun; ++i) {
-    if constexpr (!CC) {  // no branch: a non-candidate's offset is past the run's resource (reads 0, no access)
-      Av[i] = __builtin_amdgcn_raw_buffer_load_b32(ta, (cand >> i) & 1u ? aoff + i * (kPlanes * 64u * 4u) : 0x80000000u,
-                                                   0, POL > 0 ? 2 : 0);
-    } else {
-      Av[i] = (cand >> i) & 1u ? __builtin_amdgcn_raw_buffer_load_b32(ta, aoff + i * (kPlanes * 64u * 4u), 0, POL > 0 ? 2 : 0)
-                               : 0u;
-    }
-  }
+  for (uint32_t i = 0; i < kUniRun; ++i) Av[i] = u.Av[i];
   // the overwritten published words (p.count_changed: publish) with them, not one dependent load per tile
 #pragma unroll
   for (uint32_t i = 0; i < kUniRun; ++i) {
@@ -1101,8 +1116,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
         tile = wave0 * p.tpw;
         tile_end = min(tile + p.tpw, tiles);
         stride = 1u;
-        if (uniform && p.uni_merge > 1u && p.lean && p.settled_fast && p.klazy && p.vv &&
-            p.tpw * p.uni_merge <= kUniRun) {
+        if (p.uni_merge > 1u && p.lean && p.settled_fast && p.klazy && p.vv && p.tpw * p.uni_merge <= kUniRun &&
+            uniform) {
           // uniform input: most tiles settle with no draw, and what is left per wave is its set-up,
           // so every uni_merge-th wave takes its neighbours' runs too and the others end here
           if (wave0 % p.uni_merge) tile = tile_end = tiles;
@@ -1112,6 +1127,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           const uint32_t nlA = uni(div_bl(p, tile * 64u));
           const uint32_t nlB = uni(div_bl(p, min(tile_end * 64u, p.L) - 1u));
           const uint32_t nn = nlB - nlA + 1u;
+          // uniform rows: settled_run_uni's loads requested first (UniPre); wasted only in a klazy round
+          // whose input is not uniform (the converging rounds), where the general path re-reads A
+          UniPre upre;
+          const bool uni_ok = p.uni_in && p.lean && p.settled_fast && p.klazy && p.vv && nn <= 256u &&
+                              tile_end - tile <= kUniRun;
+#if AVK_UNI_PREFETCH
+          if (uni_ok) uni_prefetch<POL>(p, lane, tile, tile_end, nlA, nn, upre);
+#endif
           // the run's per-tile words, one lane per tile (tpw <= 16)
           const uint32_t ti = tile + lane;
           const uint32_t st = p.vv && ti < tile_end ? p.vstale[ti] : 0u;
@@ -1122,8 +1145,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           wd.nn = nn;
           // uniform rows: the run's settled candidates first, with no draw; the draw only if a tile is left
           const uint32_t all_tiles = (uint32_t)((1ull << (tile_end - tile)) - 1ull);
-          if (uniform && p.lean && p.settled_fast && p.klazy && p.vv && nn <= 256u && tile_end - tile <= kUniRun) {
-            uni_done = settled_run_uni<POL, CC>(p, lane, tile, tile_end, wd.meta, nlA, nn, acc);
+          if (uni_ok && uniform) {
+#if !AVK_UNI_PREFETCH
+            uni_prefetch<POL>(p, lane, tile, tile_end, nlA, nn, upre);
+#endif
+            uni_done = settled_run_uni<POL, CC>(p, lane, tile, tile_end, wd.meta, nlA, nn, upre, acc);
             uni_ran = true;
           }
           const bool any_stale = __ballot((st & kVMask) == kVStale) != 0ull;
