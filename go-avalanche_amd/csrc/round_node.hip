@@ -446,6 +446,12 @@ __global__ __launch_bounds__(MAXT) void k_replay_node(const RoundParams p) {
 #ifndef AVK_REPLAY_BUF3
 #define AVK_REPLAY_BUF3 0
 #endif
+#ifndef AVK_REPLAY_PIPE3
+#define AVK_REPLAY_PIPE3 0
+#endif
+#ifndef AVK_REPLAY_PIPE3_LATE
+#define AVK_REPLAY_PIPE3_LATE 0
+#endif
 // (round 5, tools/fuse_probe.py --repeat 15, three alternations on one box: depth 2 3.52-3.53 us per
 // round against 3.69-3.73 at depth 1; profiles/r05/s11/ab_c2e.log)
 #ifndef AVK_REPLAY_EMIT_DEPTH
@@ -632,6 +638,119 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
     return true;
   };
+#if AVK_REPLAY_PIPE3
+  if constexpr (K == 8) {
+    // The emission one step later still: round q's update masks are made in step q, its log space
+    // reserved at the start of step q + 1 and its entries stored at the start of step q + 2, beside
+    // the refill. Every memory operation of a step is then issued before its slot network, so that
+    // when the next step's head waits for everything outstanding (the compiler's vmcnt(0) there:
+    // stores and atomics sit in lane-conditional blocks), those operations are a whole step old.
+    // Three vote buffers and three (E, A, reservation) sets, the loop unrolled three times.
+    EmitRes RX{}, RY{}, RZ{};
+    uint32_t EX[K], EY[K], EZ[K], AX = 0u, AY = 0u, AZ = 0u;
+    u32x4 wb2[RQ];
+    auto stepP = [&](uint32_t r, u32x4 (&wb)[RQ], u32x4 (&nb)[RQ], uint32_t (&Ec)[K], uint32_t& Ac,
+                     const uint32_t (&Er)[K], EmitRes& Rr, const uint32_t (&Es)[K], uint32_t As,
+                     const EmitRes& Rs) -> bool {
+      if (r >= J) {
+        const uint32_t nearfin = Kp[6] & Kp[5] & Kp[4] & Kp[3];
+        if (__syncthreads_or(nearfin != 0u)) {
+          done = r;
+          return false;
+        }
+      }
+      uint32_t ys[7 + K], ns[7 + K], cv[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint32_t wj = wb[j >> 1][(j & 1) * 2];
+        cv[j] = wb[j >> 1][(j & 1) * 2 + 1];
+        const uint32_t yw = wj & cv[j];  // err == 0 implies considered (vote.go:55-56)
+        ys[7 + j] = yw;
+        ns[7 + j] = ~yw & cv[j];
+      }
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        ys[i] = V[6 - i] & C[6 - i];
+        ns[i] = ~V[6 - i] & C[6 - i];
+      }
+#pragma unroll
+      for (int i = 7; i >= 0; --i) {
+        V[i] = i < K ? ys[6 + K - i] : V[i - K];
+        if (i < K) {
+          uint32_t cc;
+          asm volatile("v_mov_b32 %0, %1" : "=v"(cc) : "v"(cv[K - 1 - i]));
+          C[i] = cc;
+        } else {
+          C[i] = C[i - K];
+        }
+      }
+      // round r - 2's entries first: their wait for its reservation (made a step ago; vmcnt counts in
+      // issue order) then covers nothing issued in this step; then round r - 1's reservation and the
+      // refill, which the next step's head waits for a whole step later
+      if (r >= 2u) emitted += emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, Es, As, 0u, Rs, p.round_rel + r - 2u);
+      if (r >= 1u) Rr = emit_reserve_med<K>(p, shard, lane, Er, 0u, upd);  // round r - 1
+#if !AVK_REPLAY_PIPE3_LATE
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < RQ; ++i) nb[i] = pld4<true>(rq + (size_t)min(r + 2u, R - 1u) * rstride + i * 64);
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      uint32_t alive = ~0u, c[4] = {0u, 0u, 0u, 0u}, F = 0u, ap = 0u;
+      const uint32_t low3[3] = {Kp[0], Kp[1], Kp[2]};
+      round_slots<K, false>(ys, ns, low3, 0u, false, alive, A, Ec, c, F, ap);
+      applied += (uint32_t)K * 32u;
+      uint32_t cy = 0u;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const uint32_t ci = i < 4 ? c[i] : 0u;
+        const uint32_t t = Kp[i] ^ ci;
+        const uint32_t si = t ^ cy;
+        cy = (t & cy) | (Kp[i] & ci);
+        Kp[i] = (F & ci) | (~F & si);
+      }
+      if (r + 3u >= R) {  // the last three rounds fill the three snapshot buffers
+        p.pref_ring[(p.ring_next + r) % 3u][prow] = byz ? byz_pattern(p.round + r + 1u) : A;
+        ++pubs;
+      }
+#if AVK_REPLAY_PIPE3_LATE
+      // the refill as the step's last memory operations: whatever else the step issued (stores and
+      // atomics in lane-conditional blocks), at least these RQ loads follow the buffer the next step
+      // reads, on every path
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < RQ; ++i) nb[i] = pld4<true>(rq + (size_t)min(r + 2u, R - 1u) * rstride + i * 64);
+#endif
+      Ac = A;
+      return true;
+    };
+    for (uint32_t r = 0; r < R; r += 3u) {
+      if (!stepP(r, wb0, wb2, EX, AX, EZ, RZ, EY, AY, RY)) break;
+      if (r + 1u >= R || !stepP(r + 1u, wb1, wb0, EY, AY, EX, RX, EZ, AZ, RZ)) break;
+      if (r + 2u >= R || !stepP(r + 2u, wb2, wb1, EZ, AZ, EY, RY, EX, AX, RX)) break;
+    }
+    // rounds done - 2 (reserved, not stored) and done - 1 (neither)
+    const uint32_t tb = p.t0 + b * 32u;
+    if (done >= 2u) {
+      const uint32_t q = done - 2u, rk = p.round_rel + q;
+      if (q % 3u == 0u) emitted += emit_store_med<K>(p, shard, lane, node, tb, EX, AX, 0u, RX, rk);
+      else if (q % 3u == 1u) emitted += emit_store_med<K>(p, shard, lane, node, tb, EY, AY, 0u, RY, rk);
+      else emitted += emit_store_med<K>(p, shard, lane, node, tb, EZ, AZ, 0u, RZ, rk);
+    }
+    if (done >= 1u) {
+      const uint32_t q = done - 1u, rk = p.round_rel + q;
+      if (q % 3u == 0u) {
+        RX = emit_reserve_med<K>(p, shard, lane, EX, 0u, upd);
+        emitted += emit_store_med<K>(p, shard, lane, node, tb, EX, AX, 0u, RX, rk);
+      } else if (q % 3u == 1u) {
+        RY = emit_reserve_med<K>(p, shard, lane, EY, 0u, upd);
+        emitted += emit_store_med<K>(p, shard, lane, node, tb, EY, AY, 0u, RY, rk);
+      } else {
+        RZ = emit_reserve_med<K>(p, shard, lane, EZ, 0u, upd);
+        emitted += emit_store_med<K>(p, shard, lane, node, tb, EZ, AZ, 0u, RZ, rk);
+      }
+    }
+  } else {
+#endif
 #if AVK_REPLAY_BUF3
   // three replayed-vote buffers and three pending sets, the loop unrolled three times: round r reads
   // buffer r % 3 and refills buffer (r + 2) % 3 (read in round r - 1: its registers are dead, so the
@@ -691,6 +810,9 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
       emitted += odd ? emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpB, ApB, 0u, pendB, p.round_rel + done - 1u)
                      : emit_store_med<K>(p, shard, lane, node, p.t0 + b * 32u, EpA, ApA, 0u, pendA, p.round_rel + done - 1u);
     }
+  }
+#endif
+#if AVK_REPLAY_PIPE3
   }
 #endif
   if (done < R && b == 0) p.node_flags[nl] = done + 1u;  // the exact pass takes rounds done..R-1

@@ -907,8 +907,10 @@ __device__ __forceinline__ bool byz_bit(const unsigned long long (&bm)[4], uint3
 // word, the reference row's words, the Byzantine bits), requested at the start of the wave's run,
 // before the uniform test's slot words and the run's tile words are waited for: the settled wave
 // then waits for one memory latency instead of three in a row (slot words -> tile words -> A).
+// (A/B: requested at run start, before the uniform test, 4.24 vs 4.19-4.22 ms per C4 epoch after it,
+// profiles/r05/s14/ab_pre.log: the settled waves are not waiting on that chain; left off)
 #ifndef AVK_UNI_PREFETCH
-#define AVK_UNI_PREFETCH 1
+#define AVK_UNI_PREFETCH 0
 #endif
 struct UniPre {
   uint32_t Av[kUniRun];
