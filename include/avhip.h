@@ -288,8 +288,9 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  *                    engines, M <= 4096). 1 and 2 run the first-generation
  *                    kernel.
  * Sweep-kernel tuning and A/B switches (defaults are the measured best;
- * DESIGN.md §3-4): "tiles_per_wave" (0 = by size: 8
- * from 256k tiles at BL >= 16, else 4), "wave_runs" (1: a wave takes a run
+ * DESIGN.md §3-4): "tiles_per_wave" (0 = by size: 16 at BL <= 8; else the
+ * longest of 16 / 8 / 4 with at most BL tiles that keeps >= 15000 waves;
+ * node shards of an exchange of >= 4 ranks at BL >= 16: 16), "wave_runs" (1: a wave takes a run
  * of consecutive tiles and draws their peers once), "settled_fast" (1),
  * "sweep_nopipe" (1), "virtual_votes" (1), "vv_min_bl" (16), "count_lazy"
  * (1), "fresh" (1), "dense_min" (6 at k = 8: updates per lane that make a
@@ -297,7 +298,14 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  * tile whose 8 peers published the reference node's row reads that row once
  * instead of gathering 8 copies of it; exact, measured slower), "replay_fuse" (16: replay
  * rounds per k_replay_node launch on capped engines, <= 1 = one launch per
- * round). Diagnostics that make results invalid: "ablate_gather",
+ * round), "uni_merge" (1: runs per wave in a round with a uniform input),
+ * "tile_draw" (0; 1: runs whose nodes overflow the run's peer draw share one
+ * draw per tile; exact, measured level), "materialize_run" (1: tiles per wave
+ * of the deferred state's write-back), "pref_uncached" (0; 1: snapshot
+ * buffers in uncached memory; exact, measured slower), "peer_mask" (1:
+ * need-masked peer pushes; set before the exchange), "push_defer" (1: a
+ * wave's pushes queued in LDS and issued after its tiles), "peer_fine" (1).
+ * Diagnostics that make results invalid: "ablate_gather",
  * "ablate_emit" (StatusUpdates counted, not stored), "ablate_node"
  * (k_round_node: 1 = lanes past the cap skipped, 4 = no plane stores),
  * "unsynced_shard". Diagnostics that leave results valid: "count_changed"

@@ -54,6 +54,8 @@ for s in "$@"; do
     ab_unc) step ab_unc 900 bash -c 'for w in c5 c4 c4p; do for i in 1 2; do for o in 0 1; do echo "== $w pref_uncached=$o"; python tools/round_probe.py --workload $w --option pref_uncached=$o | tail -1; done; done; done' ;;
     ab_c2p) step ab_c2p 600 bash -c 'for i in 1 2 3; do for v in default pipe3 pipe3late; do echo "== $v"; if [ $v = default ]; then python tools/fuse_probe.py --fuse 16 --repeat 15; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/fuse_probe.py --fuse 16 --repeat 15; fi; done; done' ;;
     testsrepv) step pytest_repv 600 env AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_${V:-pipe3}.so python -u -m pytest tests/test_gpu_replay_fused.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    c2pmc) step c2pmc 300 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_IFETCH SQ_INSTS_VALU GRBM_GUI_ACTIVE \
+            --output-format csv -d $OUT/c2pmc -o c2 -- python3 tools/fuse_probe.py --fuse 16 --repeat 3 ;;
     peers) step pytest_peers 900 python -u -m pytest tests/test_gpu_peer_group.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gm_c4) step gm_c4 900 python tools/group_model.py --workload c4 --variant nomask:peer_mask=0 --variant tpw16:tiles_per_wave=16 --variant nomask_tpw16:peer_mask=0,tiles_per_wave=16 --json $OUT/group_model_c4.json ;;
     gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --variant nomask:peer_mask=0 --json $OUT/group_model_c4p.json ;;
