@@ -56,6 +56,8 @@ for s in "$@"; do
     testsrepv) step pytest_repv 600 env AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_${V:-pipe3}.so python -u -m pytest tests/test_gpu_replay_fused.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     c2pmc) step c2pmc 300 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_IFETCH SQ_INSTS_VALU GRBM_GUI_ACTIVE \
             --output-format csv -d $OUT/c2pmc -o c2 -- python3 tools/fuse_probe.py --fuse 16 --repeat 3 ;;
+    gm_ptpw) step gm_ptpw_c4p 600 python tools/group_model.py --workload c4p --ranks 4,8 --kinds masked --variant tpw8:tiles_per_wave=8 --variant tpw4:tiles_per_wave=4 --json $OUT/gm_ptpw_c4p.json && \
+             step gm_ptpw_c4pb 600 python tools/group_model.py --workload c4pb --ranks 4,8 --kinds masked --variant tpw8:tiles_per_wave=8 --variant tpw4:tiles_per_wave=4 --json $OUT/gm_ptpw_c4pb.json ;;
     peers) step pytest_peers 900 python -u -m pytest tests/test_gpu_peer_group.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gm_c4) step gm_c4 900 python tools/group_model.py --workload c4 --variant nomask:peer_mask=0 --variant tpw16:tiles_per_wave=16 --variant nomask_tpw16:peer_mask=0,tiles_per_wave=16 --json $OUT/group_model_c4.json ;;
     gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --variant nomask:peer_mask=0 --json $OUT/group_model_c4p.json ;;
