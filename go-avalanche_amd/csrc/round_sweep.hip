@@ -1477,6 +1477,13 @@ __global__ __launch_bounds__(256) void k_kl_materialize(const RoundParams p) {
   if (lane == 0) p.kpend[tile] = 0u;
 }
 
+// The write-back's stores non-temporal (a write-only stream; the next round streams the planes back
+// with non-temporal loads of its own), which also leaves L2 / MALL to the stale tiles' regathered
+// rows. A/B (tools/wb_probe.py, three alternations on one box, profiles/r05/s18/ab_matnt.log):
+// C4 0.80 -> 0.74 ms, C4p 0.65 -> 0.455, C5 1.56 -> 1.42 per segment end.
+#ifndef AVK_MAT_NT
+#define AVK_MAT_NT 1
+#endif
 // Both deferred forms written back in one pass (do_v: stale vote planes and unstored consider planes,
 // as k_vv_materialize; do_k: pending count steps and virtual K4..K7 groups, as k_kl_materialize).
 // Per tile every load (A for a uniform vote register, the K groups, a stale tile's peer rows) is issued
@@ -1516,11 +1523,11 @@ __device__ __forceinline__ void materialize_tile(const RoundParams& p, uint32_t 
   // ---- stores
   if ((raw & kCAll) && x.active) {  // consider planes: all-ones
 #pragma unroll
-    for (int c = 0; c < 8; ++c) tp[1024u + (uint32_t)c * 64u + lane] = ~0u;
+    for (int c = 0; c < 8; ++c) pst<AVK_MAT_NT>(tp + 1024u + (uint32_t)c * 64u + lane, ~0u);
   }
   if (st && x.active) {
-    grp[0] = o0;
-    grp[64] = o1;
+    pst4<AVK_MAT_NT>(grp, o0);
+    pst4<AVK_MAT_NT>(grp + 64, o1);
   }
   if (dok) {  // + 8 * pend on the polled records' counts
     uint32_t Kp[8];
@@ -1545,8 +1552,8 @@ __device__ __forceinline__ void materialize_tile(const RoundParams& p, uint32_t 
       o2[c] = Kp[c];
       o3[c] = Kp[4 + c];
     }
-    grp[128] = o2;
-    grp[192] = o3;
+    pst4<AVK_MAT_NT>(grp + 128, o2);
+    pst4<AVK_MAT_NT>(grp + 192, o3);
   }
 }
 
