@@ -896,13 +896,6 @@ __device__ __forceinline__ uint32_t settled_run(const RoundParams& p, uint32_t l
 // general path.
 constexpr uint32_t kUniRun = 16;  // longest run settled_run_uni takes (p.tpw <= 16)
 
-// bit rel of the 256-bit set bm (rel per lane: a select chain, no scratch-indexed array)
-__device__ __forceinline__ bool byz_bit(const unsigned long long (&bm)[4], uint32_t rel) {
-  const uint32_t q = rel >> 6;
-  const unsigned long long w = q == 0u ? bm[0] : q == 1u ? bm[1] : q == 2u ? bm[2] : bm[3];
-  return (w >> (rel & 63u)) & 1ull;
-}
-
 // Everything settled_run_uni reads that depends on no other load (the run's A planes, the validity
 // word, the reference row's words, the Byzantine bits), requested at the start of the wave's run,
 // before the uniform test's slot words and the run's tile words are waited for: the settled wave
@@ -948,8 +941,10 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
   const uint32_t ntiles = tile_end - t0;
   const uint32_t b = lane & (p.BL - 1u);
   const uint32_t vw = u.vw, refp = u.refp, rin = u.rin;
-  const unsigned long long(&byzm)[4] = u.byzm;
-  const uint32_t bpat = byz_pattern(p.round + 1u);
+  // a run holding a Byzantine node is left to the general path (a uniform input with Byzantine voters
+  // needs every honest row equal to their flip-flop pattern: rare), so that every settled word here
+  // is the tile's A plane, with no per-lane Byzantine-bit lookup per tile
+  if ((u.byzm[0] | u.byzm[1] | u.byzm[2] | u.byzm[3]) != 0ull) return 0u;
   uint32_t cand = 0u;
   for (uint32_t i = 0; i < ntiles; ++i) {
     const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, (int)i);
@@ -989,7 +984,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
       const uint32_t A = Av[i];
       const uint32_t mis = __ballot((refp ^ A) & P0) != 0ull ? 1u : 0u;  // always evaluated: no branch
       const bool ok = (((cand >> i) & 1u) & (mis ^ 1u)) != 0u;             // wave-uniform
-      const uint32_t pub = byz_bit(byzm, rel) ? bpat : A;
+      const uint32_t pub = A;
       const bool st = ok && active;
       __builtin_amdgcn_raw_buffer_store_b32(pub, prb, st ? prow * 4u : 0xFFFFFFFCu, 0, POL == 1 ? 2 : 0);  // (table < 4 GiB: 0xFFFFFFFC is past it)
       umis |= (st & (pub != rin)) ? 1u : 0u;
@@ -1019,8 +1014,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
     const uint32_t P0 = active ? vw : 0u;  // polled = live (kPendAllLive) and valid
     if (__ballot((refp ^ A) & P0) != 0ull) continue;
     const uint32_t node = p.n0 + nl;
-    const bool bz = byz_bit(byzm, nl - nlA);
-    const uint32_t pub = bz ? bpat : A;
+    const uint32_t pub = A;
     if (active) {
       umis |= pub != rin ? 1u : 0u;
       const uint32_t prow = node * p.PS + b;  // < N * PS < 2^30 (sweep gate)
@@ -1028,7 +1022,7 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
       // overwritten (publish): honest rows publish that word again, Byzantine rows its pattern's
       const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)meta, (int)i);
       const bool known = AVK_CC_PREFETCH || (m & 0xFFu) >= 2u;
-      const uint32_t old = AVK_CC_PREFETCH ? Ov[i] : (bz ? byz_pattern(p.round - 2u) : pub);
+      const uint32_t old = AVK_CC_PREFETCH ? Ov[i] : pub;
       publish<POL, CC>(p, prow, pub, old, acc, known, nl, i);
     }
     done |= 1u << i;
