@@ -94,6 +94,8 @@ for s in "$@"; do
             --master-addr 127.0.0.1 --master-port 29538 bench.py --gpus 8 --rehearse-one-gpu --no-secondary --workload c4p ;;
     rehearse8) step rehearse8 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
             --master-addr 127.0.0.1 --master-port 29539 bench.py --gpus 8 --rehearse-one-gpu --no-secondary ;;
+    rehearse8all) step rehearse8all 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+            --master-addr 127.0.0.1 --master-port 29540 bench.py --gpus 8 --rehearse-one-gpu ;;
     rehearse4p) step rehearse4p 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
             --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 4 --rehearse-one-gpu --no-secondary --shard peers ;;
     capped) step capped 600 python -u -m pytest tests/test_gpu_parity.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "capped or c2 or replay or fuzz or poll_sets" ;;
