@@ -104,6 +104,13 @@ def shard_for(wl, world, requested):
     return AUTO_SHARD.get(world, {}).get(wl, "targets")
 
 
+NODE_SHARD_TPW = {"c4p": 8, "c4pb": 8}
+
+
+def eng_tpw_set(args):
+    return getattr(args, "tiles_per_wave", None) is not None
+
+
 PARALLELISM = {
     "peers": "node-sharded, changed preference words pushed to peers over xGMI + device barrier per round",
     "nodes": "node-sharded, RCCL all-gather of preference rows per round",
@@ -278,6 +285,11 @@ class Runner:
             dist.broadcast_object_list(obj, src=0)
             eng.comm_init(world, rank, obj[0])
         elif world > 1 and args.shard == "peers":
+            # runs of 8 tiles for the conflicting workloads' node shards (no settled rounds, which are
+            # what the engine's 16-tile default for >= 4 ranks is for): +1-3 % at 4 and 8 ranks
+            # (tools/group_model.py, profiles/r05/s16/gm_ptpw_*.log)
+            if wl in NODE_SHARD_TPW and not eng_tpw_set(args):
+                eng.set_option("tiles_per_wave", NODE_SHARD_TPW[wl])
             # map every rank's preference snapshots (IPC over xGMI); if any rank
             # cannot, every rank falls back to target sharding (same network)
             blobs = [None] * world
