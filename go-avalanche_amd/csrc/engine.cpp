@@ -360,7 +360,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.tile_draw = e->tile_draw;
   p.seed = e->cfg.seed;
   p.log_cap = e->log_cap;
-  p.log_shards = e->log_shards;
+  p.log_shards = e->log_shards;  // a power of two (set_log_layout): the sweep kernel masks by it
   p.n_nodes = (uint32_t)e->N;
   p.n0 = (uint32_t)e->n0;
   p.NL = e->NL;

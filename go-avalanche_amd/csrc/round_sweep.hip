@@ -1065,7 +1065,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   const uint32_t nwaves = gridDim.x * 4u;
   const uint32_t tiles = p.Lpad >> 6;
   SweepAcc acc;
-  acc.shard = wave0 % p.log_shards;  // once per wave (a runtime modulo is a ~20-instruction sequence)
+  acc.shard = wave0 & (p.log_shards - 1u);  // a power of two (engine.cpp set_log_layout)
   if constexpr (CC) {  // deferred pushes: the wave's queue (dynamic LDS, launched only with p.push_q)
     extern __shared__ __attribute__((aligned(16))) uint8_t s_dyn[];
     const uint32_t w = threadIdx.x >> 6;
@@ -1199,6 +1199,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
     }
     const uint32_t qfirst = tile, qstep = stride;  // deferred pushes: slot s = tile qfirst + s * qstep
     uint32_t qn = 0;
+    if constexpr (MODE == kModeWarm && K == 8) {
+      // every tile of the run settled in the lean loops (the settled rounds): no tile loop at all, whose
+      // per-tile skip test cost a settled wave ~8 scalar instructions per tile (the settled rounds are
+      // bound by the CU's scalar issue); the queued pushes of those tiles are still flushed below
+      if (lean_ran && stride == 1u && tile < tile_end &&
+          lean_done == (uint32_t)((1ull << (tile_end - tile)) - 1ull)) {
+        qn = tile_end - tile;
+        tile = tile_end;
+      }
+    }
     // tile draws (p.tile_draw): a run whose nodes overflow the run's draw (narrow rows: at BL <= 16 a
     // 16-tile run holds 64-256 nodes) still shares one Philox pass per tile, 2 producer lanes per
     // node (a tile's 64 / BL nodes fit: BL >= 2, or >= 4 with a stale tile's paired draw), instead of
