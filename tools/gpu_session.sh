@@ -61,6 +61,9 @@ for s in "$@"; do
     c2abl) step c2abl 300 bash -c 'for i in 1 2; do for o in "replay_fast=1" "ablate_emit=1"; do echo "== $o"; python tools/fuse_probe.py --fuse 16 --repeat 15 --option $o; done; done' ;;
     ab_matnt) step ab_matnt 600 bash -c 'for i in 1 2 3; do for v in default matnt; do echo "== $v"; if [ $v = default ]; then python tools/wb_probe.py --runs 1; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/wb_probe.py --runs 1; fi; done; done' ;;
     probes) step probes 600 bash -c 'for w in c4 c4 c5 c4p; do echo "== $w"; python tools/round_probe.py --workload $w | tail -17; done' ;;
+    benchx2) step bench_a 900 python bench.py && step bench_b 900 python bench.py ;;
+    profc4) step profc4 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc4 -o c4 -- \
+            python3 bench.py --no-cpu-baseline --no-secondary ;;
     peers) step pytest_peers 900 python -u -m pytest tests/test_gpu_peer_group.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gm_c4) step gm_c4 900 python tools/group_model.py --workload c4 --variant nomask:peer_mask=0 --variant tpw16:tiles_per_wave=16 --variant nomask_tpw16:peer_mask=0,tiles_per_wave=16 --json $OUT/group_model_c4.json ;;
     gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --variant nomask:peer_mask=0 --json $OUT/group_model_c4p.json ;;
