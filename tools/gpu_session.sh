@@ -64,6 +64,7 @@ for s in "$@"; do
     benchx2) step bench_a 900 python bench.py && step bench_b 900 python bench.py ;;
     profc4) step profc4 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/profc4 -o c4 -- \
             python3 bench.py --no-cpu-baseline --no-secondary ;;
+    ab_c3tpw) step ab_c3tpw 600 bash -c 'for i in 1 2; do for t in 4 8 16; do echo "== tpw $t"; python tools/round_probe.py --workload c3 --option tiles_per_wave=$t | tail -1; done; done' ;;
     peers) step pytest_peers 900 python -u -m pytest tests/test_gpu_peer_group.py tests/test_gpu_peer_push.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     gm_c4) step gm_c4 900 python tools/group_model.py --workload c4 --variant nomask:peer_mask=0 --variant tpw16:tiles_per_wave=16 --variant nomask_tpw16:peer_mask=0,tiles_per_wave=16 --json $OUT/group_model_c4.json ;;
     gm_c4p) step gm_c4p 900 python tools/group_model.py --workload c4p --variant nomask:peer_mask=0 --json $OUT/group_model_c4p.json ;;
