@@ -172,3 +172,21 @@ def test_shard_auto_per_workload():
     assert bench.shard_for("c4pb", 8, "auto") == "peers"
     assert bench.shard_for("c4p", 4, "auto") == "targets"
     assert bench.shard_for("c4p", 8, "nodes") == "nodes"
+
+
+def test_compact_delivery_fields():
+    """The line's `delivery` summary: the on-device digest rate, the host fetch rates into pageable
+    and pinned memory, and the vote-record rate with every round fetched into pinned memory."""
+    import bench
+    d = {"digest_updates_per_s": 1e10,
+         "pageable": {"updates_per_s": 3e9, "delivered_votes_per_s": 2e11},
+         "pinned": {"updates_per_s": 5e9, "delivered_votes_per_s": 4e11}}
+    c = bench.compact_delivery(d)
+    assert c == {"digest_updates_per_s": 1e10, "fetch_updates_per_s": {"pageable": 3e9, "pinned": 5e9},
+                 "votes_per_s_with_fetch": 4e11}
+
+
+def test_node_shard_run_length_only_for_conflicting_workloads():
+    import bench
+    assert bench.NODE_SHARD_TPW == {"c4p": 8, "c4pb": 8}
+    assert "c4" not in bench.NODE_SHARD_TPW
