@@ -406,18 +406,77 @@ def window_segments(warmup, steps):
 
 def compact_delivery(d):
     """The delivery measurement in the line: StatusUpdates per second consumed on the device
-    (av_updates_digest) and fetched to the host (pageable / pinned destination), and the vote-record
-    updates per second of rounds 0-3 with every round's updates fetched into pinned memory."""
+    (av_updates_digest) and fetched to the host as packed words (pageable / pinned destination), and
+    the vote-record updates per second of rounds 0-3 with every round's updates delivered to host
+    memory: votes_per_s_with_fetch = the pipelined compact stream (round r + 1 computes while round
+    r's stream is copied), _words = the same with every stream expanded into the caller's packed
+    words, _unpipelined = one round then its packed-word fetch into pinned memory."""
+    cp = d.get("compact") or {}
     return {"digest_updates_per_s": d["digest_updates_per_s"],
             "fetch_updates_per_s": {"pageable": d["pageable"]["updates_per_s"], "pinned": d["pinned"]["updates_per_s"]},
-            "votes_per_s_with_fetch": d["pinned"]["delivered_votes_per_s"]}
+            "votes_per_s_with_fetch": cp.get("votes_per_s"),
+            "votes_per_s_with_fetch_words": cp.get("votes_per_s_expanded"),
+            "votes_per_s_with_fetch_unpipelined": d["pinned"]["delivered_votes_per_s"],
+            "compact_bytes_per_update": cp.get("bytes_per_update")}
+
+
+def compact_pipeline(run, rounds=4, most_updates=0):
+    """Rounds 0..rounds-1 of a fresh epoch with every round's StatusUpdates delivered to host memory
+    as the compact stream (av_fetch_compact_async / _wait): round r + 1 is enqueued while round r's
+    stream is copied on the copy stream. Wall clock from the first round's enqueue to the last
+    stream in host memory; then the same with every stream also expanded into the caller's packed
+    words (av_compact_expand, host threads) before the next round is enqueued."""
+    eng = run.eng
+    out = {}
+    # the caller's packed-word buffer, allocated and touched before the timed rounds
+    words = np.empty(max(most_updates, 1) + (1 << 20), np.uint64)
+    words.fill(0)
+    for mode in ("stream", "expanded"):
+        run.goto(0)
+        eng.synchronize()
+        a0 = eng.applied_votes()
+        nbytes = nupd = 0
+        pend = []
+
+        def consume(t):
+            nonlocal nbytes, nupd
+            view = eng.fetch_compact_wait(t, copy=False)
+            h = avhip.compact_header(view)
+            nbytes += h["bytes"]
+            nupd += h["n_updates"]
+            if mode == "expanded":
+                got = avhip.compact_expand_into(view, words)
+                assert got == h["n_updates"]
+        t0 = time.perf_counter()
+        for _ in range(rounds):
+            eng.run_rounds(1)
+            pend.append(eng.fetch_compact_async())
+            if len(pend) >= 2:
+                consume(pend.pop(0))
+        while pend:
+            consume(pend.pop(0))
+        dt = time.perf_counter() - t0
+        run.pos += rounds
+        applied = eng.applied_votes() - a0
+        out[mode] = {"s": dt, "applied": applied, "updates": nupd, "bytes": nbytes}
+    st, ex = out["stream"], out["expanded"]
+    return {"rounds": rounds, "updates": st["updates"], "bytes": st["bytes"],
+            "bytes_per_update": st["bytes"] / max(1, st["updates"]),
+            "votes_per_s": st["applied"] / st["s"], "ms": st["s"] * 1e3,
+            "GB_per_s": st["bytes"] / st["s"] / 1e9, "updates_per_s": st["updates"] / st["s"],
+            "votes_per_s_expanded": ex["applied"] / ex["s"], "ms_expanded": ex["s"] * 1e3,
+            "note": "compact stream (include/avhip.h av_compact_header: ~2 B per update, canonical order) "
+                    "copied into engine-owned pinned host memory handed to the caller (zero-copy view, valid "
+                    "two tickets); expanded: also av_compact_expand into the caller's packed uint64 words"}
 
 
 def size_log(eng, per_round, warmup, steps):
     """Log entries per kind for the largest timed segment (the warm-up epoch's per-round counts
     summed over the segment's rounds, 1.3x + 64 per shard of slack), in place of the worst case per
-    update: the device log holds what one timed segment emits. Returns the log's bytes."""
-    need = [0, 0, 0]
+    update: the device log holds what one timed segment emits, and at least any one round of the
+    epoch (the delivery pass fetches rounds 0-3 one at a time, whatever the window). Returns the
+    log's bytes."""
+    need = [max(per_round.get(r, (0, 0, 0))[k] for r in range(EPOCH)) for k in range(3)]
     for seg in window_segments(warmup, steps):
         tot = [sum(per_round.get(r, (0, 0, 0))[k] for r in seg) for k in range(3)]
         need = [max(a, b) for a, b in zip(need, tot)]
@@ -531,7 +590,8 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
                     "delivered_votes_per_s": sum(r["applied"] for r in rs) / (ms * 1e-3)}
         pg, pn = rate("pageable"), rate("pinned")
         dg = [r for r in rows if r["dest"] == "pageable"]
-        delivery = {"rounds": rows, "pageable": pg, "pinned": pn,
+        compact = compact_pipeline(run, rounds=4, most_updates=max(r["updates"] for r in rows))
+        delivery = {"rounds": rows, "pageable": pg, "pinned": pn, "compact": compact,
                     "delivered_updates_per_s": pg["delivered_votes_per_s"],
                     "status_updates_per_s": pg["updates_per_s"],
                     "digest_updates_per_s": sum(r["updates"] for r in dg) / (sum(r["digest_ms"] for r in dg) * 1e-3),
@@ -600,8 +660,13 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
             changed.append({"round": rnd, "words": w1 - w0, "segments": g1 - g0})
         eng.set_option("count_changed", 0)
     replicas = None
+    needed_rows = None
     if world > 1 and args.shard in ("peers", "nodes"):
-        # every rank's replica of the published preferences must be the same:
+        # the exchange's own invariant, checked before any resynchronisation: every peer row a local
+        # node draws in the next round (R1: the draw is a function of (seed, node, round)) is, in this
+        # rank's replica, the row its owner holds now (a push lost in a round shows here)
+        needed_rows = exchange_rows_match(eng, n, world, rank)
+        # then every rank's whole replica must be the same once the withheld rows are pushed:
         # hash a slice of every rank's node range as this rank sees it
         if args.shard == "peers":
             eng.peer_sync()  # need-masked pushes leave rows no local node reads behind (collective)
@@ -659,9 +724,39 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
         "first_round": warmup % EPOCH,
         "writeback_ms": writeback_ms, "changed": changed,
         "value_general": value_general, "general_rounds": sorted({pr["round"] for pr in gen}),
+        "needed_rows_match": needed_rows,
         "log_bytes": log_bytes, "delivery": delivery, "shard": args.shard,
         "shard_fallback": getattr(args, "shard_fallback", None),
     }
+
+
+def exchange_rows_match(eng, n, world, rank, sample=2048):
+    """Node-sharded ranks: every peer row the first `sample` local nodes draw in the next round must
+    equal, in this rank's replica, its owner's current row. Each rank hashes its replica's copy of
+    those rows per owner and sends (rows, hash); each owner re-hashes the rows from its own (the
+    authoritative) copy. Collective; True iff every request matches on every rank."""
+    a, b = sharding.node_shard(n, world, rank)
+    peers = eng.sample_peers(eng.round, a, min(b, a + sample))
+    rows = np.unique(peers.reshape(-1))
+    owners = [sharding.node_shard(n, world, q) for q in range(world)]
+    mine = eng.read_pref_words(0, n)  # this rank's replica, as stored
+    req = {}
+    for q, (q0, q1) in enumerate(owners):
+        if q == rank:
+            continue
+        rq = rows[(rows >= q0) & (rows < q1)]
+        req[q] = (rq.tolist(), hashlib.sha256(np.ascontiguousarray(mine[rq]).tobytes()).hexdigest())
+    allreq = [None] * world
+    dist.all_gather_object(allreq, req)
+    ok = True
+    for p in range(world):
+        if p == rank or allreq[p] is None or rank not in allreq[p]:
+            continue
+        rq, h = allreq[p][rank]
+        ok &= hashlib.sha256(np.ascontiguousarray(mine[np.asarray(rq, np.int64)]).tobytes()).hexdigest() == h
+    oks = [None] * world
+    dist.all_gather_object(oks, bool(ok))
+    return all(oks)
 
 
 def allgather_probe(world, local_rank, total_bytes=1_000_000 * 128, reps=5):
@@ -900,6 +995,7 @@ def main(argv=None):
                     secondary[wl]["delivery"] = compact_delivery(sr["delivery"])
                 if world > 1:
                     secondary[wl]["replicas_identical"] = sr["replicas_identical"]
+                    secondary[wl]["needed_rows_match"] = sr["needed_rows_match"]
                     secondary[wl]["shard"] = sr["shard"]
                 detail["workloads"][wl] = {"workload": sr["desc"], "value": sr["value"], "delivery": sr["delivery"],
                                            "ms_per_step": sr["elapsed"] / args.steps * 1e3,
@@ -950,6 +1046,7 @@ def main(argv=None):
             line["delivery"] = compact_delivery(r["delivery"])
         if r["replicas_identical"] is not None:
             line["config"]["replicas_identical"] = r["replicas_identical"]
+            line["config"]["needed_rows_match"] = r["needed_rows_match"]
         if r.get("shard_fallback"):
             line["config"]["shard_fallback"] = "peer exchange unavailable: " + r["shard_fallback"]
         if secondary:

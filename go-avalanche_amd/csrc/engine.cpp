@@ -280,6 +280,25 @@ struct av_engine {
   void* stage[2] = {nullptr, nullptr};
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
   bool dropin_fast = true;
+  // StatusUpdate encoder (log_ops.hip launch_encode_log): error flags and per-pass totals (device)
+  uint32_t* enc_err = nullptr;
+  uint64_t* enc_tot = nullptr;  // [4]
+  uint32_t enc_buckets = 1u << 26;  // option "enc_buckets": (round, node) buckets per encoder pass
+  // compact stream delivery (av_fetch_compact_async / _wait): two slots, each a device buffer the
+  // encoder writes and a pinned host buffer its copy lands in, the copy on copy_stream (overlaps the
+  // next rounds on the engine stream)
+  hipStream_t copy_stream = nullptr;
+  void* cdev[2] = {nullptr, nullptr};
+  size_t cdev_bytes[2] = {0, 0};
+  void* chost[2] = {nullptr, nullptr};
+  size_t chost_bytes[2] = {0, 0};
+  hipEvent_t cev[2] = {nullptr, nullptr};
+  av_compact_header chdr[2] = {};
+  int64_t cticket = 0;           // next ticket
+  bool cpend[2] = {false, false};  // a copy was issued into the slot
+  // batched poll sets (av_get_invs_batch): host-mapped pinned output the fill kernel writes
+  void* invs_host = nullptr;
+  size_t invs_host_bytes = 0;
 
   size_t round_replay_words() const { return avk::replay_words(Lpad, k); }
 };
@@ -425,9 +444,21 @@ int materialize_votes(av_engine* e) {
   return AV_OK;
 }
 
+// A serial peer group's members store into each other's buffers: once any member was destroyed (its
+// buffers freed), no member may push or exchange need masks any more.
+int group_alive(const av_engine* e) {
+  if (e->group)
+    for (const av_engine* m : e->group->members) AV_CHECK(m, AV_ERR_UNSUPPORTED, "peer group: a rank was destroyed");
+  return AV_OK;
+}
+
 // Peer-push exchange: copy this rank's rows of snapshot buffer `b` into every
 // peer replica (a full resynchronisation of those rows).
 int push_own_rows(av_engine* e, int b) {
+  {
+    int rc = group_alive(e);
+    if (rc != AV_OK) return rc;
+  }
   avk::PeerPtrs dst{};
   uint32_t n = 0;
   for (int r = 0; r < e->peer_world; ++r)
@@ -522,6 +553,10 @@ int need_draw(av_engine* e, int64_t w, hipStream_t s) {
 
 int need_gen(av_engine* e, int64_t w) {
   if (!e->masked || e->need_pushed == w) return AV_OK;
+  {
+    int rc = group_alive(e);
+    if (rc != AV_OK) return rc;
+  }
   if (e->need_drawn_w == w) {
     AV_HIP(hipStreamWaitEvent(e->stream, e->need_drawn, 0));  // drawn ahead on the side stream
   } else {
@@ -1026,6 +1061,18 @@ int av_destroy(av_engine* e) {
     if (e->stage_ev[i]) (void)hipEventDestroy(e->stage_ev[i]);
   }
   if (e->digest) (void)hipFree(e->digest);
+  if (e->copy_stream) {
+    (void)hipStreamSynchronize(e->copy_stream);
+    (void)hipStreamDestroy(e->copy_stream);
+  }
+  for (int i = 0; i < 2; ++i) {
+    if (e->cdev[i]) (void)hipFree(e->cdev[i]);
+    if (e->chost[i]) (void)hipHostFree(e->chost[i]);
+    if (e->cev[i]) (void)hipEventDestroy(e->cev[i]);
+  }
+  if (e->invs_host) (void)hipHostFree(e->invs_host);
+  if (e->enc_err) (void)hipFree(e->enc_err);
+  if (e->enc_tot) (void)hipFree(e->enc_tot);
   if (e->changed) (void)hipFree(e->changed);
   if (e->push_tbl) (void)hipFree(e->push_tbl);
   if (e->marker) (void)hipEventDestroy(e->marker);
@@ -1389,8 +1436,9 @@ int av_register_votes(av_engine* e, int64_t node, const int64_t* targets, const 
 //  * fast path (it holds): one workgroup per node applies the node's
 //    Responses in call order, each lane's run of votes where it lies
 //    (k_dropin_resp), no grouping step;
-//  * otherwise: lane keys on the device, stable radix sort of (lane, vote
-//    position) and run-length encoding (launch_group_votes), then
+//  * otherwise: lane keys on the device, the hand-written stable radix sort
+//    of (lane, vote position) and run-length encoding (log_ops.hip
+//    launch_group_votes, dev_scan.h), then
 //    k_register_votes over the runs.
 // Statuses come back as one byte per vote and are widened on the host.
 // Copies: 4 B per vote each way plus 1 B back (the caller's int64 hashes and
@@ -1491,13 +1539,12 @@ int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, 
   if (!fast) {
     const uint64_t keys_total = (uint64_t)e->L + 1;  // L = unknown targets
     while (key_bits < 32 && (1ull << key_bits) < keys_total) ++key_bits;
-    AV_HIP(avk::launch_group_votes(nullptr, &tb, nullptr, nullptr, nullptr, m, key_bits, nullptr, nullptr, nullptr,
-                                   nullptr, nullptr, nullptr, nullptr, nullptr, e->stream));
+    tb = (size_t)avk::group_votes_scratch_words(m) * 8;
   }
-  // packed | off | node | status bytes || keys vidx info keys_s perm perm_s lanes counts(m+1) offs(m+1) nruns
-  // entries(2m) temp
+  // packed | off | node | status bytes || keys vidx info keys_s perm_s keys_t perm_t lanes offs(m+1) nruns
+  // entries(2m) | u64 scratch (radix sort, run scan)
   const size_t head_words = (size_t)m + tab_words + ((size_t)m + 3) / 4;
-  const size_t grp_words = fast ? 0 : 7 * (size_t)m + 2 * ((size_t)m + 1) + 1 + 2 * (size_t)m;
+  const size_t grp_words = fast ? 0 : 8 * (size_t)m + ((size_t)m + 1) + 1 + 2 * (size_t)m;
   void* buf = nullptr;
   int rc = engine_scratch(e, (head_words + grp_words) * 4 + tb + 512, &buf);
   if (rc != AV_OK) return rc;
@@ -1530,12 +1577,12 @@ int av_register_votes_batch(av_engine* e, int64_t n_resp, const int64_t* nodes, 
     AV_HIP(avk::launch_dropin_resp(p, e->stream));
   } else {
     uint32_t* g0 = w + head_words;
-    uint32_t *keys = g0, *vidx = keys + m, *info = vidx + m, *keys_s = info + m, *perm = keys_s + m,
-             *perm_s = perm + m, *lanes = perm_s + m, *counts = lanes + m, *offs = counts + m + 1,
+    uint32_t *keys = g0, *vidx = keys + m, *info = vidx + m, *keys_s = info + m, *perm_s = keys_s + m,
+             *keys_t = perm_s + m, *perm_t = keys_t + m, *lanes = perm_t + m, *offs = lanes + m,
              *nruns = offs + m + 1, *ent = nruns + 1;
-    void* temp = reinterpret_cast<void*>(((uintptr_t)(ent + 2 * (size_t)m) + 255) & ~(uintptr_t)255);
+    auto* temp = reinterpret_cast<uint64_t*>(((uintptr_t)(ent + 2 * (size_t)m) + 255) & ~(uintptr_t)255);
     AV_HIP(avk::launch_dropin_keys(p, keys, vidx, info, e->stream));
-    AV_HIP(avk::launch_group_votes(temp, &tb, keys, vidx, info, m, key_bits, keys_s, perm, perm_s, lanes, counts, offs,
+    AV_HIP(avk::launch_group_votes(temp, keys, vidx, info, m, key_bits, keys_s, perm_s, keys_t, perm_t, lanes, offs,
                                    nruns, ent, e->stream));
     uint32_t nb = 0;
     AV_HIP(hipMemcpyAsync(&nb, nruns, 4, hipMemcpyDeviceToHost, e->stream));
@@ -1649,6 +1696,9 @@ int av_get_invs(av_engine* e, int64_t node, int64_t* out_targets, int64_t cap, i
   return AV_OK;
 }
 
+// GetInvsForNextPoll for a node range (processor.go:144-170): counts, their device scan and the CSR
+// fill enqueued back to back, the fill writing offsets and targets straight into host-mapped pinned
+// staging (coalesced stores): one synchronization per call, then a host copy into the caller's arrays.
 int av_get_invs_batch(av_engine* e, int64_t n0, int64_t n1, int64_t* offsets, int32_t* targets, int64_t cap,
                       int64_t* total) {
   AV_ENTER(e);
@@ -1659,26 +1709,32 @@ int av_get_invs_batch(av_engine* e, int64_t n0, int64_t n1, int64_t* offsets, in
   *total = 0;
   offsets[0] = 0;
   if (!n) return AV_OK;
-  Scratch sc;
-  AV_HIP(sc.ensure((size_t)n * 4));
-  auto* dcounts = static_cast<uint32_t*>(sc.p);
-  AV_HIP(avk::launch_poll_sets(e->planes, e->valid, e->BL, (uint32_t)(n0 - e->n0), n, (uint32_t)e->t0, dcounts,
-                               nullptr, nullptr, e->stream));
-  std::vector<uint32_t> counts(n);
-  AV_HIP(hipMemcpyAsync(counts.data(), dcounts, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream));
+  // staging: offsets (n + 1 int64) then up to min(cap, the largest possible poll sets) int32 targets
+  const uint64_t most = (uint64_t)n * (uint64_t)std::min<int64_t>(AV_MAX_ELEMENT_POLL, e->t1 - e->t0);
+  const uint64_t keep = std::min<uint64_t>((uint64_t)std::max<int64_t>(cap, 0), most);
+  const size_t hb = ((size_t)n + 1) * 8 + (size_t)keep * 4;
+  if (hb > e->invs_host_bytes) {
+    if (e->invs_host) AV_HIP(hipHostFree(e->invs_host));
+    e->invs_host = nullptr;
+    e->invs_host_bytes = 0;
+    AV_HIP(hipHostMalloc(&e->invs_host, hb, hipHostMallocMapped));
+    e->invs_host_bytes = hb;
+  }
+  void* dev_view = nullptr;
+  AV_HIP(hipHostGetDevicePointer(&dev_view, e->invs_host, 0));
+  auto* hoffs = static_cast<int64_t*>(e->invs_host);
+  auto* doffs = static_cast<int64_t*>(dev_view);
+  void* scratch = nullptr;
+  int rc = engine_scratch(e, (size_t)avk::poll_sets_scratch_words(n) * 8, &scratch);
+  if (rc != AV_OK) return rc;
+  AV_HIP(avk::launch_poll_sets_batch(e->planes, e->valid, e->BL, (uint32_t)(n0 - e->n0), n, (uint32_t)e->t0, keep,
+                                     static_cast<uint64_t*>(scratch), doffs, reinterpret_cast<int32_t*>(doffs + n + 1),
+                                     e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));
-  for (uint32_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + counts[i];
-  *total = offsets[n];
+  *total = hoffs[n];
+  std::memcpy(offsets, hoffs, ((size_t)n + 1) * 8);
   AV_CHECK(*total <= cap, AV_ERR_OVERFLOW, "cap too small (%lld needed)", (long long)*total);
-  if (!*total) return AV_OK;
-  Scratch so, st;
-  AV_HIP(so.ensure((size_t)(n + 1) * 8));
-  AV_HIP(st.ensure((size_t)*total * 4));
-  AV_HIP(hipMemcpyAsync(so.p, offsets, (size_t)(n + 1) * 8, hipMemcpyHostToDevice, e->stream));
-  AV_HIP(avk::launch_poll_sets(e->planes, e->valid, e->BL, (uint32_t)(n0 - e->n0), n, (uint32_t)e->t0, nullptr,
-                               static_cast<const int64_t*>(so.p), static_cast<int32_t*>(st.p), e->stream));
-  AV_HIP(hipMemcpyAsync(targets, st.p, (size_t)*total * 4, hipMemcpyDeviceToHost, e->stream));
-  AV_HIP(hipStreamSynchronize(e->stream));
+  if (*total) std::memcpy(targets, reinterpret_cast<const int32_t*>(hoffs + n + 1), (size_t)*total * 4);
   return AV_OK;
 }
 
@@ -1908,30 +1964,34 @@ int relayout_log_if_empty(av_engine* e) {
   return AV_OK;
 }
 
-// n words from device memory into the caller's host buffer. Pinned caller memory: one DMA. Pageable
+extern "C++" {
+namespace {
+
+// n bytes from device memory into the caller's host buffer. Pinned caller memory: one DMA. Pageable
 // memory: chunks through two pinned staging buffers, the DMA of chunk i + 1 in flight while host
 // threads copy chunk i out (a hipMemcpy into pageable memory is staged by the runtime at ~14.5 GB/s,
 // DESIGN.md §4 delivery).
-int copy_out(av_engine* e, uint64_t* out, const uint64_t* dev, size_t n) {
+int copy_out_bytes(av_engine* e, void* out, const void* dev, size_t n) {
   if (!n) return AV_OK;
   hipPointerAttribute_t at{};
   bool pinned = false;
   if (hipPointerGetAttributes(&at, out) == hipSuccess) pinned = at.type == hipMemoryTypeHost;
   (void)hipGetLastError();
-  constexpr size_t kChunk = (size_t)8 << 20;  // words (64 MiB)
-  if (pinned || n <= (size_t)1 << 19) {
-    AV_HIP(hipMemcpyAsync(out, dev, n * 8, hipMemcpyDeviceToHost, e->stream));
+  constexpr size_t kChunk = (size_t)64 << 20;  // bytes
+  if (pinned || n <= (size_t)4 << 20) {
+    AV_HIP(hipMemcpyAsync(out, dev, n, hipMemcpyDeviceToHost, e->stream));
     AV_HIP(hipStreamSynchronize(e->stream));
     return AV_OK;
   }
   for (int i = 0; i < 2; ++i) {
-    if (!e->stage[i]) AV_HIP(hipHostMalloc(&e->stage[i], kChunk * 8, hipHostMallocDefault));
+    if (!e->stage[i]) AV_HIP(hipHostMalloc(&e->stage[i], kChunk, hipHostMallocDefault));
     if (!e->stage_ev[i]) AV_HIP(hipEventCreateWithFlags(&e->stage_ev[i], hipEventDisableTiming));
   }
   const size_t chunks = (n + kChunk - 1) / kChunk;
+  const char* src_dev = static_cast<const char*>(dev);
   auto dma = [&](size_t c) -> int {
     const size_t w = std::min(kChunk, n - c * kChunk);
-    AV_HIP(hipMemcpyAsync(e->stage[c & 1], dev + c * kChunk, w * 8, hipMemcpyDeviceToHost, e->stream));
+    AV_HIP(hipMemcpyAsync(e->stage[c & 1], src_dev + c * kChunk, w, hipMemcpyDeviceToHost, e->stream));
     AV_HIP(hipEventRecord(e->stage_ev[c & 1], e->stream));
     return AV_OK;
   };
@@ -1944,111 +2004,330 @@ int copy_out(av_engine* e, uint64_t* out, const uint64_t* dev, size_t n) {
     }
     AV_HIP(hipEventSynchronize(e->stage_ev[c & 1]));
     const size_t w = std::min(kChunk, n - c * kChunk);
-    const uint64_t* src = static_cast<const uint64_t*>(e->stage[c & 1]);
-    uint64_t* dst = out + c * kChunk;
-    parallel_chunks((int64_t)w, 1 << 18, [&](int, int64_t a, int64_t b) {
-      std::memcpy(dst + a, src + a, (size_t)(b - a) * 8);
+    const char* src = static_cast<const char*>(e->stage[c & 1]);
+    char* dst = static_cast<char*>(out) + c * kChunk;
+    parallel_chunks((int64_t)w, 1 << 21, [&](int, int64_t a, int64_t b) {
+      std::memcpy(dst + a, src + a, (size_t)(b - a));
     });
   }
   return AV_OK;
 }
+
+int copy_out(av_engine* e, uint64_t* out, const uint64_t* dev, size_t n) { return copy_out_bytes(e, out, dev, n * 8); }
+
+// ---- canonical StatusUpdate order on the device (log_ops.hip launch_encode_log) ----
+constexpr uint32_t kChunkNodes = 4096;         // compact index granularity (nodes per index entry)
+constexpr size_t kHdrBytes = sizeof(av_compact_header);
+
+uint32_t bits_for(uint64_t n) {  // bits of the values 0 .. n - 1
+  uint32_t b = 0;
+  while (b < 32 && (1ull << b) < n) ++b;
+  return b;
+}
+
+struct Encoded {
+  int64_t updates = 0;
+  int64_t bytes = 0;  // compact: the whole stream, header included
+  av_compact_header hdr{};
+};
+
+// Rounds the pending log can hold (round_rel < this)
+uint32_t log_rounds(const av_engine* e) { return (uint32_t)std::max<int64_t>(e->round - e->log_base, 1); }
+
+avk::EncodeParams encode_params(av_engine* e) {
+  avk::EncodeParams p{};
+  p.log = e->log;
+  p.mlog = e->mlog;
+  p.dlog = e->dlog;
+  p.log_count = e->log_count;
+  p.log_cap = e->log_cap;
+  p.mlog_cap = e->mlog_cap;
+  p.dlog_cap = e->dlog_cap;
+  p.shards = e->log_shards;
+  p.K = (uint32_t)e->k;
+  p.n0 = (uint32_t)e->n0;
+  p.NL = e->NL;
+  p.BL = e->BL;
+  p.t0 = (uint32_t)e->t0;
+  p.r_total = log_rounds(e);
+  const uint32_t tb = bits_for((uint64_t)(e->t1 - e->t0)), sb = bits_for((uint64_t)e->k);
+  p.target_bits = tb;
+  p.code_bytes = sb + tb + 2 <= 16 ? 2u : 4u;
+  p.err = e->enc_err;
+  return p;
+}
+
+// Device bytes a compact stream of the pending log needs at most (c: the log's counts).
+size_t compact_bound(const av_engine* e, const avk::EncodeParams& p, const LogCounts& c) {
+  const uint64_t R = p.r_total, chunks = (e->NL + kChunkNodes - 1) / kChunkNodes;
+  const uint64_t entries = (uint64_t)(c.n_singles + c.n_med + c.n_records);
+  const uint64_t groups = std::min<uint64_t>(R * e->NL, entries);
+  return kHdrBytes + (size_t)(R * chunks + 1) * 16 + (size_t)groups * 12 + (size_t)c.total * p.code_bytes + 256;
+}
+
+// Encode the pending log (counts c) into dev: packed words (compact = false; dev holds c.total u64)
+// or the compact stream (dev: compact_bound bytes; the header is returned, not written). Enqueued on
+// the engine stream; synchronizes once per encoder pass (a log spanning more (round, node) buckets
+// than one pass holds takes several) and checks that every counted update was laid out.
+int encode_log(av_engine* e, const LogCounts& c, bool compact, void* dev, Encoded* res) {
+  *res = Encoded{};
+  if (!e->enc_err) AV_HIP(dev_alloc(&e->enc_err, 1));
+  if (!e->enc_tot) AV_HIP(dev_alloc(&e->enc_tot, 4));
+  avk::EncodeParams p = encode_params(e);
+  const uint32_t R = p.r_total;
+  const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(R, e->enc_buckets / std::max<uint32_t>(e->NL, 1)));
+  const uint64_t entries = (uint64_t)(c.n_singles + c.n_med + c.n_records);
+  AV_CHECK(entries < (1ull << 40), AV_ERR_UNSUPPORTED, "StatusUpdate log too large to order");
+  p.nr = per;
+  void* scratch = nullptr;
+  int rc = engine_scratch(e, avk::encode_scratch_bytes(p, entries, per * e->NL), &scratch);
+  if (rc != AV_OK) return rc;
+  const uint32_t chunks = (e->NL + kChunkNodes - 1) / kChunkNodes;
+  auto* base = static_cast<uint8_t*>(dev);
+  uint64_t* cidx = compact ? reinterpret_cast<uint64_t*>(base + kHdrBytes) : nullptr;
+  uint8_t* groups = compact ? base + kHdrBytes + (size_t)((uint64_t)R * chunks + 1) * 16 : nullptr;
+  AV_HIP(hipMemsetAsync(e->enc_err, 0, 4, e->stream));
+  uint64_t ubase = 0, cbase = 0;
+  for (uint32_t r0 = 0; r0 < R; r0 += per) {
+    p.r0 = r0;
+    p.nr = std::min(per, R - r0);
+    const bool last = r0 + p.nr >= R;
+    AV_HIP(avk::launch_encode_log(p, entries, scratch, compact ? nullptr : static_cast<uint64_t*>(dev), groups, cidx,
+                                  chunks, kChunkNodes, ubase, cbase, last, e->enc_tot, e->stream));
+    uint64_t tot[4] = {0, 0, 0, 0};
+    uint32_t err = 0;
+    AV_HIP(hipMemcpyAsync(tot, e->enc_tot, sizeof(tot), hipMemcpyDeviceToHost, e->stream));
+    AV_HIP(hipMemcpyAsync(&err, e->enc_err, 4, hipMemcpyDeviceToHost, e->stream));
+    AV_HIP(hipStreamSynchronize(e->stream));
+    AV_CHECK(err == 0, AV_ERR_HIP, "StatusUpdate log inconsistent (encoder flags %u)", err);
+    ubase += tot[0];
+    cbase += tot[1];
+  }
+  AV_CHECK((int64_t)ubase == c.total, AV_ERR_HIP, "StatusUpdate log inconsistent (%lld of %lld updates ordered)",
+           (long long)ubase, (long long)c.total);
+  res->updates = (int64_t)ubase;
+  if (compact) {
+    av_compact_header& h = res->hdr;
+    h.magic = AV_COMPACT_MAGIC;
+    h.version = AV_COMPACT_VERSION;
+    h.log_base = e->log_base;
+    h.n_updates = (int64_t)ubase;
+    h.node_base = e->n0;
+    h.target_base = e->t0;
+    h.n_rounds = (int32_t)R;
+    h.chunks = (int32_t)chunks;
+    h.chunk_nodes = (int32_t)kChunkNodes;
+    h.code_bytes = (int32_t)p.code_bytes;
+    h.target_bits = (int32_t)p.target_bits;
+    h.slot_bits = (int32_t)bits_for((uint64_t)e->k);
+    h.bytes = (int64_t)(groups - base) + (int64_t)cbase;
+    res->bytes = h.bytes;
+  }
+  return AV_OK;
+}
+
+// Grow a device buffer (contents not kept).
+int grow_dev(void** p, size_t* have, size_t want) {
+  if (want <= *have) return AV_OK;
+  if (*p) AV_HIP(hipFree(*p));
+  *p = nullptr;
+  *have = 0;
+  want = std::max(want + want / 8, (size_t)1 << 20);
+  hipError_t he = hipMalloc(p, want);
+  AV_CHECK(he == hipSuccess, he == hipErrorOutOfMemory ? AV_ERR_OOM : AV_ERR_HIP, "device buffer (%zu B): %s", want,
+           hipGetErrorString(he));
+  *have = want;
+  return AV_OK;
+}
+int grow_pinned(void** p, size_t* have, size_t want) {
+  if (want <= *have) return AV_OK;
+  if (*p) AV_HIP(hipHostFree(*p));
+  *p = nullptr;
+  *have = 0;
+  want = std::max(want + want / 8, (size_t)1 << 20);
+  AV_HIP(hipHostMalloc(p, want, hipHostMallocDefault));
+  *have = want;
+  return AV_OK;
+}
+
+// Read the log's counters, failing (and clearing the log) if it overflowed.
+int pending_counts(av_engine* e, LogCounts& c) {
+  int rc = read_log_counts(e, c);
+  if (rc != AV_OK) return rc;
+  if (c.ovf) {
+    rc = clear_log(e);
+    if (rc != AV_OK) return rc;
+    return fail(AV_ERR_OVERFLOW, "device StatusUpdate log overflowed (%lld updates, capacity %lld per shard)",
+                (long long)c.total, (long long)e->log_cap);
+  }
+  return AV_OK;
+}
+
+}  // namespace
+}  // extern "C++"
 
 int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out) {
   AV_ENTER(e);
   AV_PEER_SYNC_CHECK(e);
   AV_CHECK(n_out && (cap == 0 || out), AV_ERR_INVALID_ARG, "null argument");
   LogCounts c;
-  int rc = read_log_counts(e, c);
+  int rc = pending_counts(e, c);
+  *n_out = c.total;
   if (rc != AV_OK) return rc;
-  const int64_t total = c.total, singles = c.n_singles, records = c.n_records, meds = c.n_med;
-  *n_out = total;
-  if (c.ovf) {
-    rc = clear_log(e);
+  AV_CHECK(c.total <= cap, AV_ERR_OVERFLOW, "cap too small: %lld updates pending", (long long)c.total);
+  if (c.total > 0) {
+    // the compact slots' device buffers hold no in-flight copy source after this wait
+    if (e->copy_stream) AV_HIP(hipStreamSynchronize(e->copy_stream));
+    rc = grow_dev(&e->cdev[0], &e->cdev_bytes[0], (size_t)c.total * 8);
     if (rc != AV_OK) return rc;
-    return fail(AV_ERR_OVERFLOW, "device StatusUpdate log overflowed (%lld updates, capacity %lld per shard)",
-                (long long)total, (long long)e->log_cap);
-  }
-  AV_CHECK(total <= cap, AV_ERR_OVERFLOW, "cap too small: %lld updates pending", (long long)total);
-  if (total > 0) {
-    // device: singles and expanded medium and dense records side by side,
-    // radix-sorted into the canonical (round, node, slot, target) order, then
-    // one copy out
-    const uint32_t K = (uint32_t)e->k, dw = avk::dense_words(K);
-    const int64_t nrec = std::max(records, meds);
-    size_t scan_bytes = 0, sort_bytes = 0;
-    AV_HIP(avk::launch_dense_expand(nullptr, (uint64_t)nrec, K, nullptr, nullptr, nullptr, &scan_bytes, nullptr,
-                                    e->stream));
-    // sort on the key bits that vary: [2, 52 + width of the largest round_rel)
-    // (status bits need no ordering: (round, node, slot, target) is unique)
-    const int64_t max_rel = std::max<int64_t>(e->round - 1 - e->log_base, 0);
-    int end_bit = 52;
-    while (end_bit < 64 && (max_rel >> (end_bit - 52)) != 0) ++end_bit;
-    AV_HIP(avk::launch_sort_updates(nullptr, &sort_bytes, nullptr, nullptr, (uint64_t)total, 2, end_bit, e->stream));
-    auto up = [](size_t b) { return (b + 255) / 256 * 256; };
-    const size_t b_words = up((size_t)total * 8), b_rec = up((size_t)records * dw * 8),
-                 b_med = up((size_t)meds * 8 * avk::med_rec_words()), b_cnt = up((size_t)nrec * 8 + 8), b_off = up(3 * avk::kLogShards * 8);
-    const size_t bytes = 2 * b_words + b_rec + b_med + 2 * b_cnt + b_off + up(scan_bytes) + up(sort_bytes);
-    void* base = nullptr;
-    rc = engine_scratch(e, bytes, &base);
+    Encoded r;
+    rc = encode_log(e, c, false, e->cdev[0], &r);
     if (rc != AV_OK) return rc;
-    char* q = static_cast<char*>(base);
-    auto* words = reinterpret_cast<uint64_t*>(q);
-    q += b_words;
-    auto* sorted = reinterpret_cast<uint64_t*>(q);
-    q += b_words;
-    auto* recs = reinterpret_cast<uint64_t*>(q);
-    q += b_rec;
-    auto* mrecs = reinterpret_cast<uint64_t*>(q);
-    q += b_med;
-    auto* cnt = reinterpret_cast<uint64_t*>(q);
-    q += b_cnt;
-    auto* offs = reinterpret_cast<uint64_t*>(q);
-    q += b_cnt;
-    auto* soff = reinterpret_cast<uint64_t*>(q);
-    auto* doff = soff + avk::kLogShards;
-    auto* moff = doff + avk::kLogShards;
-    q += b_off;
-    void* scan_tmp = q;
-    q += up(scan_bytes);
-    void* sort_tmp = q;
-    AV_HIP(hipMemcpyAsync(soff, c.soff.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
-    AV_HIP(hipMemcpyAsync(doff, c.doff.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
-    AV_HIP(hipMemcpyAsync(moff, c.moff.data(), avk::kLogShards * 8, hipMemcpyHostToDevice, e->stream));
-    AV_HIP(avk::launch_compact_log(e->log, e->log_count, soff, e->log_cap, e->log_shards, 1, words, e->stream));
-    // expand one record kind (dense: k, medium: kMedKind) at words + at; returns the updates it held
-    auto expand = [&](const uint64_t* src, int64_t n, uint32_t kind, int64_t at, int64_t* got) -> int {
-      *got = 0;
-      if (!n) return AV_OK;
-      size_t sb = scan_bytes;
-      AV_HIP(avk::launch_dense_expand(src, (uint64_t)n, kind, cnt, offs, scan_tmp, &sb, words + at, e->stream));
-      uint64_t last[2] = {0, 0};
-      AV_HIP(hipMemcpyAsync(&last[0], offs + n - 1, 8, hipMemcpyDeviceToHost, e->stream));
-      AV_HIP(hipMemcpyAsync(&last[1], cnt + n - 1, 8, hipMemcpyDeviceToHost, e->stream));
-      AV_HIP(hipStreamSynchronize(e->stream));
-      *got = (int64_t)(last[0] + last[1]);
-      return AV_OK;
-    };
-    int64_t n_med = 0, n_dense = 0;
-    if (meds) {
-      AV_HIP(avk::launch_compact_log(e->mlog, e->mlog_count, moff, e->mlog_cap, e->log_shards, avk::med_rec_words(),
-                                    mrecs, e->stream));
-      rc = expand(mrecs, meds, avk::kMedKind, singles, &n_med);
-      if (rc != AV_OK) return rc;
-      AV_CHECK(singles + n_med <= total, AV_ERR_HIP, "StatusUpdate log inconsistent (medium records)");
-    }
-    if (records) {
-      AV_HIP(avk::launch_compact_log(e->dlog, e->dlog_count, doff, e->dlog_cap, e->log_shards, dw, recs, e->stream));
-      rc = expand(recs, records, K, singles + n_med, &n_dense);
-      if (rc != AV_OK) return rc;
-    }
-    // the expansion must produce exactly the counted updates
-    AV_CHECK(singles + n_med + n_dense == total, AV_ERR_HIP, "StatusUpdate log inconsistent (%lld of %lld)",
-             (long long)(singles + n_med + n_dense), (long long)total);
-    AV_HIP(avk::launch_sort_updates(sort_tmp, &sort_bytes, words, sorted, (uint64_t)total, 2, end_bit, e->stream));
-    rc = copy_out(e, out, sorted, (size_t)total);
+    rc = copy_out(e, out, static_cast<const uint64_t*>(e->cdev[0]), (size_t)c.total);
     if (rc != AV_OK) return rc;
   }
   return clear_log(e);
+}
+
+int av_fetch_compact(av_engine* e, void* out, int64_t cap, int64_t* bytes) {
+  AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
+  AV_CHECK(bytes && (cap == 0 || out), AV_ERR_INVALID_ARG, "null argument");
+  *bytes = 0;
+  LogCounts c;
+  int rc = pending_counts(e, c);
+  if (rc != AV_OK) return rc;
+  if (e->copy_stream) AV_HIP(hipStreamSynchronize(e->copy_stream));
+  const avk::EncodeParams p = encode_params(e);
+  rc = grow_dev(&e->cdev[0], &e->cdev_bytes[0], compact_bound(e, p, c));
+  if (rc != AV_OK) return rc;
+  Encoded r;
+  rc = encode_log(e, c, true, e->cdev[0], &r);
+  if (rc != AV_OK) return rc;
+  *bytes = r.bytes;
+  AV_CHECK(r.bytes <= cap, AV_ERR_OVERFLOW, "cap too small: the stream takes %lld bytes", (long long)r.bytes);
+  rc = copy_out_bytes(e, static_cast<uint8_t*>(out) + kHdrBytes, static_cast<const uint8_t*>(e->cdev[0]) + kHdrBytes,
+                      (size_t)r.bytes - kHdrBytes);
+  if (rc != AV_OK) return rc;
+  std::memcpy(out, &r.hdr, kHdrBytes);
+  return clear_log(e);
+}
+
+int av_fetch_compact_async(av_engine* e, int64_t* ticket) {
+  AV_ENTER(e);
+  AV_PEER_SYNC_CHECK(e);
+  AV_CHECK(ticket, AV_ERR_INVALID_ARG, "null argument");
+  if (!e->copy_stream) AV_HIP(hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+  const int s = (int)(e->cticket & 1);
+  if (!e->cev[s]) AV_HIP(hipEventCreateWithFlags(&e->cev[s], hipEventDisableTiming));
+  LogCounts c;
+  int rc = pending_counts(e, c);  // waits for the rounds enqueued before
+  if (rc != AV_OK) return rc;
+  // the slot's previous copy (ticket - 2) has read its device buffer and filled its host buffer
+  if (e->cpend[s]) AV_HIP(hipEventSynchronize(e->cev[s]));
+  e->cpend[s] = false;
+  const avk::EncodeParams p = encode_params(e);
+  rc = grow_dev(&e->cdev[s], &e->cdev_bytes[s], compact_bound(e, p, c));
+  if (rc != AV_OK) return rc;
+  Encoded r;
+  rc = encode_log(e, c, true, e->cdev[s], &r);  // synchronizes the engine stream
+  if (rc != AV_OK) return rc;
+  rc = grow_pinned(&e->chost[s], &e->chost_bytes[s], (size_t)r.bytes);
+  if (rc != AV_OK) return rc;
+  AV_HIP(hipMemcpyAsync(static_cast<uint8_t*>(e->chost[s]) + kHdrBytes, static_cast<const uint8_t*>(e->cdev[s]) + kHdrBytes,
+                        (size_t)r.bytes - kHdrBytes, hipMemcpyDeviceToHost, e->copy_stream));
+  AV_HIP(hipEventRecord(e->cev[s], e->copy_stream));
+  e->chdr[s] = r.hdr;
+  e->cpend[s] = true;
+  *ticket = e->cticket++;
+  return clear_log(e);
+}
+
+int av_fetch_compact_wait(av_engine* e, int64_t ticket, const void** stream, int64_t* bytes) {
+  AV_ENTER(e);
+  AV_CHECK(stream && bytes, AV_ERR_INVALID_ARG, "null argument");
+  AV_CHECK(ticket >= 0 && ticket < e->cticket && ticket >= e->cticket - 2, AV_ERR_INVALID_ARG,
+           "ticket %lld is not one of the last two issued", (long long)ticket);
+  const int s = (int)(ticket & 1);
+  AV_CHECK(e->cpend[s], AV_ERR_INVALID_ARG, "ticket %lld has no copy", (long long)ticket);
+  AV_HIP(hipEventSynchronize(e->cev[s]));
+  std::memcpy(e->chost[s], &e->chdr[s], kHdrBytes);
+  *stream = e->chost[s];
+  *bytes = e->chdr[s].bytes;
+  return AV_OK;
+}
+
+int av_compact_expand(const void* stream, int64_t bytes, uint64_t* out, int64_t cap, int64_t* n_out) {
+  AV_CHECK(stream && n_out && (cap == 0 || out), AV_ERR_INVALID_ARG, "null argument");
+  *n_out = 0;
+  AV_CHECK(bytes >= (int64_t)kHdrBytes, AV_ERR_INVALID_ARG, "stream shorter than its header");
+  av_compact_header h;
+  std::memcpy(&h, stream, kHdrBytes);
+  AV_CHECK(h.magic == AV_COMPACT_MAGIC && h.version == AV_COMPACT_VERSION, AV_ERR_INVALID_ARG, "not a compact stream");
+  AV_CHECK(h.bytes == bytes && h.n_rounds >= 1 && h.chunks >= 1 && (h.code_bytes == 2 || h.code_bytes == 4) &&
+               h.target_bits >= 0 && h.target_bits <= 22 && h.n_updates >= 0,
+           AV_ERR_INVALID_ARG, "malformed compact stream header");
+  const uint64_t n_idx = (uint64_t)h.n_rounds * (uint64_t)h.chunks + 1;
+  const uint8_t* base = static_cast<const uint8_t*>(stream);
+  const uint64_t gstart = kHdrBytes + n_idx * 16;
+  AV_CHECK((uint64_t)bytes >= gstart, AV_ERR_INVALID_ARG, "compact stream index truncated");
+  const uint64_t* idx = reinterpret_cast<const uint64_t*>(base + kHdrBytes);
+  AV_CHECK(idx[2 * (n_idx - 1)] == (uint64_t)bytes - gstart && idx[2 * (n_idx - 1) + 1] == (uint64_t)h.n_updates,
+           AV_ERR_INVALID_ARG, "compact stream index inconsistent");
+  *n_out = h.n_updates;
+  AV_CHECK(h.n_updates <= cap, AV_ERR_OVERFLOW, "cap too small: %lld updates", (long long)h.n_updates);
+  const uint8_t* groups = base + gstart;
+  const uint32_t tb = (uint32_t)h.target_bits, cw = (uint32_t)h.code_bytes;
+  const uint32_t tmask = (1u << tb) - 1u;
+  std::vector<int> bad(64, 0);
+  parallel_chunks((int64_t)(n_idx - 1), 1, [&](int t, int64_t j0, int64_t j1) {
+    for (int64_t j = j0; j < j1; ++j) {
+      const uint64_t rr = (uint64_t)j / (uint64_t)h.chunks;
+      const uint64_t b0 = idx[2 * j], b1 = idx[2 * j + 2];
+      uint64_t u = idx[2 * j + 1];
+      const uint64_t u1 = idx[2 * j + 3];
+      if (b0 > b1 || b1 > (uint64_t)bytes - gstart || u > u1) {
+        bad[t] = 1;
+        return;
+      }
+      for (uint64_t at = b0; at < b1;) {
+        if (at + 8 > b1) {
+          bad[t] = 1;
+          return;
+        }
+        uint32_t node, n;
+        std::memcpy(&node, groups + at, 4);
+        std::memcpy(&n, groups + at + 4, 4);
+        const uint64_t len = 8 + (((uint64_t)n * cw + 3) & ~3ull);
+        if (at + len > b1 || u + n > u1 || node >= (1u << 24)) {
+          bad[t] = 1;
+          return;
+        }
+        const uint64_t hi = (rr << 52) | ((uint64_t)node << 28);
+        const uint8_t* cp = groups + at + 8;
+        for (uint32_t i = 0; i < n; ++i) {
+          uint32_t code;
+          if (cw == 2) {
+            uint16_t v;
+            std::memcpy(&v, cp + 2 * i, 2);
+            code = v;
+          } else {
+            std::memcpy(&code, cp + 4 * i, 4);
+          }
+          const uint64_t slot = code >> (tb + 2), tl = (code >> 2) & tmask;
+          out[u + i] = hi | (slot << 24) | (((uint64_t)h.target_base + tl) << 2) | (code & 3u);
+        }
+        u += n;
+        at += len;
+      }
+      if (u != u1) {
+        bad[t] = 1;
+        return;
+      }
+    }
+  });
+  for (int b : bad) AV_CHECK(!b, AV_ERR_INVALID_ARG, "malformed compact stream groups");
+  return AV_OK;
 }
 
 int av_updates_digest(av_engine* e, uint64_t out[3]) { return av_updates_digest_range(e, 0, e ? e->N : 0, out); }
@@ -2338,6 +2617,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     }
     e->solo_barrier = value != 0;
     e->solo_used = e->solo_used || e->solo_barrier;
+  } else if (n == "enc_buckets") {  // (round, node) buckets per encoder pass (tests of the multi-pass path)
+    AV_CHECK(value >= 1 && value <= (1ll << 30), AV_ERR_INVALID_ARG, "enc_buckets must be in [1, 2^30]");
+    e->enc_buckets = (uint32_t)value;
   } else if (n == "dropin_fast") {
     e->dropin_fast = value != 0;
   } else if (n == "settled_lean") {

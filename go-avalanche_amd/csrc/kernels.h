@@ -445,21 +445,34 @@ hipError_t launch_log_digest(const uint64_t* log, const uint32_t* counts, uint32
                              const uint32_t* dcounts, uint32_t dcap, const uint64_t* mlog, const uint32_t* mcounts,
                              uint32_t mcap, uint32_t shards, uint32_t k, uint32_t node0, uint32_t node1,
                              unsigned long long* out, hipStream_t s);
-// Expand n compacted dense records into packed words at out (scratch: n u64
-// counts + n u64 offsets; temp == nullptr: *temp_bytes = the scan's scratch size).
-hipError_t launch_dense_expand(const uint64_t* recs, uint64_t n, uint32_t k, uint64_t* counts_scratch,
-                               uint64_t* offsets, void* temp, size_t* temp_bytes, uint64_t* out, hipStream_t s);
-// The same for n compacted medium records (k = 0 selects the medium form in launch_dense_expand's
-// kernels: med_rec_words() u64 per record).
-constexpr uint32_t kMedKind = 0u;
-// Radix sort of packed update words on bits [begin_bit, end_bit) (temp ==
-// nullptr: size query).
-hipError_t launch_sort_updates(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
-                               int begin_bit, int end_bit, hipStream_t s);
-hipError_t launch_group_votes(void* temp, size_t* temp_bytes, const uint32_t* keys, const uint32_t* vidx,
-                              const uint32_t* info, uint32_t n, int key_bits, uint32_t* keys_s, uint32_t* perm,
-                              uint32_t* perm_s, uint32_t* lanes, uint32_t* counts, uint32_t* offs, uint32_t* n_runs,
-                              uint32_t* entries, hipStream_t s);
+// Canonical order of the pending StatusUpdates (log_ops.hip): a counting sort by (round, node) bucket
+// for rounds [r0, r0 + nr) of the log (round_rel < r_total), then one wave per bucket writing its
+// updates in (slot, target) order, as packed words (out + ubase + the bucket's update offset) or as
+// compact groups (cout + cbase + its byte offset; index entries into cidx). Reads the log counters on
+// the device. totals (device, may be null): this pass's updates, compact bytes, entries.
+struct EncodeParams {
+  const uint64_t* log;
+  const uint64_t* mlog;
+  const uint64_t* dlog;
+  const uint32_t* log_count;  // [3][kLogShards][kCtrStride]: singles, slot records, dense records
+  uint32_t log_cap, mlog_cap, dlog_cap, shards;
+  uint32_t K, n0, NL, BL, t0;
+  uint32_t r0, nr, r_total;
+  uint32_t code_bytes, target_bits;  // compact codes: slot << (target_bits + 2) | local target << 2 | status
+  uint32_t* err;  // bit 0: an entry outside the engine's nodes / rounds; bit 1: a bucket's count mismatch
+};
+uint64_t encode_scratch_bytes(const EncodeParams& p, uint64_t entries, uint32_t buckets);
+hipError_t launch_encode_log(const EncodeParams& p, uint64_t entries, void* scratch, uint64_t* out, uint8_t* cout,
+                             uint64_t* cidx, uint32_t chunks, uint32_t chunk_nodes, uint64_t ubase, uint64_t cbase,
+                             bool last_pass, uint64_t* totals, hipStream_t s);
+// Drop-in batch grouping: stable radix sort of (lane key, position) into (keys_s, perm_s) (keys_t,
+// perm_t: the other buffer set), run-length encoding into lanes / offs (n_runs + 1) / *n_runs, and the
+// (vote index, packed vote) entries in grouped order. scratch: group_votes_scratch_words(n) u64.
+uint64_t group_votes_scratch_words(uint32_t n);
+hipError_t launch_group_votes(uint64_t* scratch, const uint32_t* keys, const uint32_t* vidx, const uint32_t* info,
+                              uint32_t n, int key_bits, uint32_t* keys_s, uint32_t* perm_s, uint32_t* keys_t,
+                              uint32_t* perm_t, uint32_t* lanes, uint32_t* offs, uint32_t* n_runs, uint32_t* entries,
+                              hipStream_t s);
 
 hipError_t launch_write_records(uint32_t* planes, uint32_t BL, uint32_t nl0, uint32_t nl1, uint32_t tl0,
                                 uint32_t tl1, const uint32_t* in, hipStream_t s);
@@ -475,11 +488,13 @@ hipError_t launch_gen_replay(uint64_t seed, uint32_t n0, uint32_t NL, uint32_t B
                              hipStream_t s);
 hipError_t launch_count_live(const uint32_t* planes, const uint32_t* valid, const uint32_t* byz, uint32_t n0,
                              uint32_t BL, uint32_t L, int honest_only, unsigned long long* out, hipStream_t s);
-// Batched poll sets: counts (out == nullptr path) or CSR targets at offsets.
-hipError_t launch_poll_sets(const uint32_t* planes, const uint32_t* valid, uint32_t BL, uint32_t nl0, uint32_t n,
-                            uint32_t t0, uint32_t* counts, const int64_t* offsets, int32_t* out, hipStream_t s);
-// Concatenate the shards' first min(count, cap) entries of `words` u64 each.
-hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets,
-                              uint32_t log_cap, uint32_t shards, uint32_t words, uint64_t* out, hipStream_t s);
+// Batched poll sets (GetInvsForNextPoll of nodes [nl0, nl0 + n)): the per-node counts, their device
+// scan into offsets (n + 1, u64) and the CSR targets in one stream-ordered sequence; entries at or past
+// cap are not written. offs_out / targets_out may be host-mapped pinned memory (hipHostGetDevicePointer):
+// the fill kernel's stores are coalesced. scratch: poll_sets_scratch_words(n) u64.
+uint64_t poll_sets_scratch_words(uint32_t n);
+hipError_t launch_poll_sets_batch(const uint32_t* planes, const uint32_t* valid, uint32_t BL, uint32_t nl0,
+                                  uint32_t n, uint32_t t0, uint64_t cap, uint64_t* scratch, int64_t* offs_out,
+                                  int32_t* targets_out, hipStream_t s);
 
 }  // namespace avk

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 
+#include "dev_scan.h"
 #include "kernels.h"
 #include "round_common.h"
 
@@ -724,40 +725,65 @@ __global__ void k_count_live(const uint32_t* planes, const uint32_t* valid, cons
   if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
 }
 
-__global__ void k_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets, uint32_t log_cap,
-                              uint32_t words, uint64_t* out) {
-  const uint32_t shard = blockIdx.x;
-  const uint32_t n = min(counts[shard * kCtrStride], log_cap) * words;
-  const uint64_t* src = log + (size_t)shard * log_cap * words;
-  uint64_t* dst = out + offsets[shard] * words;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
-}
-
 // Batched GetInvsForNextPoll (processor.go:144-170) for local nodes
 // [nl0, nl0 + gridDim.x): one 64-lane workgroup per node walks the node's
 // blocks in order with a running wave prefix count of live, valid records
-// (rule R1: ascending target order, at most kMaxPoll). counts == nullptr:
-// write the poll set at out + offsets[node]; else only count it.
+// (rule R1: ascending target order, at most kMaxPoll). counts != nullptr: only
+// count them. Else write the poll set at out + offsets[node] (entries at or past
+// cap skipped): per 64-block chunk, lane i writes the chunk's records i, i + 64,
+// ... (its block by binary search over the chunk's prefix counts in LDS, its
+// target by the rank-th set bit), so every store is coalesced — the output may
+// be host-mapped memory written over PCIe. lane 0 of each node also writes
+// offs_out[node] (and the last node offs_out[n]) as int64.
 __global__ __launch_bounds__(64) void k_poll_sets(const uint32_t* planes, const uint32_t* valid, uint32_t BL,
                                                   uint32_t nl0, uint32_t t0, uint32_t* counts,
-                                                  const int64_t* offsets, int32_t* out) {
+                                                  const uint64_t* offsets, uint64_t cap, int64_t* offs_out,
+                                                  int32_t* out) {
+  __shared__ uint32_t pre[64];
+  __shared__ uint32_t bits_s[64];
   const uint32_t i = blockIdx.x, nl = nl0 + i, lane = threadIdx.x;
+  const uint64_t o0 = counts ? 0ull : offsets[i];
+  if (!counts && lane == 0) {
+    offs_out[i] = (int64_t)o0;
+    if (i == gridDim.x - 1u) offs_out[i + 1u] = (int64_t)offsets[i + 1u];
+  }
   uint32_t run = 0;  // records selected so far (wave-uniform)
   for (uint32_t b0 = 0; b0 < BL && run < kMaxPoll; b0 += 64u) {
     const uint32_t b = b0 + lane;
     const uint32_t bits = b < BL ? ~*pw(planes, nl * BL + b, kPK + 7) & valid[b] : 0u;
     const uint32_t c = (uint32_t)__popc(bits);
     const uint32_t incl = wave_incl_scan(c, lane);
-    if (!counts && c) {
-      uint32_t pos = run + incl - c, x = bits;
-      int32_t* dst = out + offsets[i];
-      while (x && pos < kMaxPoll) {
-        const uint32_t bit = (uint32_t)__ffs(x) - 1u;
-        x &= x - 1u;
-        dst[pos++] = (int32_t)(t0 + 32u * b + bit);
+    const uint32_t tot = (uint32_t)__shfl((int)incl, 63, 64);
+    if (!counts) {
+      pre[lane] = incl - c;
+      bits_s[lane] = bits;
+      __syncthreads();
+      const uint32_t take = min(tot, kMaxPoll - run);
+      for (uint32_t q = lane; q < take; q += 64u) {
+        uint32_t l0 = 0, l1 = 63;  // the last block lane whose prefix is <= q
+        while (l0 < l1) {
+          const uint32_t mid = (l0 + l1 + 1u) >> 1;
+          if (pre[mid] <= q) l0 = mid; else l1 = mid - 1u;
+        }
+        uint32_t m = bits_s[l0], r = q - pre[l0], pos = 0;
+#pragma unroll
+        for (uint32_t w = 16; w >= 1; w >>= 1) {
+          const uint32_t low = m & ((1u << w) - 1u);
+          const uint32_t cl = (uint32_t)__popc(low);
+          if (r >= cl) {
+            r -= cl;
+            m >>= w;
+            pos += w;
+          } else {
+            m = low;
+          }
+        }
+        const uint64_t at = o0 + run + q;
+        if (at < cap) out[at] = (int32_t)(t0 + 32u * (b0 + l0) + pos);
       }
+      __syncthreads();
     }
-    run += (uint32_t)__shfl((int)incl, 63, 64);
+    run += tot;
   }
   if (counts && lane == 0) counts[i] = min(run, kMaxPoll);
 }
@@ -1038,12 +1064,6 @@ hipError_t launch_count_live(const uint32_t* planes, const uint32_t* valid, cons
   return hipGetLastError();
 }
 
-hipError_t launch_poll_sets(const uint32_t* planes, const uint32_t* valid, uint32_t BL, uint32_t nl0, uint32_t n,
-                            uint32_t t0, uint32_t* counts, const int64_t* offsets, int32_t* out, hipStream_t s) {
-  if (!n) return hipSuccess;
-  hipLaunchKernelGGL(k_poll_sets, dim3(n), dim3(64), 0, s, planes, valid, BL, nl0, t0, counts, offsets, out);
-  return hipGetLastError();
-}
 
 hipError_t launch_push_rows(const uint32_t* src, PeerPtrs dst, uint32_t n_dst, uint64_t w0, uint64_t w1,
                             hipStream_t s) {
@@ -1107,9 +1127,24 @@ hipError_t launch_peer_barrier(PeerPtrs arrive, uint32_t world, uint32_t rank, u
   return hipGetLastError();
 }
 
-hipError_t launch_compact_log(const uint64_t* log, const uint32_t* counts, const uint64_t* offsets, uint32_t log_cap,
-                              uint32_t shards, uint32_t words, uint64_t* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_compact_log, dim3(shards), dim3(256), 0, s, log, counts, offsets, log_cap, words, out);
+uint64_t poll_sets_scratch_words(uint32_t n) {
+  return ((uint64_t)n + 1u) / 2u + 1u + ((uint64_t)n + 1u) + dscan::scan_scratch_words(n);
+}
+
+hipError_t launch_poll_sets_batch(const uint32_t* planes, const uint32_t* valid, uint32_t BL, uint32_t nl0,
+                                  uint32_t n, uint32_t t0, uint64_t cap, uint64_t* scratch, int64_t* offs_out,
+                                  int32_t* targets_out, hipStream_t s) {
+  if (!n) return hipSuccess;
+  uint32_t* counts = reinterpret_cast<uint32_t*>(scratch);
+  uint64_t* offs = scratch + ((uint64_t)n + 1u) / 2u + 1u;
+  uint64_t* sc = offs + (uint64_t)n + 1u;
+  hipLaunchKernelGGL(k_poll_sets, dim3(n), dim3(64), 0, s, planes, valid, BL, nl0, t0, counts,
+                     (const uint64_t*)nullptr, (uint64_t)0, (int64_t*)nullptr, (int32_t*)nullptr);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if ((e = dscan::launch_scan(dscan::In32{counts}, n, offs, sc, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_poll_sets, dim3(n), dim3(64), 0, s, planes, valid, BL, nl0, t0, (uint32_t*)nullptr,
+                     (const uint64_t*)offs, cap, offs_out, targets_out);
   return hipGetLastError();
 }
 

@@ -1,21 +1,33 @@
-// StatusUpdate delivery on the device (processor.go:111's *[]StatusUpdate
-// out-parameter): the round kernels leave their updates in a sharded log of
-// single packed words and dense lane records (kernels.h); these kernels
-//  * expand the dense records into packed words (A after slot j = the final
-//    A plane ^ parity of the later slots' updates; vote.go:77-91 statuses),
-//  * put the singles and the expanded words into the canonical (round, node,
-//    slot, target) order with a device radix sort (rocPRIM via hipCUB) — the
-//    packed word sorts exactly in that order (include/avhip.h),
+// StatusUpdate delivery on the device (processor.go:61,111's *[]StatusUpdate
+// out-parameter, appended in vote order, processor.go:94). The round kernels
+// leave a round's updates in a sharded log of single packed words, slot records
+// and dense lane records (kernels.h); a lane's updates of one round are in one
+// record kind. These kernels
+//  * put every pending update into the canonical (round, node, slot, target)
+//    order — the reference's append order under rule R1 —
+//    with a counting sort keyed by (round, node): the key range is known from
+//    the log layout (rounds since the last fetch x local nodes), so one pass
+//    counts each bucket's entries and updates (wave-aggregated atomics), a
+//    device scan (dev_scan.h) turns the counts into offsets, a scatter groups
+//    the entries by bucket, and one wave per bucket lays its updates out in
+//    (slot, target) order through a per-bucket table of (slot, 32-target
+//    block) cells in LDS: the cells' prefix counts give every update's position
+//    directly, so nothing is sorted by comparison and every output store is
+//    coalesced;
+//  * write them either as packed 8-byte words (av_fetch_updates) or as the
+//    compact stream (av_fetch_compact*: per (round, node) group a node id and
+//    a count, then 2 bytes per update when slot, local target and status fit);
 //  * or reduce them to an order-independent digest (count, sum and xor of
 //    splitmix64(word)) that the oracle computes the same way
 //    (oracle/avalanche_oracle.c avo_mix64), for full-size parity checks that
 //    do not copy billions of updates to the host.
+// The drop-in RegisterVotes batch groups its votes by lane with the stable
+// radix sort of dev_scan.h (launch_group_votes). No library sort or scan.
 #include <hip/hip_runtime.h>
-
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
+#include "dev_scan.h"
 #include "kernels.h"
 #include "round_common.h"
 
@@ -90,17 +102,6 @@ __device__ __forceinline__ void for_each_med(const uint64_t* rec, F&& f) {
 #endif
 }
 
-// u64 words of one record: dense (k >= 1) or medium (kMedKind)
-__host__ __device__ constexpr uint32_t rec_words(uint32_t K) { return K == kMedKind ? med_rec_words() : dense_words(K); }
-
-template <typename F>
-__device__ __forceinline__ void for_each_rec(const uint64_t* rec, uint32_t K, F&& f) {
-  if (K == kMedKind)
-    for_each_med(rec, f);
-  else
-    for_each_dense(reinterpret_cast<const uint32_t*>(rec), K, f);
-}
-
 __device__ __forceinline__ bool in_nodes(uint64_t w, uint32_t node0, uint32_t node1) {
   const uint32_t node = (uint32_t)(w >> 28) & 0xFFFFFFu;
   return node >= node0 && node < node1;
@@ -162,35 +163,352 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
   }
 }
 
-// Updates held by each dense record (popcount of its E_j) or medium record (its n).
-__global__ __launch_bounds__(256) void k_dense_counts(const uint64_t* recs, uint64_t n, uint32_t K, uint64_t* cnt) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (K == kMedKind) {
+// ---------------------------------------------------------------------------
+// Canonical order by (round, node) buckets.
+// ---------------------------------------------------------------------------
+// Flat entry index f: the log's entries kind by kind (singles, slot records, dense records), shard by
+// shard, each shard's first min(count, cap) entries. flat[kind * shards + shard] = the first f of that
+// shard (dscan over the counters), flat[3 * shards] = the total.
+struct FlatIn {
+  const uint32_t* counts;  // [3][kLogShards][kCtrStride]
+  uint32_t shards, cap0, cap1, cap2;
+  __device__ uint64_t operator()(uint64_t i) const {
+    const uint32_t kind = (uint32_t)(i / shards), shard = (uint32_t)(i - (uint64_t)kind * shards);
+    const uint32_t cap = kind == 0 ? cap0 : kind == 1 ? cap1 : cap2;
+    return min(counts[((size_t)kind * kLogShards + shard) * kCtrStride], cap);
+  }
+};
+
+constexpr uint64_t kInvalid64 = ~0ull;
+constexpr uint32_t kCntShift = 40;  // cnt64[b] = entries << 40 | updates
+constexpr uint64_t kUpdMask = (1ull << kCntShift) - 1ull;
+
+struct EncArgs {
+  EncodeParams p;
+  const uint64_t* flat;  // [3 * shards + 1]
+  unsigned long long* cnt;  // [B]
+  uint64_t* ekey;        // [entries]: bucket << 32 | rank, or kInvalid64
+  uint32_t B;            // buckets of this pass = nr * NL
+};
+
+// Locate flat entry f: (kind, address of the entry in its kind's array, in entries).
+__device__ __forceinline__ void locate(const uint64_t* flat_lds, uint32_t shards, uint64_t f, uint32_t& kind,
+                                       uint64_t& addr, const EncodeParams& p) {
+  uint32_t lo = 0, hi = 3u * shards - 1u;  // last slot s with flat[s] <= f
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1u) >> 1;
+    if (flat_lds[mid] <= f) lo = mid; else hi = mid - 1u;
+  }
+  kind = lo / shards;
+  const uint32_t shard = lo - kind * shards;
+  const uint32_t cap = kind == 0 ? p.log_cap : kind == 1 ? p.mlog_cap : p.dlog_cap;
+  addr = (uint64_t)shard * cap + (f - flat_lds[lo]);
+}
+
+// An entry's key word (pack_update of its first update or of its block) and number of updates.
+__device__ __forceinline__ uint64_t entry_key(const EncodeParams& p, uint32_t kind, uint64_t addr, uint32_t& nu) {
+  if (kind == 0) {
+    nu = 1u;
+    return p.log[addr];
+  }
+  if (kind == 1) {
+    constexpr uint32_t MW = med_rec_words();
 #if AVK_MED_S4
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(recs + i * med_rec_words());
-    const uint32_t nw = (w[2] & kMedS4Died) ? 3u : 4u;
-    uint32_t c = 0;
-    for (uint32_t j = 0; j < nw; ++j) c += (uint32_t)__popc(w[4 + j]);
-    cnt[i] = c;
+    const u32x4* q = reinterpret_cast<const u32x4*>(p.mlog + addr * MW);
+    const u32x4 a = q[0], b = q[1];
+    const uint32_t S = a[2];
+    nu = (uint32_t)(__popc(b[0]) + __popc(b[1]) + __popc(b[2]) + ((S & kMedS4Died) ? 0 : __popc(b[3])));
+    return (uint64_t)a[0] | ((uint64_t)a[1] << 32);
 #else
-    cnt[i] = min((uint32_t)(recs[2u * i + 1u] & 15u), kMedMax);
+    const uint64_t* r = p.mlog + addr * MW;
+    nu = min((uint32_t)(r[1] & 15u), kMedMax);
+    return r[0];
+#endif
+  }
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p.dlog + addr * dense_words(p.K));
+  uint32_t c = 0;
+  for (uint32_t j = 0; j < p.K; ++j) c += (uint32_t)__popc(w[2 + j]);
+  nu = c;
+  return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+}
+
+constexpr uint32_t kEncThreads = 256;
+constexpr uint32_t kFlatMax = 3u * kLogShards + 1u;
+
+__device__ __forceinline__ void load_flat(uint64_t* lds, const uint64_t* flat, uint32_t shards) {
+  for (uint32_t i = threadIdx.x; i <= 3u * shards; i += blockDim.x) lds[i] = flat[i];
+  __syncthreads();
+}
+
+// Count pass: every entry of the pass's rounds adds (1 << 40 | its updates) to its bucket; runs of
+// lanes with the same bucket (a wave's entries come from one writer wave's consecutive lanes, so a
+// node's records sit together) add once, and every lane gets its rank among the bucket's entries.
+__global__ __launch_bounds__(kEncThreads) void k_bucket_count(EncArgs a) {
+  __shared__ uint64_t flat[kFlatMax];
+  const EncodeParams& p = a.p;
+  load_flat(flat, a.flat, p.shards);
+  const uint64_t total = flat[3u * p.shards];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t mask_le = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+  for (uint64_t base = (uint64_t)blockIdx.x * kEncThreads + (threadIdx.x & ~63u); base < total;
+       base += (uint64_t)gridDim.x * kEncThreads) {
+    const uint64_t f = base + lane;
+    uint32_t b = 0xFFFFFFFFu, nu = 0u;
+    if (f < total) {
+      uint32_t kind;
+      uint64_t addr;
+      locate(flat, p.shards, f, kind, addr, p);
+      const uint64_t key = entry_key(p, kind, addr, nu);
+      const uint32_t rr = (uint32_t)(key >> 52), node = (uint32_t)(key >> 28) & 0xFFFFFFu;
+      const bool ok = node >= p.n0 && node - p.n0 < p.NL && rr < p.r_total;
+      if (ok && rr >= p.r0 && rr < p.r0 + p.nr) b = (rr - p.r0) * p.NL + (node - p.n0);
+      if (!ok) atomicOr(p.err, 1u);  // an entry outside the engine's nodes or the log's rounds
+    }
+    const uint32_t prev = (uint32_t)__shfl_up((int)b, 1u, 64);
+    const bool head = lane == 0u || b != prev;
+    const uint64_t H = __ballot(head);
+    const uint32_t s0 = 63u - (uint32_t)__builtin_clzll(H & mask_le);
+    const uint64_t above = H & ~mask_le;
+    const uint32_t s1 = above ? (uint32_t)__builtin_ctzll(above) - 1u : 63u;
+    const uint32_t incl = wave_incl_scan(nu, lane);
+    const uint32_t excl0 = (uint32_t)__shfl((int)(incl - nu), (int)s0, 64);
+    const uint32_t seg_upd = (uint32_t)__shfl((int)incl, (int)s1, 64) - excl0;
+    unsigned long long old = 0ull;
+    if (head && b != 0xFFFFFFFFu)
+      old = atomicAdd(&a.cnt[b], ((unsigned long long)(s1 - s0 + 1u) << kCntShift) | seg_upd);
+    old = __shfl(old, (int)s0, 64);
+    if (f < total) a.ekey[f] = b == 0xFFFFFFFFu ? kInvalid64 : ((uint64_t)b << 32) | ((old >> kCntShift) + (lane - s0));
+  }
+}
+
+// Scan sources over the buckets
+struct EntriesIn {
+  const unsigned long long* c;
+  __device__ uint64_t operator()(uint64_t i) const { return c[i] >> kCntShift; }
+};
+struct UpdatesIn {
+  const unsigned long long* c;
+  __device__ uint64_t operator()(uint64_t i) const { return c[i] & kUpdMask; }
+};
+struct GroupBytesIn {  // compact stream: 8-B group header + the codes, padded to 4 B
+  const unsigned long long* c;
+  uint32_t cw;
+  __device__ uint64_t operator()(uint64_t i) const {
+    const uint64_t n = c[i] & kUpdMask;
+    return n ? 8ull + ((n * cw + 3ull) & ~3ull) : 0ull;
+  }
+};
+
+// Scatter pass: refs[eoff[bucket] + rank] = kind << 62 | address.
+__global__ __launch_bounds__(kEncThreads) void k_bucket_scatter(EncArgs a, const uint64_t* eoff, uint64_t* refs) {
+  __shared__ uint64_t flat[kFlatMax];
+  const EncodeParams& p = a.p;
+  load_flat(flat, a.flat, p.shards);
+  const uint64_t total = flat[3u * p.shards];
+  for (uint64_t f = (uint64_t)blockIdx.x * kEncThreads + threadIdx.x; f < total;
+       f += (uint64_t)gridDim.x * kEncThreads) {
+    const uint64_t k = a.ekey[f];
+    if (k == kInvalid64) continue;
+    uint32_t kind;
+    uint64_t addr;
+    locate(flat, p.shards, f, kind, addr, p);
+    refs[eoff[k >> 32] + (k & 0xFFFFFFFFull)] = ((uint64_t)kind << 62) | addr;
+  }
+}
+
+// Position of the r-th (0-based) set bit of m (r < popcount(m)).
+__device__ __forceinline__ uint32_t nth_set(uint32_t m, uint32_t r) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 16; w >= 1; w >>= 1) {
+    const uint32_t low = m & ((1u << w) - 1u);
+    const uint32_t c = (uint32_t)__popc(low);
+    if (r >= c) {
+      r -= c;
+      m >>= w;
+      pos += w;
+    } else {
+      m = low;
+    }
+  }
+  return pos;
+}
+
+struct EmitArgs {
+  EncodeParams p;
+  const uint64_t* eoff;   // [B + 1]
+  const uint64_t* uoff;   // [B + 1]
+  const uint64_t* coff;   // [B + 1] (compact)
+  const uint64_t* refs;
+  uint32_t B;
+  uint32_t C;             // cells = K * BL
+  uint32_t* gtable;       // global tables (cells > kLdsCells): 4 * C u32 per workgroup, zeroed
+  uint64_t* out;          // packed words (at ubase + uoff[b])
+  uint8_t* cout;          // compact groups (at cbase + coff[b])
+  uint64_t ubase, cbase;
+};
+constexpr uint32_t kLdsCells = 4096;  // 64 KiB of LDS per wave
+
+template <bool G>
+__device__ __forceinline__ uint32_t tld(const uint32_t* p) {
+  if constexpr (G) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+
+// Medium / dense record or single word -> cells (slot, block): the update masks, status bit 1 (A after
+// the slot) and status bit 0 (~(A ^ died)) planes (vote.go:77-91: Rejected 1, Accepted 2, Invalid 0,
+// Finalized 3; A after slot j = A_final ^ parity of the later slots' updates).
+__device__ __forceinline__ void cell_or(uint32_t* msk, uint32_t* hi, uint32_t* lo, uint32_t cell, uint32_t e,
+                                        uint32_t h, uint32_t l) {
+  atomicOr(msk + cell, e);
+  if (h) atomicOr(hi + cell, h);
+  if (l) atomicOr(lo + cell, l);
+}
+
+__device__ __forceinline__ void fill_entry(const EncodeParams& p, uint64_t ref, uint32_t* msk, uint32_t* hi,
+                                           uint32_t* lo) {
+  const uint32_t kind = (uint32_t)(ref >> 62);
+  const uint64_t addr = ref & ((1ull << 62) - 1ull);
+  if (kind == 0) {
+    const uint64_t w = p.log[addr];
+    const uint32_t tl = (uint32_t)((w >> 2) & 0x3FFFFFu) - p.t0;
+    const uint32_t slot = (uint32_t)(w >> 24) & 15u, st = (uint32_t)w & 3u, m = 1u << (tl & 31u);
+    cell_or(msk, hi, lo, slot * p.BL + (tl >> 5), m, (st & 2u) ? m : 0u, (st & 1u) ? m : 0u);
+    return;
+  }
+  if (kind == 1) {
+#if AVK_MED_S4
+    const u32x4* q = reinterpret_cast<const u32x4*>(p.mlog + addr * med_rec_words());
+    const u32x4 a = q[0], b = q[1];
+    const uint32_t blk = ((a[0] >> 2) & 0x3FFFFFu) - p.t0;  // the key's target field: the block's first
+    const uint32_t S = a[2], A = a[3];
+    const bool hasd = (S & kMedS4Died) != 0u;
+    const uint32_t died = hasd ? b[3] : 0u;
+    const uint32_t E[4] = {b[0], b[1], b[2], hasd ? 0u : b[3]};
+    uint32_t slot[4] = {0u, 0u, 0u, 0u}, n = 0;
+    for (uint32_t m = S & 0xFFu; m && n < 4u; m &= m - 1u) slot[n++] = (uint32_t)__builtin_ctz(m);
+    uint32_t par = 0u;
+    for (int i = (int)n - 1; i >= 0; --i) {
+      const uint32_t aj = A ^ par, e = E[i];
+      par ^= e;
+      if (e) cell_or(msk, hi, lo, slot[i] * p.BL + (blk >> 5), e, aj & e, ~(aj ^ died) & e);
+    }
+#else
+    const uint64_t* r = p.mlog + addr * med_rec_words();
+    const uint64_t key = r[0], pl = r[1];
+    const uint32_t blk = (uint32_t)((key >> 2) & 0x3FFFFFu) - p.t0;
+    const uint32_t n = min((uint32_t)(pl & 15u), kMedMax);
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t fld = (uint32_t)(pl >> (4u + 10u * i)) & 1023u;
+      const uint32_t slot = fld >> 7, bit = (fld >> 2) & 31u, st = fld & 3u, m = 1u << bit;
+      cell_or(msk, hi, lo, slot * p.BL + (blk >> 5), m, (st & 2u) ? m : 0u, (st & 1u) ? m : 0u);
+    }
 #endif
     return;
   }
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(recs + i * dense_words(K));
-  uint32_t c = 0;
-  for (uint32_t j = 0; j < K; ++j) c += (uint32_t)__popc(w[2 + j]);
-  cnt[i] = c;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p.dlog + addr * dense_words(p.K));
+  const uint32_t blk = ((w[0] >> 2) & 0x3FFFFFu) - p.t0;
+  const uint32_t A = w[2 + p.K], died = w[3 + p.K];
+  uint32_t par = 0u;
+  for (int j = (int)p.K - 1; j >= 0; --j) {
+    const uint32_t aj = A ^ par, e = w[2 + j];
+    par ^= e;
+    if (e) cell_or(msk, hi, lo, (uint32_t)j * p.BL + (blk >> 5), e, aj & e, ~(aj ^ died) & e);
+  }
 }
 
-// Expand record i at out[off[i] ...] (off: exclusive scan of k_dense_counts).
-__global__ __launch_bounds__(256) void k_dense_expand(const uint64_t* recs, uint64_t n, uint32_t K,
-                                                      const uint64_t* off, uint64_t* out) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint64_t* dst = out + off[i];
-  for_each_rec(recs + i * rec_words(K), K, [&](uint64_t wd) { *dst++ = wd; });
+__device__ __forceinline__ void wave_sync(bool global_table) {
+  if (global_table) __threadfence();
+  __syncthreads();  // one wave per workgroup: a compiler and memory barrier, no cross-wave wait
+}
+
+// One 64-lane workgroup per bucket (grid-stride): its entries OR their updates into the bucket's
+// (slot, block) cells, a wave scan over the cells in canonical order (slot-major, block-minor) gives
+// each cell's first output position, and lane i writes updates i, i + 64, ... (cell by binary search
+// over the prefixes, target by the rank-th set bit of the cell's mask): every store coalesced.
+template <bool COMPACT, bool G>
+__global__ __launch_bounds__(64) void k_bucket_emit(EmitArgs a) {
+  extern __shared__ uint32_t sm[];
+  const EncodeParams& p = a.p;
+  const uint32_t C = a.C, lane = threadIdx.x;
+  uint32_t* tbl = G ? a.gtable + (size_t)blockIdx.x * 4u * C : sm;
+  uint32_t *msk = tbl, *hi = tbl + C, *lo = tbl + 2u * C, *pre = tbl + 3u * C;
+  if (!G) {
+    for (uint32_t c = lane; c < 3u * C; c += 64u) tbl[c] = 0u;
+    __syncthreads();
+  }
+  for (uint32_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    const uint64_t e0 = a.eoff[b], e1 = a.eoff[b + 1];
+    if (e0 == e1) continue;
+    const uint32_t nl = b % p.NL, rr = p.r0 + b / p.NL, node = p.n0 + nl;
+    for (uint64_t e = e0 + lane; e < e1; e += 64u) fill_entry(p, a.refs[e], msk, hi, lo);
+    wave_sync(G);
+    uint32_t run = 0;
+    for (uint32_t c0 = 0; c0 < C; c0 += 64u) {
+      const uint32_t c = c0 + lane;
+      const uint32_t cnt = c < C ? (uint32_t)__popc(tld<G>(msk + c)) : 0u;
+      const uint32_t incl = wave_incl_scan(cnt, lane);
+      if (c < C) pre[c] = run + incl - cnt;
+      run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+    // the bucket's counted updates (its output span): a mismatch is flagged, and no store leaves the span
+    const uint32_t want = (uint32_t)(a.uoff[b + 1] - a.uoff[b]);
+    if (run != want && lane == 0) atomicOr(p.err, 2u);
+    const uint32_t n = min(run, want);
+    wave_sync(G);
+    uint64_t* out = COMPACT ? nullptr : a.out + a.ubase + a.uoff[b];
+    uint8_t* grp = COMPACT ? a.cout + a.cbase + a.coff[b] : nullptr;
+    const uint64_t hi_word = ((uint64_t)rr << 52) | ((uint64_t)node << 28);
+    for (uint32_t i = lane; i < n; i += 64u) {
+      uint32_t l0 = 0, l1 = C - 1u;
+      while (l0 < l1) {
+        const uint32_t mid = (l0 + l1 + 1u) >> 1;
+        if (tld<G>(pre + mid) <= i) l0 = mid; else l1 = mid - 1u;
+      }
+      const uint32_t cell = l0;
+      const uint32_t bit = nth_set(tld<G>(msk + cell), i - tld<G>(pre + cell));
+      const uint32_t st = (((tld<G>(hi + cell) >> bit) & 1u) << 1) | ((tld<G>(lo + cell) >> bit) & 1u);
+      const uint32_t slot = cell / p.BL, tl = (cell - slot * p.BL) * 32u + bit;
+      if constexpr (COMPACT) {
+        const uint32_t code = (slot << (p.target_bits + 2u)) | (tl << 2) | st;
+        if (p.code_bytes == 2u) reinterpret_cast<uint16_t*>(grp + 8)[i] = (uint16_t)code;
+        else reinterpret_cast<uint32_t*>(grp + 8)[i] = code;
+      } else {
+        out[i] = hi_word | ((uint64_t)slot << 24) | ((uint64_t)(p.t0 + tl) << 2) | st;
+      }
+    }
+    if constexpr (COMPACT) {
+      if (lane == 0) {
+        reinterpret_cast<uint32_t*>(grp)[0] = node;
+        reinterpret_cast<uint32_t*>(grp)[1] = n;
+        if (p.code_bytes == 2u && (n & 1u)) reinterpret_cast<uint16_t*>(grp + 8)[n] = 0u;  // pad to 4 B
+      }
+    }
+    wave_sync(G);
+    for (uint32_t c = lane; c < 3u * C; c += 64u) tbl[c] = 0u;
+    wave_sync(G);
+  }
+}
+
+// Compact stream index: entry (round r0 + r, chunk c) = {byte offset of its first group from the groups'
+// start, updates before it}; the last pass also writes the end entry.
+__global__ void k_compact_index(const uint64_t* coff, const uint64_t* uoff, uint64_t* idx, uint32_t r0, uint32_t nr,
+                                uint32_t chunks, uint32_t chunk_nodes, uint32_t NL, uint64_t cbase, uint64_t ubase,
+                                uint32_t end_entry) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n = nr * chunks;
+  if (j < n) {
+    const uint32_t r = j / chunks, c = j - r * chunks;
+    const uint64_t b = (uint64_t)r * NL + (uint64_t)c * chunk_nodes;
+    const uint64_t at = ((uint64_t)(r0 + r) * chunks + c) * 2u;
+    idx[at] = cbase + coff[b];
+    idx[at + 1] = ubase + uoff[b];
+  } else if (j == n && end_entry) {
+    const uint64_t B = (uint64_t)nr * NL;
+    const uint64_t at = ((uint64_t)(r0 + nr) * chunks) * 2u;
+    idx[at] = cbase + coff[B];
+    idx[at + 1] = ubase + uoff[B];
+  }
 }
 
 }  // namespace
@@ -206,31 +524,141 @@ hipError_t launch_log_digest(const uint64_t* log, const uint32_t* counts, uint32
   return hipGetLastError();
 }
 
-hipError_t launch_dense_expand(const uint64_t* recs, uint64_t n, uint32_t k, uint64_t* counts_scratch,
-                               uint64_t* offsets, void* temp, size_t* temp_bytes, uint64_t* out, hipStream_t s) {
-  if (!temp) {  // size query for the scan
-    return hipcub::DeviceScan::ExclusiveSum(nullptr, *temp_bytes, counts_scratch, offsets, n, s);
-  }
-  if (!n) return hipSuccess;
-  const uint64_t blocks = (n + 255) / 256;
-  hipLaunchKernelGGL(k_dense_counts, dim3((uint32_t)blocks), dim3(256), 0, s, recs, n, k, counts_scratch);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  e = hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, counts_scratch, offsets, n, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_dense_expand, dim3((uint32_t)blocks), dim3(256), 0, s, recs, n, k, offsets, out);
-  return hipGetLastError();
-}
-
-hipError_t launch_sort_updates(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n,
-                               int begin_bit, int end_bit, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortKeys(temp, *temp_bytes, in, out, n, begin_bit, end_bit, s);
-}
-
+// ---- encoder scratch layout (u64 words) ----
 namespace {
-__global__ __launch_bounds__(256) void k_iota(uint32_t* out, uint32_t n) {
+struct EncLayout {
+  uint64_t flat, flat_sc, cnt, eoff, uoff, coff, bsc, ekey, refs, gtab, words;
+};
+EncLayout enc_layout(const EncodeParams& p, uint64_t entries, uint32_t B, uint32_t grid_g) {
+  EncLayout L{};
+  auto up = [](uint64_t w) { return (w + 31u) / 32u * 32u; };  // 256-B aligned regions
+  uint64_t at = 0;
+  L.flat = at;
+  at += up(kFlatMax);
+  L.flat_sc = at;
+  at += up(dscan::scan_scratch_words(3u * p.shards));
+  L.cnt = at;
+  at += up(B);
+  L.eoff = at;
+  at += up((uint64_t)B + 1u);
+  L.uoff = at;
+  at += up((uint64_t)B + 1u);
+  L.coff = at;
+  at += up((uint64_t)B + 1u);
+  L.bsc = at;
+  at += up(dscan::scan_scratch_words((uint64_t)B + 1u));
+  L.ekey = at;
+  at += up(entries);
+  L.refs = at;
+  at += up(entries);
+  L.gtab = at;
+  const uint64_t C = (uint64_t)p.K * p.BL;
+  at += C > kLdsCells ? up((uint64_t)grid_g * 4u * C / 2u + 1u) : 0u;
+  L.words = at;
+  return L;
+}
+uint32_t emit_global_grid(uint64_t cells) {
+  // global tables: 16 B per cell per workgroup, at most ~1 GiB of them
+  const uint64_t per = 16u * cells;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (1ull << 30) / per));
+}
+}  // namespace
+
+uint64_t encode_scratch_bytes(const EncodeParams& p, uint64_t entries, uint32_t B) {
+  return enc_layout(p, entries, B, emit_global_grid((uint64_t)p.K * p.BL)).words * 8u;
+}
+
+hipError_t launch_encode_log(const EncodeParams& p, uint64_t entries, void* scratch, uint64_t* out, uint8_t* cout,
+                             uint64_t* cidx, uint32_t chunks, uint32_t chunk_nodes, uint64_t ubase, uint64_t cbase,
+                             bool last_pass, uint64_t* totals, hipStream_t s) {
+  const uint32_t B = p.nr * p.NL;
+  const uint64_t C = (uint64_t)p.K * p.BL;
+  const bool G = C > kLdsCells;
+  const uint32_t gg = emit_global_grid(C);
+  const EncLayout L = enc_layout(p, entries, B, gg);
+  uint64_t* w = static_cast<uint64_t*>(scratch);
+  hipError_t e;
+  // flat entry offsets of the shards (device counters: no host round trip)
+  FlatIn fin{p.log_count, p.shards, p.log_cap, p.mlog_cap, p.dlog_cap};
+  if ((e = dscan::launch_scan(fin, 3u * p.shards, w + L.flat, w + L.flat_sc, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(w + L.cnt, 0, (size_t)B * 8u, s)) != hipSuccess) return e;
+  EncArgs ea{p, w + L.flat, reinterpret_cast<unsigned long long*>(w + L.cnt), w + L.ekey, B};
+  const uint32_t egrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((entries + kEncThreads - 1) / kEncThreads, 2048));
+  if (entries) {
+    hipLaunchKernelGGL(k_bucket_count, dim3(egrid), dim3(kEncThreads), 0, s, ea);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  const unsigned long long* cnt = reinterpret_cast<const unsigned long long*>(w + L.cnt);
+  if ((e = dscan::launch_scan(EntriesIn{cnt}, B, w + L.eoff, w + L.bsc, s)) != hipSuccess) return e;
+  if ((e = dscan::launch_scan(UpdatesIn{cnt}, B, w + L.uoff, w + L.bsc, s)) != hipSuccess) return e;
+  if (cout && (e = dscan::launch_scan(GroupBytesIn{cnt, p.code_bytes}, B, w + L.coff, w + L.bsc, s)) != hipSuccess)
+    return e;
+  if (entries) {
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(egrid), dim3(kEncThreads), 0, s, ea, (const uint64_t*)(w + L.eoff),
+                       w + L.refs);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  EmitArgs em{p, w + L.eoff, w + L.uoff, w + L.coff, w + L.refs, B, (uint32_t)C,
+              reinterpret_cast<uint32_t*>(w + L.gtab), out, cout, ubase, cbase};
+  if (entries && B) {
+    if (G) {
+      if ((e = hipMemsetAsync(w + L.gtab, 0, (size_t)gg * 16u * C, s)) != hipSuccess) return e;
+      const uint32_t grid = std::min<uint32_t>(B, gg);
+      if (cout)
+        hipLaunchKernelGGL((k_bucket_emit<true, true>), dim3(grid), dim3(64), 0, s, em);
+      else
+        hipLaunchKernelGGL((k_bucket_emit<false, true>), dim3(grid), dim3(64), 0, s, em);
+    } else {
+      const uint32_t grid = std::min<uint32_t>(B, 256u * 32u);
+      const size_t lds = (size_t)16u * C;
+      if (cout)
+        hipLaunchKernelGGL((k_bucket_emit<true, false>), dim3(grid), dim3(64), lds, s, em);
+      else
+        hipLaunchKernelGGL((k_bucket_emit<false, false>), dim3(grid), dim3(64), lds, s, em);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (cout && cidx) {
+    const uint32_t n = p.nr * chunks + 1u;
+    hipLaunchKernelGGL(k_compact_index, dim3((n + 255u) / 256u), dim3(256), 0, s, (const uint64_t*)(w + L.coff),
+                       (const uint64_t*)(w + L.uoff), cidx, p.r0, p.nr, chunks, chunk_nodes, p.NL, cbase, ubase,
+                       last_pass ? 1u : 0u);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  // this pass's totals: updates, compact bytes, entries grouped
+  if (totals) {
+    if ((e = hipMemcpyAsync(totals, w + L.uoff + B, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    if (cout && (e = hipMemcpyAsync(totals + 1, w + L.coff + B, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(totals + 2, w + L.eoff + B, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// Drop-in RegisterVotes batch (engine.cpp av_register_votes_batch): group the votes by lane (node,
+// 32-target block) keeping their order inside a lane — the stable radix sort of (lane, position) —
+// then run-length encode the sorted lanes into the (lanes, offs) CSR k_register_votes walks.
+// ---------------------------------------------------------------------------
+namespace {
+struct HeadsIn {
+  const uint32_t* k;
+  __device__ uint64_t operator()(uint64_t i) const { return (i == 0 || k[i] != k[i - 1]) ? 1u : 0u; }
+};
+// run r of the sorted keys: lanes[r] = its key, offs[r] = its first position; offs[n_runs] = n
+__global__ __launch_bounds__(256) void k_rle_write(const uint32_t* ks, const uint64_t* run_of, uint32_t n,
+                                                   uint32_t* lanes, uint32_t* offs, uint32_t* n_runs) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i < n) out[i] = i;
+  if (i >= n) return;
+  if (i == 0 || ks[i] != ks[i - 1]) {
+    const uint32_t r = (uint32_t)run_of[i];
+    lanes[r] = ks[i];
+    offs[r] = i;
+  }
+  if (i == n - 1u) {
+    const uint32_t nr = (uint32_t)run_of[n];
+    offs[nr] = n;
+    *n_runs = nr;
+  }
 }
 // entries[2i] = vote index, entries[2i+1] = packed vote (k_register_votes)
 __global__ __launch_bounds__(256) void k_vote_entries(const uint32_t* perm, const uint32_t* vidx, const uint32_t* info,
@@ -243,39 +671,25 @@ __global__ __launch_bounds__(256) void k_vote_entries(const uint32_t* perm, cons
 }
 }  // namespace
 
-// Drop-in RegisterVotes batch (engine.cpp av_register_votes_batch): group the
-// votes by lane (node, 32-target block) keeping their order inside a lane —
-// a stable radix sort of (lane, position) pairs — then run-length encode the
-// sorted lanes into the (lanes, offs) CSR k_register_votes walks. temp ==
-// nullptr: *temp_bytes = the scratch the three hipcub passes need.
-hipError_t launch_group_votes(void* temp, size_t* temp_bytes, const uint32_t* keys, const uint32_t* vidx,
-                              const uint32_t* info, uint32_t n, int key_bits, uint32_t* keys_s, uint32_t* perm,
-                              uint32_t* perm_s, uint32_t* lanes, uint32_t* counts, uint32_t* offs, uint32_t* n_runs,
-                              uint32_t* entries, hipStream_t s) {
-  size_t b_sort = 0, b_rle = 0, b_scan = 0;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, b_sort, keys, keys_s, perm, perm_s, n, 0, key_bits, s);
-  if (e == hipSuccess) e = hipcub::DeviceRunLengthEncode::Encode(nullptr, b_rle, keys_s, lanes, counts, n_runs, n, s);
-  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, b_scan, counts, offs, n + 1u, s);
+uint64_t group_votes_scratch_words(uint32_t n) {
+  return std::max<uint64_t>(dscan::radix_scratch_words(n), (uint64_t)n + 1u + dscan::scan_scratch_words((uint64_t)n + 1u));
+}
+
+hipError_t launch_group_votes(uint64_t* scratch, const uint32_t* keys, const uint32_t* vidx, const uint32_t* info,
+                              uint32_t n, int key_bits, uint32_t* keys_s, uint32_t* perm_s, uint32_t* keys_t,
+                              uint32_t* perm_t, uint32_t* lanes, uint32_t* offs, uint32_t* n_runs, uint32_t* entries,
+                              hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(n_runs, 0, 4, s);
+  hipError_t e = dscan::launch_radix_sort_pairs(keys, nullptr, n, key_bits, keys_s, perm_s, keys_t, perm_t, scratch, s);
   if (e != hipSuccess) return e;
-  const size_t need = std::max(b_sort, std::max(b_rle, b_scan));
-  if (!temp) {
-    *temp_bytes = need;
-    return hipSuccess;
-  }
-  if (*temp_bytes < need) return hipErrorInvalidValue;
+  // run index of every position: exclusive scan of the run heads (run_of[n] = runs)
+  uint64_t* run_of = scratch;
+  if ((e = dscan::launch_scan(HeadsIn{keys_s}, n, run_of, scratch + n + 1u, s)) != hipSuccess) return e;
   const uint32_t g = (n + 255u) / 256u;
-  hipLaunchKernelGGL(k_iota, dim3(g), dim3(256), 0, s, perm, n);
+  hipLaunchKernelGGL(k_rle_write, dim3(g), dim3(256), 0, s, (const uint32_t*)keys_s, (const uint64_t*)run_of, n,
+                     lanes, offs, n_runs);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  size_t t = need;
-  if ((e = hipcub::DeviceRadixSort::SortPairs(temp, t, keys, keys_s, perm, perm_s, n, 0, key_bits, s)) != hipSuccess) return e;
-  // counts has n + 1 slots: the runs' counts, then zeros, so that the scan's
-  // entry n_runs is the total (offs[n_runs] = n)
-  if ((e = hipMemsetAsync(counts, 0, (size_t)(n + 1u) * 4, s)) != hipSuccess) return e;
-  t = need;
-  if ((e = hipcub::DeviceRunLengthEncode::Encode(temp, t, keys_s, lanes, counts, n_runs, n, s)) != hipSuccess) return e;
-  t = need;
-  if ((e = hipcub::DeviceScan::ExclusiveSum(temp, t, counts, offs, n + 1u, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_vote_entries, dim3(g), dim3(256), 0, s, perm_s, vidx, info, n, entries);
+  hipLaunchKernelGGL(k_vote_entries, dim3(g), dim3(256), 0, s, (const uint32_t*)perm_s, vidx, info, n, entries);
   return hipGetLastError();
 }
 

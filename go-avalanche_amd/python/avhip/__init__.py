@@ -83,7 +83,8 @@ EXPORTED = [
     "av_peer_handles", "av_peer_init", "av_get_round", "av_set_round", "av_log_base_round", "av_updates_digest",
     "av_updates_digest_range", "av_read_pref_words", "av_set_polling",
     "av_register_votes_batch", "av_changed_words", "av_materialize", "av_peer_group_serial", "av_peer_sync",
-    "av_pushed_words", "av_log_entries", "av_resize_log",
+    "av_pushed_words", "av_log_entries", "av_resize_log", "av_fetch_compact", "av_fetch_compact_async",
+    "av_fetch_compact_wait", "av_compact_expand",
 ]
 
 _lib = None
@@ -156,6 +157,10 @@ def lib():
         "av_pushed_words": (i32, [_vp, P(i64)]),
         "av_log_entries": (i32, [_vp, _vp]),
         "av_resize_log": (i32, [_vp, _vp]),
+        "av_fetch_compact": (i32, [_vp, _vp, i64, P(i64)]),
+        "av_fetch_compact_async": (i32, [_vp, P(i64)]),
+        "av_fetch_compact_wait": (i32, [_vp, i64, P(_vp), P(i64)]),
+        "av_compact_expand": (i32, [_vp, i64, _vp, i64, P(i64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -192,6 +197,39 @@ def decode_updates(u: np.ndarray, base_round: int = 0) -> np.ndarray:
     out[:, 3] = ((u >> np.uint64(2)) & np.uint64(0x3FFFFF)).astype(np.int64)
     out[:, 4] = (u & np.uint64(3)).astype(np.int64)
     return out
+
+
+COMPACT_MAGIC = 0x31435641  # include/avhip.h AV_COMPACT_MAGIC
+COMPACT_HEADER = np.dtype([("magic", "<u4"), ("version", "<u4"), ("log_base", "<i8"), ("n_updates", "<i8"),
+                           ("bytes", "<i8"), ("node_base", "<i8"), ("target_base", "<i8"), ("n_rounds", "<i4"),
+                           ("chunks", "<i4"), ("chunk_nodes", "<i4"), ("code_bytes", "<i4"),
+                           ("target_bits", "<i4"), ("slot_bits", "<i4")])
+assert COMPACT_HEADER.itemsize == 72
+
+
+def compact_header(stream) -> dict:
+    """The av_compact_header of a compact StatusUpdate stream, as a dict."""
+    h = np.frombuffer(memoryview(stream)[:72], COMPACT_HEADER)[0]
+    return {k: int(h[k]) for k in COMPACT_HEADER.names}
+
+
+def compact_expand(stream) -> np.ndarray:
+    """av_compact_expand: a compact stream -> the packed update words av_fetch_updates returns."""
+    b = np.frombuffer(stream, np.uint8)
+    n = compact_header(b)["n_updates"]
+    out = np.zeros(max(n, 1), np.uint64)
+    got = C.c_int64(0)
+    _check(lib().av_compact_expand(_ptr(b), b.size, _ptr(out), out.size, C.byref(got)))
+    return out[: got.value]
+
+
+def compact_expand_into(stream, words: np.ndarray) -> int:
+    """av_compact_expand into the caller's uint64 buffer; returns the number of updates."""
+    assert words.dtype == np.uint64 and words.flags.c_contiguous
+    b = np.frombuffer(stream, np.uint8) if not isinstance(stream, np.ndarray) else stream
+    got = C.c_int64(0)
+    _check(lib().av_compact_expand(_ptr(b), b.size, _ptr(words), words.size, C.byref(got)))
+    return got.value
 
 
 def comm_unique_id() -> bytes:
@@ -239,6 +277,15 @@ class Engine:
         self.target_range = (cfg.target_begin, cfg.target_end) if target_range else (0, n_targets)
 
     def close(self):
+        """Destroy the engine; a member of a serial peer group takes the whole group with it (the
+        members store into each other's buffers: av_peer_group_serial)."""
+        group = getattr(self, "_group", None)
+        if group:
+            for e in group:
+                e._group = None
+            for e in group:
+                if e is not self:
+                    e.close()
         if getattr(self, "_h", None):
             lib().av_destroy(self._h)
             self._h = None
@@ -395,6 +442,39 @@ class Engine:
         got = C.c_int64(0)
         _check(lib().av_fetch_updates(self._h, _ptr(buf), buf.size, C.byref(got)))
         return got.value
+
+    def fetch_compact(self):
+        """All pending StatusUpdates as a compact stream (av_fetch_compact), as a uint8 array."""
+        need = C.c_int64(0)
+        rc = lib().av_fetch_compact(self._h, None, 0, C.byref(need))
+        if rc not in (AV_OK, AV_ERR_OVERFLOW):
+            _check(rc)
+        buf = np.zeros(max(need.value, 72), np.uint8)
+        got = C.c_int64(0)
+        _check(lib().av_fetch_compact(self._h, _ptr(buf), buf.size, C.byref(got)))
+        return buf[: got.value]
+
+    def fetch_compact_into(self, buf):
+        """av_fetch_compact into the caller's uint8 buffer; returns the stream's bytes."""
+        assert buf.dtype == np.uint8 and buf.flags.c_contiguous
+        got = C.c_int64(0)
+        _check(lib().av_fetch_compact(self._h, _ptr(buf), buf.size, C.byref(got)))
+        return got.value
+
+    def fetch_compact_async(self):
+        """av_fetch_compact_async: encode the pending updates, start their copy, clear the log; a ticket."""
+        t = C.c_int64(0)
+        _check(lib().av_fetch_compact_async(self._h, C.byref(t)))
+        return t.value
+
+    def fetch_compact_wait(self, ticket, copy=True):
+        """av_fetch_compact_wait: the ticket's stream. copy=False: a zero-copy view of the engine's
+        pinned buffer (valid until the fetch_compact_async call two tickets later)."""
+        p = _vp()
+        n = C.c_int64(0)
+        _check(lib().av_fetch_compact_wait(self._h, ticket, C.byref(p), C.byref(n)))
+        view = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n.value,))
+        return view.copy() if copy else view
 
     def updates_digest(self, n0=None, n1=None):
         """(count, sum, xor) of splitmix64 over the pending packed updates (not

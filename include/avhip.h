@@ -28,7 +28,11 @@
  *                          / Connman.NodesIDs net.go:25-31 replaced by
  *                          counter-RNG k-peer sampling)
  *   av_fetch_updates    <- the *[]StatusUpdate out-parameter     processor.go:61,111
- *                          (device-side canonical ordering: radix sort of the packed words)
+ *                          (device-side canonical ordering: counting sort by
+ *                          (round, node) + per-node (slot, target) layout)
+ *   av_fetch_compact[_async/_wait], av_compact_expand <- the same out-parameter
+ *                          as a compact stream (~2 B per update), pipelined
+ *                          with the next rounds
  */
 #ifndef AVHIP_H
 #define AVHIP_H
@@ -207,6 +211,55 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out);
 /* The round the pending log's round fields count from (the engine round at
  * the last fetch/discard): round of a fetched word = this + av_update_round_rel. */
 int av_log_base_round(av_engine* e, int64_t* out);
+
+/* ---- compact StatusUpdate stream (the same updates as av_fetch_updates, in the
+ * same canonical order, ~2 B per update instead of 8; processor.go:61,111) ----
+ * Layout (little-endian):
+ *   av_compact_header (72 B)
+ *   index: n_rounds * chunks + 1 entries of {uint64 byte offset of the entry's
+ *          first group from the start of the groups, uint64 updates before it};
+ *          entry r * chunks + c covers the groups of round log_base + r and
+ *          nodes [node_base + c * chunk_nodes, node_base + (c + 1) * chunk_nodes)
+ *   groups: one per (round, node) with >= 1 update, ascending (round, node):
+ *          uint32 node (global id), uint32 count, then count codes of
+ *          code_bytes each in (slot, target) order, zero-padded to 4 B;
+ *          code = slot << (target_bits + 2) | (target - target_base) << 2 | status
+ * av_compact_expand turns a stream back into av_fetch_updates' packed words. */
+#define AV_COMPACT_MAGIC 0x31435641u /* "AVC1" */
+#define AV_COMPACT_VERSION 1
+typedef struct {
+  uint32_t magic;
+  uint32_t version;
+  int64_t log_base;     /* round of the stream's round 0 */
+  int64_t n_updates;
+  int64_t bytes;        /* whole stream, header included */
+  int64_t node_base;
+  int64_t target_base;
+  int32_t n_rounds;
+  int32_t chunks;       /* index entries per round */
+  int32_t chunk_nodes;
+  int32_t code_bytes;   /* 2 or 4 */
+  int32_t target_bits;
+  int32_t slot_bits;
+} av_compact_header;
+/* Every pending update as a compact stream into out (cap bytes), clearing the
+ * log; AV_ERR_OVERFLOW with *bytes = the size needed (log kept) if cap is too
+ * small. */
+int av_fetch_compact(av_engine* e, void* out, int64_t cap, int64_t* bytes);
+/* Pipelined delivery: encode every pending update on the device (waiting for
+ * the rounds enqueued before), start its copy into engine-owned pinned host
+ * memory on a copy stream, clear the log and return at once with a ticket; the
+ * caller enqueues the next rounds while the copy runs. av_fetch_compact_wait
+ * blocks until that copy landed and returns the stream (engine memory, valid
+ * until the av_fetch_compact_async call two tickets later or av_destroy). At
+ * most two tickets are outstanding: the third call waits for the oldest copy. */
+int av_fetch_compact_async(av_engine* e, int64_t* ticket);
+int av_fetch_compact_wait(av_engine* e, int64_t ticket, const void** stream, int64_t* bytes);
+/* Host-side expansion of a compact stream into packed update words (the
+ * av_fetch_updates form; round fields relative to the header's log_base),
+ * multi-threaded. AV_ERR_OVERFLOW with *n_out = the count if cap is too small;
+ * AV_ERR_INVALID_ARG for a malformed stream. */
+int av_compact_expand(const void* stream, int64_t bytes, uint64_t* out, int64_t cap, int64_t* n_out);
 /* Order-independent digest of every pending StatusUpdate without fetching
  * (or clearing) them: out = {count, sum, xor} of splitmix64(packed word).
  * AV_ERR_OVERFLOW if the log overflowed. Full-size parity checks compare it
