@@ -284,18 +284,22 @@ struct av_engine {
   uint32_t* enc_err = nullptr;
   uint64_t* enc_tot = nullptr;  // [4]
   uint32_t enc_buckets = 1u << 26;  // option "enc_buckets": (round, node) buckets per encoder pass
-  // compact stream delivery (av_fetch_compact_async / _wait): two slots, each a device buffer the
-  // encoder writes and a pinned host buffer its copy lands in, the copy on copy_stream (overlaps the
-  // next rounds on the engine stream)
+  // option "copy_blocks": workgroups of the compact stream's device-to-host copy kernel (k_stream_out);
+  // 0 = hipMemcpyAsync (the runtime's copy)
+  uint32_t copy_blocks = 0;
+  // compact stream delivery (av_fetch_compact_async / _wait): kSlots slots, each a device buffer
+  // the encoder writes and a pinned host buffer its copy lands in, the copy on copy_stream (overlaps
+  // the next rounds on the engine stream); ticket t uses slot t % kSlots
+  static constexpr int kSlots = 3;
   hipStream_t copy_stream = nullptr;
-  void* cdev[2] = {nullptr, nullptr};
-  size_t cdev_bytes[2] = {0, 0};
-  void* chost[2] = {nullptr, nullptr};
-  size_t chost_bytes[2] = {0, 0};
-  hipEvent_t cev[2] = {nullptr, nullptr};
-  av_compact_header chdr[2] = {};
+  void* cdev[kSlots] = {};
+  size_t cdev_bytes[kSlots] = {};
+  void* chost[kSlots] = {};
+  size_t chost_bytes[kSlots] = {};
+  hipEvent_t cev[kSlots] = {};
+  av_compact_header chdr[kSlots] = {};
   int64_t cticket = 0;           // next ticket
-  bool cpend[2] = {false, false};  // a copy was issued into the slot
+  bool cpend[kSlots] = {};       // a copy was issued into the slot
   // batched poll sets (av_get_invs_batch): host-mapped pinned output the fill kernel writes
   void* invs_host = nullptr;
   size_t invs_host_bytes = 0;
@@ -1065,7 +1069,7 @@ int av_destroy(av_engine* e) {
     (void)hipStreamSynchronize(e->copy_stream);
     (void)hipStreamDestroy(e->copy_stream);
   }
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < av_engine::kSlots; ++i) {
     if (e->cdev[i]) (void)hipFree(e->cdev[i]);
     if (e->chost[i]) (void)hipHostFree(e->chost[i]);
     if (e->cev[i]) (void)hipEventDestroy(e->cev[i]);
@@ -2145,7 +2149,7 @@ int grow_pinned(void** p, size_t* have, size_t want) {
   *p = nullptr;
   *have = 0;
   want = std::max(want + want / 8, (size_t)1 << 20);
-  AV_HIP(hipHostMalloc(p, want, hipHostMallocDefault));
+  AV_HIP(hipHostMalloc(p, want, hipHostMallocMapped));
   *have = want;
   return AV_OK;
 }
@@ -2218,12 +2222,12 @@ int av_fetch_compact_async(av_engine* e, int64_t* ticket) {
   AV_PEER_SYNC_CHECK(e);
   AV_CHECK(ticket, AV_ERR_INVALID_ARG, "null argument");
   if (!e->copy_stream) AV_HIP(hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
-  const int s = (int)(e->cticket & 1);
+  const int s = (int)(e->cticket % av_engine::kSlots);
   if (!e->cev[s]) AV_HIP(hipEventCreateWithFlags(&e->cev[s], hipEventDisableTiming));
   LogCounts c;
   int rc = pending_counts(e, c);  // waits for the rounds enqueued before
   if (rc != AV_OK) return rc;
-  // the slot's previous copy (ticket - 2) has read its device buffer and filled its host buffer
+  // the slot's previous copy (ticket - kSlots) has read its device buffer and filled its host buffer
   if (e->cpend[s]) AV_HIP(hipEventSynchronize(e->cev[s]));
   e->cpend[s] = false;
   const avk::EncodeParams p = encode_params(e);
@@ -2232,10 +2236,17 @@ int av_fetch_compact_async(av_engine* e, int64_t* ticket) {
   Encoded r;
   rc = encode_log(e, c, true, e->cdev[s], &r);  // synchronizes the engine stream
   if (rc != AV_OK) return rc;
-  rc = grow_pinned(&e->chost[s], &e->chost_bytes[s], (size_t)r.bytes);
+  rc = grow_pinned(&e->chost[s], &e->chost_bytes[s], (size_t)r.bytes + 16);
   if (rc != AV_OK) return rc;
-  AV_HIP(hipMemcpyAsync(static_cast<uint8_t*>(e->chost[s]) + kHdrBytes, static_cast<const uint8_t*>(e->cdev[s]) + kHdrBytes,
-                        (size_t)r.bytes - kHdrBytes, hipMemcpyDeviceToHost, e->copy_stream));
+  if (e->copy_blocks) {  // a small copy kernel (the header's bytes are copied too, and overwritten on wait)
+    void* hdev = nullptr;
+    AV_HIP(hipHostGetDevicePointer(&hdev, e->chost[s], 0));
+    AV_HIP(avk::launch_stream_out(e->cdev[s], hdev, (uint64_t)r.bytes, e->copy_blocks, e->copy_stream));
+  } else {
+    AV_HIP(hipMemcpyAsync(static_cast<uint8_t*>(e->chost[s]) + kHdrBytes,
+                          static_cast<const uint8_t*>(e->cdev[s]) + kHdrBytes, (size_t)r.bytes - kHdrBytes,
+                          hipMemcpyDeviceToHost, e->copy_stream));
+  }
   AV_HIP(hipEventRecord(e->cev[s], e->copy_stream));
   e->chdr[s] = r.hdr;
   e->cpend[s] = true;
@@ -2246,9 +2257,9 @@ int av_fetch_compact_async(av_engine* e, int64_t* ticket) {
 int av_fetch_compact_wait(av_engine* e, int64_t ticket, const void** stream, int64_t* bytes) {
   AV_ENTER(e);
   AV_CHECK(stream && bytes, AV_ERR_INVALID_ARG, "null argument");
-  AV_CHECK(ticket >= 0 && ticket < e->cticket && ticket >= e->cticket - 2, AV_ERR_INVALID_ARG,
-           "ticket %lld is not one of the last two issued", (long long)ticket);
-  const int s = (int)(ticket & 1);
+  AV_CHECK(ticket >= 0 && ticket < e->cticket && ticket >= e->cticket - av_engine::kSlots, AV_ERR_INVALID_ARG,
+           "ticket %lld is not one of the last %d issued", (long long)ticket, av_engine::kSlots);
+  const int s = (int)(ticket % av_engine::kSlots);
   AV_CHECK(e->cpend[s], AV_ERR_INVALID_ARG, "ticket %lld has no copy", (long long)ticket);
   AV_HIP(hipEventSynchronize(e->cev[s]));
   std::memcpy(e->chost[s], &e->chdr[s], kHdrBytes);
@@ -2617,6 +2628,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     }
     e->solo_barrier = value != 0;
     e->solo_used = e->solo_used || e->solo_barrier;
+  } else if (n == "copy_blocks") {
+    AV_CHECK(value >= 0 && value <= 4096, AV_ERR_INVALID_ARG, "copy_blocks must be in [0, 4096]");
+    e->copy_blocks = (uint32_t)value;
   } else if (n == "enc_buckets") {  // (round, node) buckets per encoder pass (tests of the multi-pass path)
     AV_CHECK(value >= 1 && value <= (1ll << 30), AV_ERR_INVALID_ARG, "enc_buckets must be in [1, 2^30]");
     e->enc_buckets = (uint32_t)value;

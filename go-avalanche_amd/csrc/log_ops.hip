@@ -342,12 +342,12 @@ struct EmitArgs {
   const uint64_t* refs;
   uint32_t B;
   uint32_t C;             // cells = K * BL
-  uint32_t* gtable;       // global tables (cells > kLdsCells): 4 * C u32 per workgroup, zeroed
+  uint32_t* gtable;       // global tables (cells > kLdsCells): 3 * C u32 per wave, zeroed
   uint64_t* out;          // packed words (at ubase + uoff[b])
   uint8_t* cout;          // compact groups (at cbase + coff[b])
   uint64_t ubase, cbase;
 };
-constexpr uint32_t kLdsCells = 4096;  // 64 KiB of LDS per wave
+constexpr uint32_t kLdsCells = 4096;  // 48 KiB of LDS per wave
 
 template <bool G>
 __device__ __forceinline__ uint32_t tld(const uint32_t* p) {
@@ -365,128 +365,240 @@ __device__ __forceinline__ void cell_or(uint32_t* msk, uint32_t* hi, uint32_t* l
   if (l) atomicOr(lo + cell, l);
 }
 
-__device__ __forceinline__ void fill_entry(const EncodeParams& p, uint64_t ref, uint32_t* msk, uint32_t* hi,
-                                           uint32_t* lo) {
-  const uint32_t kind = (uint32_t)(ref >> 62);
+// A log entry's updates as per-slot masks in registers: no array is indexed at run time, so nothing
+// lives in scratch memory (a scratch access is a vector-memory operation, and the wave's one in-order
+// vector-memory counter would make every such load wait behind the wave's output stores).
+struct RecRegs {
+  uint32_t kind;  // 0 single word, 1 slot (medium) record, 2 dense record
+  uint32_t key;   // low half of the key word (a single: of the update word: slot, target, status)
+  uint32_t E[8];  // updated records per slot (k <= 8); folded medium records (AVK_MED_S4 = 0): payload
+  uint32_t A, died;
+};
+
+__device__ __forceinline__ uint32_t pick4(uint32_t i, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return i == 0u ? a : i == 1u ? b : i == 2u ? c : d;
+}
+
+// k <= 8 only (E[8])
+__device__ __forceinline__ void load_rec(const EncodeParams& p, uint64_t ref, RecRegs& r) {
+  r.kind = (uint32_t)(ref >> 62);
   const uint64_t addr = ref & ((1ull << 62) - 1ull);
-  if (kind == 0) {
-    const uint64_t w = p.log[addr];
-    const uint32_t tl = (uint32_t)((w >> 2) & 0x3FFFFFu) - p.t0;
-    const uint32_t slot = (uint32_t)(w >> 24) & 15u, st = (uint32_t)w & 3u, m = 1u << (tl & 31u);
+  r.A = r.died = 0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r.E[j] = 0u;
+  if (r.kind == 0u) {
+    r.key = (uint32_t)p.log[addr];
+  } else if (r.kind == 1u) {
+#if AVK_MED_S4
+    const u32x4* q = reinterpret_cast<const u32x4*>(p.mlog + addr * med_rec_words());
+    const u32x4 x = q[0], y = q[1];
+    r.key = x[0];
+    const uint32_t S = x[2];
+    r.A = x[3];
+    const bool hasd = (S & kMedS4Died) != 0u;
+    r.died = hasd ? y[3] : 0u;
+    const uint32_t nw = hasd ? 3u : 4u;  // E words stored, in slot order
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i = (uint32_t)__popc(S & ((1u << j) - 1u));
+      r.E[j] = ((S >> j) & 1u) && i < nw ? pick4(i, y[0], y[1], y[2], y[3]) : 0u;
+    }
+#else
+    const uint64_t* q = p.mlog + addr * med_rec_words();
+    const uint64_t k0 = q[0], pl = q[1];
+    r.key = (uint32_t)k0;
+    r.E[0] = (uint32_t)pl;
+    r.E[1] = (uint32_t)(pl >> 32);
+#endif
+  } else {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p.dlog + addr * dense_words(p.K));
+    r.key = w[0];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if ((uint32_t)j < p.K) r.E[j] = w[2 + j];
+    r.A = w[2 + p.K];
+    r.died = w[3 + p.K];
+  }
+}
+
+__device__ __forceinline__ void fill_regs(const EncodeParams& p, const RecRegs& r, uint32_t* msk, uint32_t* hi,
+                                          uint32_t* lo) {
+  if (r.kind == 0u) {
+    const uint32_t tl = ((r.key >> 2) & 0x3FFFFFu) - p.t0;
+    const uint32_t slot = (r.key >> 24) & 15u, st = r.key & 3u, m = 1u << (tl & 31u);
     cell_or(msk, hi, lo, slot * p.BL + (tl >> 5), m, (st & 2u) ? m : 0u, (st & 1u) ? m : 0u);
     return;
   }
-  if (kind == 1) {
-#if AVK_MED_S4
-    const u32x4* q = reinterpret_cast<const u32x4*>(p.mlog + addr * med_rec_words());
-    const u32x4 a = q[0], b = q[1];
-    const uint32_t blk = ((a[0] >> 2) & 0x3FFFFFu) - p.t0;  // the key's target field: the block's first
-    const uint32_t S = a[2], A = a[3];
-    const bool hasd = (S & kMedS4Died) != 0u;
-    const uint32_t died = hasd ? b[3] : 0u;
-    const uint32_t E[4] = {b[0], b[1], b[2], hasd ? 0u : b[3]};
-    uint32_t slot[4] = {0u, 0u, 0u, 0u}, n = 0;
-    for (uint32_t m = S & 0xFFu; m && n < 4u; m &= m - 1u) slot[n++] = (uint32_t)__builtin_ctz(m);
-    uint32_t par = 0u;
-    for (int i = (int)n - 1; i >= 0; --i) {
-      const uint32_t aj = A ^ par, e = E[i];
-      par ^= e;
-      if (e) cell_or(msk, hi, lo, slot[i] * p.BL + (blk >> 5), e, aj & e, ~(aj ^ died) & e);
-    }
-#else
-    const uint64_t* r = p.mlog + addr * med_rec_words();
-    const uint64_t key = r[0], pl = r[1];
-    const uint32_t blk = (uint32_t)((key >> 2) & 0x3FFFFFu) - p.t0;
+  const uint32_t blk = (((r.key >> 2) & 0x3FFFFFu) - p.t0) >> 5;  // the key's target field: the block's first
+#if !AVK_MED_S4
+  if (r.kind == 1u) {
+    const uint64_t pl = (uint64_t)r.E[0] | ((uint64_t)r.E[1] << 32);
     const uint32_t n = min((uint32_t)(pl & 15u), kMedMax);
     for (uint32_t i = 0; i < n; ++i) {
       const uint32_t fld = (uint32_t)(pl >> (4u + 10u * i)) & 1023u;
       const uint32_t slot = fld >> 7, bit = (fld >> 2) & 31u, st = fld & 3u, m = 1u << bit;
-      cell_or(msk, hi, lo, slot * p.BL + (blk >> 5), m, (st & 2u) ? m : 0u, (st & 1u) ? m : 0u);
+      cell_or(msk, hi, lo, slot * p.BL + blk, m, (st & 2u) ? m : 0u, (st & 1u) ? m : 0u);
     }
-#endif
     return;
   }
+#endif
+  uint32_t par = 0u;  // A after slot j = A_final ^ parity of the later slots' updates (vote.go:77-91)
+#pragma unroll
+  for (int j = 7; j >= 0; --j) {
+    const uint32_t aj = r.A ^ par, e = r.E[j];
+    par ^= e;
+    if (e) cell_or(msk, hi, lo, (uint32_t)j * p.BL + blk, e, aj & e, ~(aj ^ r.died) & e);
+  }
+}
+
+__device__ __forceinline__ void fill_entry(const EncodeParams& p, uint64_t ref, uint32_t* msk, uint32_t* hi,
+                                           uint32_t* lo) {
+  if (p.K <= 8u || (ref >> 62) != 2u) {  // (medium records exist at k <= 8 only)
+    RecRegs r;
+    load_rec(p, ref, r);
+    fill_regs(p, r, msk, hi, lo);
+    return;
+  }
+  // dense record at k > 8: the slot masks straight from memory
+  const uint64_t addr = ref & ((1ull << 62) - 1ull);
   const uint32_t* w = reinterpret_cast<const uint32_t*>(p.dlog + addr * dense_words(p.K));
-  const uint32_t blk = ((w[0] >> 2) & 0x3FFFFFu) - p.t0;
+  const uint32_t blk = (((w[0] >> 2) & 0x3FFFFFu) - p.t0) >> 5;
   const uint32_t A = w[2 + p.K], died = w[3 + p.K];
   uint32_t par = 0u;
   for (int j = (int)p.K - 1; j >= 0; --j) {
     const uint32_t aj = A ^ par, e = w[2 + j];
     par ^= e;
-    if (e) cell_or(msk, hi, lo, (uint32_t)j * p.BL + (blk >> 5), e, aj & e, ~(aj ^ died) & e);
+    if (e) cell_or(msk, hi, lo, (uint32_t)j * p.BL + blk, e, aj & e, ~(aj ^ died) & e);
   }
 }
 
-__device__ __forceinline__ void wave_sync(bool global_table) {
-  if (global_table) __threadfence();
-  __syncthreads();  // one wave per workgroup: a compiler and memory barrier, no cross-wave wait
+// The waves of a workgroup work on different buckets: wave-level ordering only. LDS operations of one
+// wave execute in issue order, so waiting for the wave's own LDS operations (lgkmcnt) and keeping the
+// compiler from moving memory operations across is enough — no vmcnt wait: the output stores and the
+// next bucket's loads stay in flight (a workgroup fence or barrier would wait for them every time).
+// Global tables (rare: > 4096 cells) take a device fence.
+template <bool G>
+__device__ __forceinline__ void wave_sync() {
+  if constexpr (G) {
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
 }
 
-// One 64-lane workgroup per bucket (grid-stride): its entries OR their updates into the bucket's
-// (slot, block) cells, a wave scan over the cells in canonical order (slot-major, block-minor) gives
-// each cell's first output position, and lane i writes updates i, i + 64, ... (cell by binary search
-// over the prefixes, target by the rank-th set bit of the cell's mask): every store coalesced.
+// One wave per bucket (grid-stride over buckets, several independent waves per workgroup): its
+// entries OR their updates into the bucket's (slot, block) cells in LDS, then one pass over the cells
+// in canonical order (slot-major, block-minor) writes them out. The next bucket's offsets, first 64
+// entry refs and their record words (k <= 8) are loaded while this bucket is laid out.
 template <bool COMPACT, bool G>
-__global__ __launch_bounds__(64) void k_bucket_emit(EmitArgs a) {
+__global__ __launch_bounds__(256) void k_bucket_emit(EmitArgs a) {
   extern __shared__ uint32_t sm[];
   const EncodeParams& p = a.p;
-  const uint32_t C = a.C, lane = threadIdx.x;
-  uint32_t* tbl = G ? a.gtable + (size_t)blockIdx.x * 4u * C : sm;
-  uint32_t *msk = tbl, *hi = tbl + C, *lo = tbl + 2u * C, *pre = tbl + 3u * C;
+  const uint32_t C = a.C, lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, W = blockDim.x >> 6;
+  const uint32_t gw = blockIdx.x * W + wv, gstride = gridDim.x * W;
+  uint32_t* tbl = G ? a.gtable + (size_t)gw * 3u * C : sm + (size_t)wv * 3u * C;
+  uint32_t *msk = tbl, *hi = tbl + C, *lo = tbl + 2u * C;
   if (!G) {
     for (uint32_t c = lane; c < 3u * C; c += 64u) tbl[c] = 0u;
-    __syncthreads();
+    wave_sync<G>();
   }
-  for (uint32_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    const uint64_t e0 = a.eoff[b], e1 = a.eoff[b + 1];
-    if (e0 == e1) continue;
-    const uint32_t nl = b % p.NL, rr = p.r0 + b / p.NL, node = p.n0 + nl;
-    for (uint64_t e = e0 + lane; e < e1; e += 64u) fill_entry(p, a.refs[e], msk, hi, lo);
-    wave_sync(G);
-    uint32_t run = 0;
-    for (uint32_t c0 = 0; c0 < C; c0 += 64u) {
-      const uint32_t c = c0 + lane;
-      const uint32_t cnt = c < C ? (uint32_t)__popc(tld<G>(msk + c)) : 0u;
-      const uint32_t incl = wave_incl_scan(cnt, lane);
-      if (c < C) pre[c] = run + incl - cnt;
-      run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  const bool pref = p.K <= 8u;  // record words fit RecRegs
+  uint32_t b = gw;
+  uint64_t e0 = 0, e1 = 0, ref = 0;
+  RecRegs rr_cur{};
+  if (b < a.B) {
+    e0 = a.eoff[b];
+    e1 = a.eoff[b + 1];
+    if (lane < e1 - e0) {
+      ref = a.refs[e0 + lane];
+      if (pref) load_rec(p, ref, rr_cur);
     }
-    // the bucket's counted updates (its output span): a mismatch is flagged, and no store leaves the span
-    const uint32_t want = (uint32_t)(a.uoff[b + 1] - a.uoff[b]);
-    if (run != want && lane == 0) atomicOr(p.err, 2u);
-    const uint32_t n = min(run, want);
-    wave_sync(G);
-    uint64_t* out = COMPACT ? nullptr : a.out + a.ubase + a.uoff[b];
-    uint8_t* grp = COMPACT ? a.cout + a.cbase + a.coff[b] : nullptr;
-    const uint64_t hi_word = ((uint64_t)rr << 52) | ((uint64_t)node << 28);
-    for (uint32_t i = lane; i < n; i += 64u) {
-      uint32_t l0 = 0, l1 = C - 1u;
-      while (l0 < l1) {
-        const uint32_t mid = (l0 + l1 + 1u) >> 1;
-        if (tld<G>(pre + mid) <= i) l0 = mid; else l1 = mid - 1u;
+  }
+  while (b < a.B) {
+    const uint32_t nb = b + gstride;
+    uint64_t ne0 = 0, ne1 = 0;
+    if (nb < a.B) {  // issued now, used after this bucket's fill
+      ne0 = a.eoff[nb];
+      ne1 = a.eoff[nb + 1];
+    }
+    uint64_t nref = 0;
+    RecRegs rr_next{};
+    if (e0 != e1) {
+      const uint64_t u0 = a.uoff[b], u1 = a.uoff[b + 1];
+      const uint64_t c0b = COMPACT ? a.coff[b] : 0ull;
+      const uint32_t nl = b % p.NL, rnd = p.r0 + b / p.NL, node = p.n0 + nl;
+      if (lane < e1 - e0) {
+        if (pref) fill_regs(p, rr_cur, msk, hi, lo);
+        else fill_entry(p, ref, msk, hi, lo);
       }
-      const uint32_t cell = l0;
-      const uint32_t bit = nth_set(tld<G>(msk + cell), i - tld<G>(pre + cell));
-      const uint32_t st = (((tld<G>(hi + cell) >> bit) & 1u) << 1) | ((tld<G>(lo + cell) >> bit) & 1u);
-      const uint32_t slot = cell / p.BL, tl = (cell - slot * p.BL) * 32u + bit;
+      for (uint64_t e = e0 + 64u + lane; e < e1; e += 64u) fill_entry(p, a.refs[e], msk, hi, lo);
+      if (nb < a.B && lane < ne1 - ne0) {  // the next bucket's refs and records, in flight from here
+        nref = a.refs[ne0 + lane];
+        if (pref) load_rec(p, nref, rr_next);
+      }
+      wave_sync<G>();
+      // one pass over the cells in canonical order (slot-major, block-minor): lane = cell within each
+      // chunk of 64, its first output position from a wave scan of the counts, its updates written in
+      // ascending target (stores of one instruction land within the bucket's few output lines); the
+      // cell's one reader clears it for the next bucket
+      const uint32_t want = (uint32_t)(u1 - u0);
+      uint64_t* out = COMPACT ? nullptr : a.out + a.ubase + u0;
+      uint8_t* grp = COMPACT ? a.cout + a.cbase + c0b : nullptr;
+      const uint64_t hi_word = ((uint64_t)rnd << 52) | ((uint64_t)node << 28);
+      uint32_t run = 0;
+      for (uint32_t c0 = 0; c0 < C; c0 += 64u) {
+        const uint32_t c = c0 + lane;
+        uint32_t m = 0u, h = 0u, l = 0u;
+        if (c < C) {
+          m = tld<G>(msk + c);
+          if (m) {
+            h = tld<G>(hi + c);
+            l = tld<G>(lo + c);
+            msk[c] = 0u;
+            hi[c] = 0u;
+            lo[c] = 0u;
+          }
+        }
+        const uint32_t cnt = (uint32_t)__popc(m);
+        const uint32_t incl = wave_incl_scan(cnt, lane);
+        if (m) {
+          uint32_t pos = run + incl - cnt;
+          const uint32_t slot = c / p.BL, tb = (c - slot * p.BL) * 32u;
+          for (; m; m &= m - 1u, ++pos) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(m);
+            const uint32_t st = (((h >> bit) & 1u) << 1) | ((l >> bit) & 1u);
+            if (pos >= want) continue;  // a count mismatch (flagged below): no store leaves the span
+            if constexpr (COMPACT) {
+              const uint32_t code = (slot << (p.target_bits + 2u)) | ((tb + bit) << 2) | st;
+              if (p.code_bytes == 2u) reinterpret_cast<uint16_t*>(grp + 8)[pos] = (uint16_t)code;
+              else reinterpret_cast<uint32_t*>(grp + 8)[pos] = code;
+            } else {
+              out[pos] = hi_word | ((uint64_t)slot << 24) | ((uint64_t)(p.t0 + tb + bit) << 2) | st;
+            }
+          }
+        }
+        run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      }
+      if (run != want && lane == 0) atomicOr(p.err, 2u);
+      const uint32_t n = min(run, want);
       if constexpr (COMPACT) {
-        const uint32_t code = (slot << (p.target_bits + 2u)) | (tl << 2) | st;
-        if (p.code_bytes == 2u) reinterpret_cast<uint16_t*>(grp + 8)[i] = (uint16_t)code;
-        else reinterpret_cast<uint32_t*>(grp + 8)[i] = code;
-      } else {
-        out[i] = hi_word | ((uint64_t)slot << 24) | ((uint64_t)(p.t0 + tl) << 2) | st;
+        if (lane == 0) {
+          reinterpret_cast<uint32_t*>(grp)[0] = node;
+          reinterpret_cast<uint32_t*>(grp)[1] = n;
+          if (p.code_bytes == 2u && (n & 1u)) reinterpret_cast<uint16_t*>(grp + 8)[n] = 0u;  // pad to 4 B
+        }
       }
+      wave_sync<G>();
+    } else if (nb < a.B && lane < ne1 - ne0) {
+      nref = a.refs[ne0 + lane];
+      if (pref) load_rec(p, nref, rr_next);
     }
-    if constexpr (COMPACT) {
-      if (lane == 0) {
-        reinterpret_cast<uint32_t*>(grp)[0] = node;
-        reinterpret_cast<uint32_t*>(grp)[1] = n;
-        if (p.code_bytes == 2u && (n & 1u)) reinterpret_cast<uint16_t*>(grp + 8)[n] = 0u;  // pad to 4 B
-      }
-    }
-    wave_sync(G);
-    for (uint32_t c = lane; c < 3u * C; c += 64u) tbl[c] = 0u;
-    wave_sync(G);
+    b = nb;
+    e0 = ne0;
+    e1 = ne1;
+    ref = nref;
+    rr_cur = rr_next;
   }
 }
 
@@ -553,13 +665,13 @@ EncLayout enc_layout(const EncodeParams& p, uint64_t entries, uint32_t B, uint32
   at += up(entries);
   L.gtab = at;
   const uint64_t C = (uint64_t)p.K * p.BL;
-  at += C > kLdsCells ? up((uint64_t)grid_g * 4u * C / 2u + 1u) : 0u;
+  at += C > kLdsCells ? up((uint64_t)grid_g * 3u * C / 2u + 1u) : 0u;
   L.words = at;
   return L;
 }
 uint32_t emit_global_grid(uint64_t cells) {
-  // global tables: 16 B per cell per workgroup, at most ~1 GiB of them
-  const uint64_t per = 16u * cells;
+  // global tables: 12 B per cell per wave, at most ~1 GiB of them
+  const uint64_t per = 12u * cells;
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (1ull << 30) / per));
 }
 }  // namespace
@@ -602,19 +714,22 @@ hipError_t launch_encode_log(const EncodeParams& p, uint64_t entries, void* scra
               reinterpret_cast<uint32_t*>(w + L.gtab), out, cout, ubase, cbase};
   if (entries && B) {
     if (G) {
-      if ((e = hipMemsetAsync(w + L.gtab, 0, (size_t)gg * 16u * C, s)) != hipSuccess) return e;
-      const uint32_t grid = std::min<uint32_t>(B, gg);
+      if ((e = hipMemsetAsync(w + L.gtab, 0, (size_t)gg * 12u * C, s)) != hipSuccess) return e;
+      const uint32_t wpg = gg >= 4u ? 4u : 1u;  // waves per workgroup (each with its own table)
+      const uint32_t grid = (uint32_t)std::min<uint64_t>((B + wpg - 1u) / wpg, gg / wpg);
       if (cout)
-        hipLaunchKernelGGL((k_bucket_emit<true, true>), dim3(grid), dim3(64), 0, s, em);
+        hipLaunchKernelGGL((k_bucket_emit<true, true>), dim3(grid), dim3(64u * wpg), 0, s, em);
       else
-        hipLaunchKernelGGL((k_bucket_emit<false, true>), dim3(grid), dim3(64), 0, s, em);
+        hipLaunchKernelGGL((k_bucket_emit<false, true>), dim3(grid), dim3(64u * wpg), 0, s, em);
     } else {
-      const uint32_t grid = std::min<uint32_t>(B, 256u * 32u);
-      const size_t lds = (size_t)16u * C;
+      // waves per workgroup: 4 while their tables fit 48 KiB (C <= 1024), fewer for larger tables
+      const uint32_t wpg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(4, kLdsCells / C));
+      const uint32_t grid = (uint32_t)std::min<uint64_t>((B + wpg - 1u) / wpg, 256u * 32u / wpg);
+      const size_t lds = (size_t)12u * C * wpg;
       if (cout)
-        hipLaunchKernelGGL((k_bucket_emit<true, false>), dim3(grid), dim3(64), lds, s, em);
+        hipLaunchKernelGGL((k_bucket_emit<true, false>), dim3(grid), dim3(64u * wpg), lds, s, em);
       else
-        hipLaunchKernelGGL((k_bucket_emit<false, false>), dim3(grid), dim3(64), lds, s, em);
+        hipLaunchKernelGGL((k_bucket_emit<false, false>), dim3(grid), dim3(64u * wpg), lds, s, em);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
@@ -632,6 +747,36 @@ hipError_t launch_encode_log(const EncodeParams& p, uint64_t entries, void* scra
     if ((e = hipMemcpyAsync(totals + 2, w + L.eoff + B, 8, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+// Device -> host-mapped pinned memory copy on a few workgroups (the compact stream's copy beside the
+// next rounds): PCIe writes need only a few hundred KiB in flight, so a small grid saturates the link
+// and leaves the CUs to the round kernel (the runtime's blit copy takes a full grid). Four 16-B loads
+// in flight per thread, then their stores.
+namespace {
+__global__ __launch_bounds__(256) void k_stream_out(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                    uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256u;
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  for (; i + 3u * stride < n16; i += 4u * stride) {
+    const u32x4 a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + stride);
+    const u32x4 c = __builtin_nontemporal_load(src + i + 2u * stride), d = __builtin_nontemporal_load(src + i + 3u * stride);
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2u * stride] = c;
+    dst[i + 3u * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
+}
+}  // namespace
+
+hipError_t launch_stream_out(const void* src, void* dst, uint64_t bytes, uint32_t blocks, hipStream_t s) {
+  const uint64_t n16 = (bytes + 15u) / 16u;
+  if (!n16) return hipSuccess;
+  const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(blocks, (n16 + 255u) / 256u));
+  hipLaunchKernelGGL(k_stream_out, dim3(g), dim3(256), 0, s, static_cast<const u32x4*>(src), static_cast<u32x4*>(dst),
+                     n16);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -251,8 +251,9 @@ int av_fetch_compact(av_engine* e, void* out, int64_t cap, int64_t* bytes);
  * memory on a copy stream, clear the log and return at once with a ticket; the
  * caller enqueues the next rounds while the copy runs. av_fetch_compact_wait
  * blocks until that copy landed and returns the stream (engine memory, valid
- * until the av_fetch_compact_async call two tickets later or av_destroy). At
- * most two tickets are outstanding: the third call waits for the oldest copy. */
+ * until the av_fetch_compact_async call three tickets later or av_destroy), so a
+ * consumer may read one stream while the next two are encoded and copied. At
+ * most three tickets are outstanding: the fourth call waits for the oldest copy. */
 int av_fetch_compact_async(av_engine* e, int64_t* ticket);
 int av_fetch_compact_wait(av_engine* e, int64_t ticket, const void** stream, int64_t* bytes);
 /* Host-side expansion of a compact stream into packed update words (the
