@@ -1062,6 +1062,15 @@ def main(argv=None):
             line["config"]["needed_rows_match"] = r["needed_rows_match"]
         if r.get("shard_fallback"):
             line["config"]["shard_fallback"] = "peer exchange unavailable: " + r["shard_fallback"]
+        # the north star's own workload (BASELINE.json: "1M nodes x 1k conflicting targets"): C4p, 500
+        # double-spend pairs per node, every round through the slot network (no settled shortcut)
+        ns = r if args.workload == "c4p" else secondary.get("c4p")
+        if ns and ns.get("value") is not None:
+            line["north_star_value"] = ns["value"]
+            line["north_star"] = {"workload": WORKLOADS["c4p"][7], "value": ns["value"],
+                                  "value_general": ns.get("value_general"),
+                                  "target": 1e10, "note": "BASELINE.json north_star: >= 1e10 bit-exact vote-record "
+                                  "updates/s for 1M nodes x 1k conflicting targets (target on 8 GPUs)"}
         if secondary:
             line["secondary"] = secondary
         detail["workloads"][args.workload] = {"workload": r["desc"], "value": r["value"], "delivery": r["delivery"],

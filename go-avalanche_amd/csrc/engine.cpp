@@ -134,6 +134,10 @@ struct av_engine {
   unsigned long long* finalized = nullptr;
   unsigned long long* scratch_count = nullptr;
   int64_t round = 0, log_base = 0;
+  // update words (kernels.h pack_update): the round field starts at bit round_shift = 28 + the node
+  // field's width, max(24, bits of N); the log spans at most 2^(64 - round_shift) rounds
+  uint32_t round_shift = 52;
+  int64_t max_log_rounds() const { return (int64_t)1 << (64 - round_shift); }
   // every consider bit ever shifted in was 1 (no replay, no neutral drop-in
   // vote, no write_records): an all-ones oldest consider plane implies all
   // consider planes are all-ones (lets k_round_fast skip them)
@@ -394,6 +398,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.t0 = (uint32_t)e->t0;
   p.round = (uint32_t)e->round;
   p.round_rel = (uint32_t)(e->round - e->log_base);
+  p.round_shift = e->round_shift;
   p.peer_mode = e->cfg.peer_mode;
   p.warm_all = e->warm_all ? 1u : 0u;
   p.store_policy = e->store_policy;
@@ -671,8 +676,8 @@ int ref_pick(av_engine* e) {
 }
 
 int launch_one_round(av_engine* e, const uint32_t* replay) {
-  AV_CHECK(e->round - e->log_base < 4096, AV_ERR_OVERFLOW,
-           "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
+  AV_CHECK(e->round - e->log_base < e->max_log_rounds(), AV_ERR_OVERFLOW,
+           "StatusUpdate log spans %lld rounds: call av_fetch_updates more often", (long long)e->max_log_rounds());
   if (e->group) {
     // serial group: round r of rank i is enqueued after round r of every lower rank and before
     // round r of every higher one (the stream order is the exchange's barrier)
@@ -870,8 +875,8 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
 // round (count >= 120). Host-side round bookkeeping as launch_one_round.
 int launch_replay_fused(av_engine* e, const uint32_t* replay0, int32_t R) {
   if (e) ref_invalidate(e);
-  AV_CHECK(e->round + R - 1 - e->log_base < 4096, AV_ERR_OVERFLOW,
-           "StatusUpdate log spans 4096 rounds: call av_fetch_updates more often");
+  AV_CHECK(e->round + R - 1 - e->log_base < e->max_log_rounds(), AV_ERR_OVERFLOW,
+           "StatusUpdate log spans %lld rounds: call av_fetch_updates more often", (long long)e->max_log_rounds());
   int rc = materialize_votes_only(e);
   if (rc != AV_OK) return rc;
   rc = materialize_counts(e);
@@ -1111,7 +1116,9 @@ int av_create(const av_config* cfg, av_engine** out) {
   AV_CHECK(cfg && out, AV_ERR_INVALID_ARG, "null argument");
   *out = nullptr;
   const av_config& c = *cfg;
-  AV_CHECK(c.n_nodes >= 2 && c.n_nodes < (1ll << 24), AV_ERR_INVALID_ARG, "n_nodes must be in [2, 2^24)");
+  // node ids are 32-bit in the kernels; the update word's node field widens past 24 bits by taking
+  // bits from its round field (pack_update), which keeps >= 2^6 rounds between fetches below 2^30
+  AV_CHECK(c.n_nodes >= 2 && c.n_nodes < (1ll << 30), AV_ERR_INVALID_ARG, "n_nodes must be in [2, 2^30)");
   AV_CHECK(c.n_targets >= 1 && c.n_targets < (1ll << 22), AV_ERR_INVALID_ARG, "n_targets must be in [1, 2^22)");
   AV_CHECK(c.k >= 1 && c.k <= avk::kMaxK, AV_ERR_INVALID_ARG, "k must be in [1, 16]");
   AV_CHECK(c.peer_mode == AV_PEERS_RANDOM || c.peer_mode == AV_PEERS_ROUND_ROBIN, AV_ERR_INVALID_ARG,
@@ -1127,6 +1134,11 @@ int av_create(const av_config* cfg, av_engine** out) {
   e->t1 = c.target_end;
   if (e->t0 == 0 && e->t1 == 0) e->t1 = e->M;
   e->k = c.k;
+  {
+    uint32_t nb = 24;
+    while (nb < 32 && (1ll << nb) < e->N) ++nb;
+    e->round_shift = 28 + nb;
+  }
   auto bad = [&](const char* msg) {
     delete e;
     return fail(AV_ERR_INVALID_ARG, "%s", msg);
@@ -1880,6 +1892,12 @@ int av_set_polling(av_engine* e, int64_t node, int32_t polls) {
   return AV_OK;
 }
 
+int av_update_round_shift(av_engine* e, int32_t* out) {
+  AV_CHECK(e && out, AV_ERR_INVALID_ARG, "null argument");
+  *out = (int32_t)e->round_shift;
+  return AV_OK;
+}
+
 int av_log_base_round(av_engine* e, int64_t* out) {
   AV_CHECK(e && out, AV_ERR_INVALID_ARG, "null argument");
   *out = e->log_base;
@@ -2054,6 +2072,7 @@ avk::EncodeParams encode_params(av_engine* e) {
   p.BL = e->BL;
   p.t0 = (uint32_t)e->t0;
   p.r_total = log_rounds(e);
+  p.round_shift = e->round_shift;
   const uint32_t tb = bits_for((uint64_t)(e->t1 - e->t0)), sb = bits_for((uint64_t)e->k);
   p.target_bits = tb;
   p.code_bytes = sb + tb + 2 <= 16 ? 2u : 4u;
@@ -2124,6 +2143,7 @@ int encode_log(av_engine* e, const LogCounts& c, bool compact, void* dev, Encode
     h.code_bytes = (int32_t)p.code_bytes;
     h.target_bits = (int32_t)p.target_bits;
     h.slot_bits = (int32_t)bits_for((uint64_t)e->k);
+    h.round_shift = (int32_t)e->round_shift;
     h.bytes = (int64_t)(groups - base) + (int64_t)cbase;
     res->bytes = h.bytes;
   }
@@ -2276,7 +2296,8 @@ int av_compact_expand(const void* stream, int64_t bytes, uint64_t* out, int64_t 
   std::memcpy(&h, stream, kHdrBytes);
   AV_CHECK(h.magic == AV_COMPACT_MAGIC && h.version == AV_COMPACT_VERSION, AV_ERR_INVALID_ARG, "not a compact stream");
   AV_CHECK(h.bytes == bytes && h.n_rounds >= 1 && h.chunks >= 1 && (h.code_bytes == 2 || h.code_bytes == 4) &&
-               h.target_bits >= 0 && h.target_bits <= 22 && h.n_updates >= 0,
+               h.target_bits >= 0 && h.target_bits <= 22 && h.n_updates >= 0 && h.round_shift >= 52 &&
+               h.round_shift <= 60 && h.n_rounds <= (1ll << (64 - h.round_shift)),
            AV_ERR_INVALID_ARG, "malformed compact stream header");
   const uint64_t n_idx = (uint64_t)h.n_rounds * (uint64_t)h.chunks + 1;
   const uint8_t* base = static_cast<const uint8_t*>(stream);
@@ -2310,11 +2331,11 @@ int av_compact_expand(const void* stream, int64_t bytes, uint64_t* out, int64_t 
         std::memcpy(&node, groups + at, 4);
         std::memcpy(&n, groups + at + 4, 4);
         const uint64_t len = 8 + (((uint64_t)n * cw + 3) & ~3ull);
-        if (at + len > b1 || u + n > u1 || node >= (1u << 24)) {
+        if (at + len > b1 || u + n > u1 || (uint64_t)node >= (1ull << (h.round_shift - 28))) {
           bad[t] = 1;
           return;
         }
-        const uint64_t hi = (rr << 52) | ((uint64_t)node << 28);
+        const uint64_t hi = (rr << h.round_shift) | ((uint64_t)node << 28);
         const uint8_t* cp = groups + at + 8;
         for (uint32_t i = 0; i < n; ++i) {
           uint32_t code;
@@ -2351,7 +2372,8 @@ int av_updates_digest_range(av_engine* e, int64_t n0, int64_t n1, uint64_t out[3
   AV_HIP(hipMemcpyAsync(&ovf, e->log_overflow, 4, hipMemcpyDeviceToHost, e->stream));
   if (!e->digest) AV_HIP(dev_alloc(&e->digest, 3));
   AV_HIP(avk::launch_log_digest(e->log, e->log_count, e->log_cap, e->dlog, e->dlog_count, e->dlog_cap, e->mlog,
-                                e->mlog_count, e->mlog_cap, e->log_shards, (uint32_t)e->k, (uint32_t)n0, (uint32_t)n1, e->digest, e->stream));
+                                e->mlog_count, e->mlog_cap, e->log_shards, (uint32_t)e->k, (uint32_t)n0, (uint32_t)n1,
+                                e->round_shift, e->digest, e->stream));
   unsigned long long d[3] = {0, 0, 0};
   AV_HIP(hipMemcpyAsync(d, e->digest, sizeof(d), hipMemcpyDeviceToHost, e->stream));
   AV_HIP(hipStreamSynchronize(e->stream));

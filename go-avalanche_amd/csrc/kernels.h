@@ -109,6 +109,7 @@ struct RoundParams {
   uint32_t t0;               // first local target (global id, multiple of 32)
   uint32_t round;            // global round index (RNG counter, byz pattern)
   uint32_t round_rel;        // round - log base (update key field)
+  uint32_t round_shift;      // bit of the update word's round field (pack_update)
   int32_t peer_mode;
   uint32_t warm_skip;        // consider planes are monotone (sim votes only): skip all-ones planes
   uint32_t plane_nt;         // stream state planes with non-temporal loads/stores
@@ -301,11 +302,12 @@ __host__ __device__ inline uint64_t med_word(uint64_t key, uint32_t f) {
 }
 
 // Update-log entry (one StatusUpdate, avalanche.go:59-62):
-//   [63:52] round - log_base | [51:28] node | [27:24] slot | [23:2] target | [1:0] status
+//   [63:S] round - log_base | [S-1:28] node | [27:24] slot | [23:2] target | [1:0] status
+// S = the engine's round shift: 28 + max(24, bits of N) (52 below 2^24 nodes, include/avhip.h).
 // Ascending order of the packed word == canonical (round, node, slot, target).
 __host__ __device__ inline uint64_t pack_update(uint32_t round_rel, uint32_t node, uint32_t slot,
-                                                uint32_t target, uint32_t status) {
-  return ((uint64_t)round_rel << 52) | ((uint64_t)node << 28) | ((uint64_t)slot << 24) |
+                                                uint32_t target, uint32_t status, uint32_t round_shift) {
+  return ((uint64_t)round_rel << round_shift) | ((uint64_t)node << 28) | ((uint64_t)slot << 24) |
          ((uint64_t)target << 2) | (uint64_t)status;
 }
 
@@ -444,7 +446,7 @@ hipError_t launch_read_records_virtual(const RoundParams& p, uint32_t nl0, uint3
 hipError_t launch_log_digest(const uint64_t* log, const uint32_t* counts, uint32_t cap, const uint64_t* dlog,
                              const uint32_t* dcounts, uint32_t dcap, const uint64_t* mlog, const uint32_t* mcounts,
                              uint32_t mcap, uint32_t shards, uint32_t k, uint32_t node0, uint32_t node1,
-                             unsigned long long* out, hipStream_t s);
+                             uint32_t round_shift, unsigned long long* out, hipStream_t s);
 // Canonical order of the pending StatusUpdates (log_ops.hip): a counting sort by (round, node) bucket
 // for rounds [r0, r0 + nr) of the log (round_rel < r_total), then one wave per bucket writing its
 // updates in (slot, target) order, as packed words (out + ubase + the bucket's update offset) or as
@@ -458,6 +460,7 @@ struct EncodeParams {
   uint32_t log_cap, mlog_cap, dlog_cap, shards;
   uint32_t K, n0, NL, BL, t0;
   uint32_t r0, nr, r_total;
+  uint32_t round_shift;  // the update words' round field (pack_update); node = bits [28, round_shift)
   uint32_t code_bytes, target_bits;  // compact codes: slot << (target_bits + 2) | local target << 2 | status
   uint32_t* err;  // bit 0: an entry outside the engine's nodes / rounds; bit 1: a bucket's count mismatch
 };

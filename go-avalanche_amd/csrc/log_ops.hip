@@ -102,8 +102,12 @@ __device__ __forceinline__ void for_each_med(const uint64_t* rec, F&& f) {
 #endif
 }
 
-__device__ __forceinline__ bool in_nodes(uint64_t w, uint32_t node0, uint32_t node1) {
-  const uint32_t node = (uint32_t)(w >> 28) & 0xFFFFFFu;
+// node field of an update word: bits [28, round_shift)
+__device__ __forceinline__ uint32_t word_node(uint64_t w, uint32_t round_shift) {
+  return (uint32_t)((w >> 28) & ((1ull << (round_shift - 28u)) - 1ull));
+}
+__device__ __forceinline__ bool in_nodes(uint64_t w, uint32_t node0, uint32_t node1, uint32_t round_shift) {
+  const uint32_t node = word_node(w, round_shift);
   return node >= node0 && node < node1;
 }
 
@@ -113,7 +117,7 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
                                                     const uint64_t* dlog, const uint32_t* dcounts, uint32_t dcap,
                                                     const uint64_t* mlog, const uint32_t* mcounts, uint32_t mcap,
                                                     uint32_t K, uint32_t node0, uint32_t node1,
-                                                    unsigned long long* out) {
+                                                    uint32_t rs, unsigned long long* out) {
   const uint32_t shard = blockIdx.y;
   const uint32_t stride = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -122,7 +126,7 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
   const uint64_t* src = log + (size_t)shard * cap;
   for (uint32_t i = t; i < n; i += stride) {
     const uint64_t w = src[i];
-    if (!in_nodes(w, node0, node1)) continue;
+    if (!in_nodes(w, node0, node1, rs)) continue;
     const uint64_t h = mix64(w);
     s += h;
     x ^= h;
@@ -133,7 +137,7 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
   const uint64_t* dsrc = dlog + (size_t)shard * dcap * DW;
   for (uint32_t i = t; i < nd; i += stride) {
     const uint32_t* rw = reinterpret_cast<const uint32_t*>(dsrc + (size_t)i * DW);
-    if (!in_nodes((uint64_t)rw[0] | ((uint64_t)rw[1] << 32), node0, node1)) continue;
+    if (!in_nodes((uint64_t)rw[0] | ((uint64_t)rw[1] << 32), node0, node1, rs)) continue;
     for_each_dense(reinterpret_cast<const uint32_t*>(dsrc + (size_t)i * DW), K, [&](uint64_t wd) {
       const uint64_t h = mix64(wd);
       s += h;
@@ -145,7 +149,7 @@ __global__ __launch_bounds__(256) void k_log_digest(const uint64_t* log, const u
   constexpr uint32_t MW = med_rec_words();
   const uint64_t* msrc = mlog + (size_t)shard * mcap * MW;
   for (uint32_t i = t; i < nm; i += stride) {
-    if (!in_nodes(msrc[MW * i], node0, node1)) continue;
+    if (!in_nodes(msrc[MW * i], node0, node1, rs)) continue;
     for_each_med(msrc + MW * i, [&](uint64_t wd) {
       const uint64_t h = mix64(wd);
       s += h;
@@ -259,7 +263,7 @@ __global__ __launch_bounds__(kEncThreads) void k_bucket_count(EncArgs a) {
       uint64_t addr;
       locate(flat, p.shards, f, kind, addr, p);
       const uint64_t key = entry_key(p, kind, addr, nu);
-      const uint32_t rr = (uint32_t)(key >> 52), node = (uint32_t)(key >> 28) & 0xFFFFFFu;
+      const uint32_t rr = (uint32_t)(key >> p.round_shift), node = word_node(key, p.round_shift);
       const bool ok = node >= p.n0 && node - p.n0 < p.NL && rr < p.r_total;
       if (ok && rr >= p.r0 && rr < p.r0 + p.nr) b = (rr - p.r0) * p.NL + (node - p.n0);
       if (!ok) atomicOr(p.err, 1u);  // an entry outside the engine's nodes or the log's rounds
@@ -545,7 +549,7 @@ __global__ __launch_bounds__(256) void k_bucket_emit(EmitArgs a) {
       const uint32_t want = (uint32_t)(u1 - u0);
       uint64_t* out = COMPACT ? nullptr : a.out + a.ubase + u0;
       uint8_t* grp = COMPACT ? a.cout + a.cbase + c0b : nullptr;
-      const uint64_t hi_word = ((uint64_t)rnd << 52) | ((uint64_t)node << 28);
+      const uint64_t hi_word = ((uint64_t)rnd << p.round_shift) | ((uint64_t)node << 28);
       uint32_t run = 0;
       for (uint32_t c0 = 0; c0 < C; c0 += 64u) {
         const uint32_t c = c0 + lane;
@@ -628,11 +632,11 @@ __global__ void k_compact_index(const uint64_t* coff, const uint64_t* uoff, uint
 hipError_t launch_log_digest(const uint64_t* log, const uint32_t* counts, uint32_t cap, const uint64_t* dlog,
                              const uint32_t* dcounts, uint32_t dcap, const uint64_t* mlog, const uint32_t* mcounts,
                              uint32_t mcap, uint32_t shards, uint32_t k, uint32_t node0, uint32_t node1,
-                             unsigned long long* out, hipStream_t s) {
+                             uint32_t round_shift, unsigned long long* out, hipStream_t s) {
   hipError_t e = hipMemsetAsync(out, 0, 3 * sizeof(unsigned long long), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_log_digest, dim3(16, shards), dim3(256), 0, s, log, counts, cap, dlog, dcounts, dcap, mlog,
-                     mcounts, mcap, k, node0, node1, out);
+                     mcounts, mcap, k, node0, node1, round_shift, out);
   return hipGetLastError();
 }
 

@@ -371,7 +371,7 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
     const uint32_t pos = dbase + __builtin_amdgcn_mbcnt_hi((uint32_t)(dl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dl, 0u));
     if (pos < p.dlog_cap) {
       uint32_t* rec = reinterpret_cast<uint32_t*>(p.dlog + ((size_t)shard * p.dlog_cap + pos) * DW);
-      const uint64_t key = pack_update(p.round_rel, node, 0u, tbase, 0u);
+      const uint64_t key = pack_update(p.round_rel, node, 0u, tbase, 0u, p.round_shift);
       rec[0] = (uint32_t)key;
       rec[1] = (uint32_t)(key >> 32);
 #pragma unroll
@@ -408,7 +408,7 @@ __device__ __forceinline__ uint32_t emit_updates(const RoundParams& p, uint32_t 
             const uint32_t pos = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
             if (pos < p.log_cap)
-              dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st);
+              dst[pos] = pack_update(p.round_rel, node, (uint32_t)j, tbase + bit, st, p.round_shift);
             else
               ovf = true;
           }
@@ -476,7 +476,7 @@ __device__ __forceinline__ uint32_t emit_updates_flat(const RoundParams& p, uint
     const uint32_t pos = dbase + __builtin_amdgcn_mbcnt_hi((uint32_t)(dl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dl, 0u));
     if (pos < p.dlog_cap) {
       uint32_t* rec = reinterpret_cast<uint32_t*>(p.dlog + ((size_t)shard * p.dlog_cap + pos) * DW);
-      const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u);
+      const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u, p.round_shift);
       rec[0] = (uint32_t)key;
       rec[1] = (uint32_t)(key >> 32);
 #pragma unroll
@@ -499,7 +499,7 @@ __device__ __forceinline__ uint32_t emit_updates_flat(const RoundParams& p, uint
     uint32_t pos = base + incl - scnt;  // this lane's first entry
     const uint32_t end = base + st_s;   // entries at or past it were dropped (overflow)
     uint32_t S = 0u, j = 0u, cur = 0u;
-    const uint64_t hi = ((uint64_t)round_rel << 52) | ((uint64_t)node << 28);
+    const uint64_t hi = ((uint64_t)round_rel << p.round_shift) | ((uint64_t)node << 28);
     for (uint32_t r = 0; r < 64u; ++r) {
       const bool more = r < scnt;
       if (__ballot(more) == 0ull) break;
@@ -700,7 +700,7 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
     const uint32_t st_m = mbase >= p.mlog_cap ? 0u : min(r.tot_m, p.mlog_cap - mbase);
     const uint32_t st_s = base >= p.log_cap ? 0u : min(r.tot_s, p.log_cap - base);
     const bool ovf = st_d < r.tot_d || st_m < r.tot_m || st_s < r.tot_s;
-    const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u);
+    const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u, p.round_shift);
     const uint64_t mine = dense ? dl : med ? ml : sl;
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
     if (dense) {
@@ -756,7 +756,7 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
   const uint32_t st_m = mbase >= p.mlog_cap ? 0u : min(tot_m, p.mlog_cap - mbase);
   const uint32_t st_s = base >= p.log_cap ? 0u : min(tot_s, p.log_cap - base);
   const bool ovf = st_d < tot_d || st_m < tot_m || st_s < tot_s;
-  const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u);
+  const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u, p.round_shift);
   const uint64_t mine = dense ? dl : med ? ml : sl;
   const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
   if (dense) {

@@ -84,7 +84,7 @@ EXPORTED = [
     "av_updates_digest_range", "av_read_pref_words", "av_set_polling",
     "av_register_votes_batch", "av_changed_words", "av_materialize", "av_peer_group_serial", "av_peer_sync",
     "av_pushed_words", "av_log_entries", "av_resize_log", "av_fetch_compact", "av_fetch_compact_async",
-    "av_fetch_compact_wait", "av_compact_expand",
+    "av_fetch_compact_wait", "av_compact_expand", "av_update_round_shift",
 ]
 
 _lib = None
@@ -161,6 +161,7 @@ def lib():
         "av_fetch_compact_async": (i32, [_vp, P(i64)]),
         "av_fetch_compact_wait": (i32, [_vp, i64, P(_vp), P(i64)]),
         "av_compact_expand": (i32, [_vp, i64, _vp, i64, P(i64)]),
+        "av_update_round_shift": (i32, [_vp, P(i32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -187,12 +188,13 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(_vp)
 
 
-def decode_updates(u: np.ndarray, base_round: int = 0) -> np.ndarray:
-    """Packed update words -> int64[n, 5] (round, node, slot, target, status)."""
+def decode_updates(u: np.ndarray, base_round: int = 0, round_shift: int = 52) -> np.ndarray:
+    """Packed update words -> int64[n, 5] (round, node, slot, target, status); round_shift = the
+    engine's (av_update_round_shift: 52 below 2^24 nodes)."""
     u = np.asarray(u, np.uint64)
     out = np.empty((u.size, 5), np.int64)
-    out[:, 0] = (u >> np.uint64(52)).astype(np.int64) + base_round
-    out[:, 1] = ((u >> np.uint64(28)) & np.uint64(0xFFFFFF)).astype(np.int64)
+    out[:, 0] = (u >> np.uint64(round_shift)).astype(np.int64) + base_round
+    out[:, 1] = ((u >> np.uint64(28)) & np.uint64((1 << (round_shift - 28)) - 1)).astype(np.int64)
     out[:, 2] = ((u >> np.uint64(24)) & np.uint64(0xF)).astype(np.int64)
     out[:, 3] = ((u >> np.uint64(2)) & np.uint64(0x3FFFFF)).astype(np.int64)
     out[:, 4] = (u & np.uint64(3)).astype(np.int64)
@@ -203,13 +205,14 @@ COMPACT_MAGIC = 0x31435641  # include/avhip.h AV_COMPACT_MAGIC
 COMPACT_HEADER = np.dtype([("magic", "<u4"), ("version", "<u4"), ("log_base", "<i8"), ("n_updates", "<i8"),
                            ("bytes", "<i8"), ("node_base", "<i8"), ("target_base", "<i8"), ("n_rounds", "<i4"),
                            ("chunks", "<i4"), ("chunk_nodes", "<i4"), ("code_bytes", "<i4"),
-                           ("target_bits", "<i4"), ("slot_bits", "<i4")])
-assert COMPACT_HEADER.itemsize == 72
+                           ("target_bits", "<i4"), ("slot_bits", "<i4"), ("round_shift", "<i4"),
+                           ("reserved", "<i4")])
+assert COMPACT_HEADER.itemsize == 80
 
 
 def compact_header(stream) -> dict:
     """The av_compact_header of a compact StatusUpdate stream, as a dict."""
-    h = np.frombuffer(memoryview(stream)[:72], COMPACT_HEADER)[0]
+    h = np.frombuffer(memoryview(stream)[:COMPACT_HEADER.itemsize], COMPACT_HEADER)[0]
     return {k: int(h[k]) for k in COMPACT_HEADER.names}
 
 
@@ -433,7 +436,14 @@ class Engine:
         base = self.log_base_round()
         _check(lib().av_fetch_updates(self._h, _ptr(buf), buf.size, C.byref(got)))
         buf = buf[: got.value]
-        return decode_updates(buf, base) if decode else buf
+        return decode_updates(buf, base, self.round_shift) if decode else buf
+
+    @property
+    def round_shift(self):
+        """The update words' round field position (av_update_round_shift)."""
+        out = C.c_int32(0)
+        _check(lib().av_update_round_shift(self._h, C.byref(out)))
+        return out.value
 
     def fetch_into(self, buf):
         """All pending StatusUpdates, packed and sorted canonical, into the caller's uint64 buffer
@@ -449,7 +459,7 @@ class Engine:
         rc = lib().av_fetch_compact(self._h, None, 0, C.byref(need))
         if rc not in (AV_OK, AV_ERR_OVERFLOW):
             _check(rc)
-        buf = np.zeros(max(need.value, 72), np.uint8)
+        buf = np.zeros(max(need.value, COMPACT_HEADER.itemsize), np.uint8)
         got = C.c_int64(0)
         _check(lib().av_fetch_compact(self._h, _ptr(buf), buf.size, C.byref(got)))
         return buf[: got.value]

@@ -87,7 +87,7 @@ extern "C" {
 typedef struct av_engine av_engine;
 
 typedef struct {
-  int64_t n_nodes;       /* N, whole network */
+  int64_t n_nodes;       /* N, whole network (< 2^30) */
   int64_t n_targets;     /* M, whole network (target slots 0..M-1) */
   int32_t k;             /* polls (Responses) per node per round, 1..16 */
   int32_t peer_mode;     /* AV_PEERS_* */
@@ -102,11 +102,19 @@ typedef struct {
 } av_config;
 
 /* Packed StatusUpdate as returned by av_fetch_updates (uint64):
- *   [63:52] round - round of the previous fetch | [51:28] node |
+ *   [63:S] round - round of the previous fetch | [S-1:28] node |
  *   [27:24] slot (poll index within the round)  | [23:2] target | [1:0] status
- * Sorted ascending == (round, node, slot, target) == reference append order. */
-static inline int64_t av_update_round_rel(uint64_t u) { return (int64_t)(u >> 52); }
-static inline int64_t av_update_node(uint64_t u) { return (int64_t)((u >> 28) & 0xFFFFFFu); }
+ * S = the engine's round shift (av_update_round_shift): 52 for networks of
+ * fewer than 2^24 nodes, 28 + ceil(log2 N) above (the node field widens, the
+ * round field narrows: a log then spans at most 2^(64 - S) rounds).
+ * Sorted ascending == (round, node, slot, target) == reference append order.
+ * The first helpers take S; the short forms assume S = 52. */
+static inline int64_t av_update_round_rel_s(uint64_t u, int32_t s) { return (int64_t)(u >> s); }
+static inline int64_t av_update_node_s(uint64_t u, int32_t s) {
+  return (int64_t)((u >> 28) & ((1ull << (s - 28)) - 1ull));
+}
+static inline int64_t av_update_round_rel(uint64_t u) { return av_update_round_rel_s(u, 52); }
+static inline int64_t av_update_node(uint64_t u) { return av_update_node_s(u, 52); }
 static inline int32_t av_update_slot(uint64_t u) { return (int32_t)((u >> 24) & 0xFu); }
 static inline int64_t av_update_target(uint64_t u) { return (int64_t)((u >> 2) & 0x3FFFFFu); }
 static inline int32_t av_update_status(uint64_t u) { return (int32_t)(u & 3u); }
@@ -211,11 +219,13 @@ int av_fetch_updates(av_engine* e, uint64_t* out, int64_t cap, int64_t* n_out);
 /* The round the pending log's round fields count from (the engine round at
  * the last fetch/discard): round of a fetched word = this + av_update_round_rel. */
 int av_log_base_round(av_engine* e, int64_t* out);
+/* The engine's update-word round shift S (see the packed StatusUpdate above). */
+int av_update_round_shift(av_engine* e, int32_t* out);
 
 /* ---- compact StatusUpdate stream (the same updates as av_fetch_updates, in the
  * same canonical order, ~2 B per update instead of 8; processor.go:61,111) ----
  * Layout (little-endian):
- *   av_compact_header (72 B)
+ *   av_compact_header (80 B)
  *   index: n_rounds * chunks + 1 entries of {uint64 byte offset of the entry's
  *          first group from the start of the groups, uint64 updates before it};
  *          entry r * chunks + c covers the groups of round log_base + r and
@@ -241,6 +251,8 @@ typedef struct {
   int32_t code_bytes;   /* 2 or 4 */
   int32_t target_bits;
   int32_t slot_bits;
+  int32_t round_shift;  /* of the expanded words (av_update_round_shift) */
+  int32_t reserved;
 } av_compact_header;
 /* Every pending update as a compact stream into out (cap bytes), clearing the
  * log; AV_ERR_OVERFLOW with *bytes = the size needed (log kept) if cap is too

@@ -7,7 +7,7 @@ import numpy as np
 HEADER = np.dtype([("magic", "<u4"), ("version", "<u4"), ("log_base", "<i8"), ("n_updates", "<i8"),
                    ("bytes", "<i8"), ("node_base", "<i8"), ("target_base", "<i8"), ("n_rounds", "<i4"),
                    ("chunks", "<i4"), ("chunk_nodes", "<i4"), ("code_bytes", "<i4"), ("target_bits", "<i4"),
-                   ("slot_bits", "<i4")])
+                   ("slot_bits", "<i4"), ("round_shift", "<i4"), ("reserved", "<i4")])
 MAGIC, VERSION, CHUNK_NODES = 0x31435641, 1, 4096
 
 
@@ -19,15 +19,15 @@ def bits_for(n):
 
 
 def encode(words, *, log_base, n_rounds, node_base, n_local, target_base, n_targets_local, k,
-           chunk_nodes=CHUNK_NODES):
+           chunk_nodes=CHUNK_NODES, round_shift=52):
     """Packed words (sorted canonical, round fields relative to log_base) -> stream bytes."""
     w = np.asarray(words, np.uint64)
     assert np.all(w[1:] >= w[:-1])
     tb, sb = bits_for(n_targets_local), bits_for(k)
     cw = 2 if sb + tb + 2 <= 16 else 4
     chunks = (n_local + chunk_nodes - 1) // chunk_nodes
-    rr = (w >> np.uint64(52)).astype(np.int64)
-    node = ((w >> np.uint64(28)) & np.uint64(0xFFFFFF)).astype(np.int64)
+    rr = (w >> np.uint64(round_shift)).astype(np.int64)
+    node = ((w >> np.uint64(28)) & np.uint64((1 << (round_shift - 28)) - 1)).astype(np.int64)
     slot = ((w >> np.uint64(24)) & np.uint64(0xF)).astype(np.int64)
     tl = ((w >> np.uint64(2)) & np.uint64(0x3FFFFF)).astype(np.int64) - target_base
     st = (w & np.uint64(3)).astype(np.int64)
@@ -61,6 +61,6 @@ def encode(words, *, log_base, n_rounds, node_base, n_local, target_base, n_targ
     for name, v in (("magic", MAGIC), ("version", VERSION), ("log_base", log_base), ("n_updates", w.size),
                     ("bytes", total), ("node_base", node_base), ("target_base", target_base),
                     ("n_rounds", n_rounds), ("chunks", chunks), ("chunk_nodes", chunk_nodes), ("code_bytes", cw),
-                    ("target_bits", tb), ("slot_bits", sb)):
+                    ("target_bits", tb), ("slot_bits", sb), ("round_shift", round_shift)):
         h[name] = v
     return np.frombuffer(h.tobytes() + idx.astype("<u8").tobytes() + bytes(body), np.uint8).copy()

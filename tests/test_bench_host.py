@@ -176,14 +176,38 @@ def test_shard_auto_per_workload():
 
 def test_compact_delivery_fields():
     """The line's `delivery` summary: the on-device digest rate, the host fetch rates into pageable
-    and pinned memory, and the vote-record rate with every round fetched into pinned memory."""
+    and pinned memory, the vote-record rate with every round's compact stream delivered pipelined
+    (and expanded into packed words), and the unpipelined packed-word rate."""
     import bench
     d = {"digest_updates_per_s": 1e10,
          "pageable": {"updates_per_s": 3e9, "delivered_votes_per_s": 2e11},
-         "pinned": {"updates_per_s": 5e9, "delivered_votes_per_s": 4e11}}
+         "pinned": {"updates_per_s": 5e9, "delivered_votes_per_s": 4e11},
+         "compact": {"votes_per_s": 1.9e12, "votes_per_s_expanded": 1.1e12, "bytes_per_update": 2.1}}
     c = bench.compact_delivery(d)
     assert c == {"digest_updates_per_s": 1e10, "fetch_updates_per_s": {"pageable": 3e9, "pinned": 5e9},
-                 "votes_per_s_with_fetch": 4e11}
+                 "votes_per_s_with_fetch": 1.9e12, "votes_per_s_with_fetch_words": 1.1e12,
+                 "votes_per_s_with_fetch_unpipelined": 4e11, "compact_bytes_per_update": 2.1}
+
+
+def test_size_log_covers_any_single_round():
+    """the log holds at least the fullest single round of the epoch (the delivery pass
+    fetches rounds 0-3 one at a time), whatever the timed window."""
+    import bench
+
+    class E:
+        def synchronize(self):
+            pass
+
+        def discard_updates(self):
+            pass
+
+        def resize_log(self, *ent):
+            self.ent = ent
+    per_round = {r: (10, 20, 30) for r in range(16)}
+    per_round[1] = (5_000_000, 6_000_000, 7_000_000)
+    e = E()
+    bench.size_log(e, per_round, 5, 10)  # window rounds 5..14: no storm round inside
+    assert all(v >= int(1.3 * w) for v, w in zip(e.ent, per_round[1]))
 
 
 def test_node_shard_run_length_only_for_conflicting_workloads():

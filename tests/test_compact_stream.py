@@ -58,7 +58,7 @@ def test_expand_inverts_encode(case):
     got = avhip.compact_expand(s)
     assert np.array_equal(got, w)
     if w.size:  # ~2-4 B per update against 8 B per packed word
-        assert s.size < 8 * w.size + 72 + 16 * (R * -(-nl // 4096) + 1)
+        assert s.size < 8 * w.size + 80 + 16 * (R * -(-nl // 4096) + 1)
 
 
 def test_one_update():
@@ -86,9 +86,23 @@ def test_malformed_streams_are_refused():
     assert _expand_rc(bad)[0] == -1
     assert _expand_rc(s[:-4])[0] == -1  # truncated: the header's byte count disagrees
     bad = s.copy()
-    hdr = 72
+    hdr = avhip.COMPACT_HEADER.itemsize
     idx_end = hdr + 16 * (2 * 1 + 1)
     bad[idx_end + 4] ^= 0x7F  # first group's count corrupted
     assert _expand_rc(bad)[0] == -1
     rc, n = _expand_rc(s, cap=max(0, w.size - 1))  # caller buffer too small
     assert rc == avhip.AV_ERR_OVERFLOW and n == w.size
+
+
+def test_wide_node_field():
+    """Networks of >= 2^24 nodes: the words' round field starts at bit 53 (include/avhip.h)."""
+    rs = 53
+    rows = np.array([(0, (1 << 24) + 5, 3, 17, 2), (1, 3, 0, 1, 1), (1, (1 << 25) - 1, 7, 63, 0)], np.uint64)
+    w = (rows[:, 0] << np.uint64(rs)) | (rows[:, 1] << np.uint64(28)) | (rows[:, 2] << np.uint64(24)) | \
+        (rows[:, 3] << np.uint64(2)) | rows[:, 4]
+    s = encode(w, log_base=9, n_rounds=2, node_base=0, n_local=1 << 25, target_base=0, n_targets_local=64, k=8,
+               round_shift=rs)
+    assert avhip.compact_header(s)["round_shift"] == rs
+    got = avhip.compact_expand(s)
+    assert np.array_equal(got, w)
+    assert np.array_equal(avhip.decode_updates(got, 9, rs), rows.astype(np.int64) + np.array([9, 0, 0, 0, 0]))

@@ -38,7 +38,7 @@ def check_compact(a, b, rounds_run):
     nl = a.node_range[1] - a.node_range[0]
     tl = a.target_range[1] - a.target_range[0]
     ref = encode(words, log_base=base, n_rounds=max(rounds_run, 1), node_base=a.node_range[0], n_local=nl,
-                 target_base=a.target_range[0], n_targets_local=tl, k=a.k)
+                 target_base=a.target_range[0], n_targets_local=tl, k=a.k, round_shift=a.round_shift)
     assert h["n_updates"] == words.size and h["log_base"] == base
     assert s.size == ref.size and np.array_equal(s, ref), "compact stream differs from the format restatement"
     assert np.array_equal(avhip.compact_expand(s), words)
@@ -149,3 +149,47 @@ def test_full_size_two_level_scan():
     assert np.all(raw[1:] > raw[:-1])
     from oracle import cabi
     assert cabi.update_digest(raw) == d
+
+
+def test_beyond_2_24_nodes(oracle):
+    """N = 2^25 (33.5M nodes x 64 targets, k = 8): the update word's node field widens to 25 bits
+    (round shift 53, include/avhip.h). Sampled nodes above 2^24 checked against the oracle's literal
+    per-node round on the engine's own snapshot (records and update digest), and the fetched words
+    decode to those nodes, in canonical order; the compact stream carries the shift."""
+    n, m, k = 1 << 25, 64, 8
+    eng = avhip.Engine(n, m, k=k, seed=23, log_capacity=1 << 27)
+    assert eng.round_shift == 53
+    eng.init_records(avhip.INIT_BERNOULLI, P80)
+    byz = oracle.byz_words(23, n, 0)
+    valid = np.ones(m, np.uint8)
+    S = 1024
+    for r, a in enumerate([n - S, (1 << 24) + 12345, 1000]):
+        before = eng.read_records(a, a + S)
+        pref = eng.read_pref_words()
+        exp_digest = np.zeros(3, np.uint64)
+        words = before.copy()
+        for i in range(S):
+            row = np.ascontiguousarray(words[i])
+            oracle.node_round_ext(23, n, k, 0, a + i, eng.round, m, pref, byz, valid, row, exp_digest)
+            words[i] = row
+        eng.run_rounds(1)
+        assert eng.updates_digest(a, a + S) == tuple(int(v) for v in exp_digest), r
+        assert np.array_equal(eng.read_records(a, a + S), words), r
+        if r == 0:
+            raw = eng.fetch_updates(decode=False)
+            assert np.all(raw[1:] > raw[:-1])
+            node = (raw >> np.uint64(28)) & np.uint64((1 << 25) - 1)
+            sel = raw[(node >= a) & (node < a + S)]
+            rows = avhip.decode_updates(sel, 0, 53)
+            assert rows.shape[0] == exp_digest[0] and rows[:, 1].max() >= (1 << 24) and np.all(rows[:, 0] == 0)
+            assert oracle.update_digest(sel) == tuple(int(v) for v in exp_digest)
+            del raw, node
+        else:
+            s = eng.fetch_compact()
+            h = avhip.compact_header(s)
+            assert h["round_shift"] == 53 and h["n_updates"] > 0 and h["log_base"] == eng.round - 1
+            w2 = avhip.compact_expand(s)
+            assert np.all(w2[1:] > w2[:-1]) and np.all((w2 >> np.uint64(53)) == 0)
+            node = (w2 >> np.uint64(28)) & np.uint64((1 << 25) - 1)
+            assert oracle.update_digest(w2[(node >= a) & (node < a + S)]) == tuple(int(v) for v in exp_digest)
+            del s, w2, node
