@@ -304,6 +304,9 @@ struct av_engine {
   av_compact_header chdr[kSlots] = {};
   int64_t cticket = 0;           // next ticket
   bool cpend[kSlots] = {};       // a copy was issued into the slot
+  // high-water marks: a slot that grows grows to the largest stream seen, so a caller's warm-up pass
+  // sizes every slot and later rounds never allocate (pinned allocations take tens of ms)
+  size_t cdev_hwm = 0, chost_hwm = 0;
   // batched poll sets (av_get_invs_batch): host-mapped pinned output the fill kernel writes
   void* invs_host = nullptr;
   size_t invs_host_bytes = 0;
@@ -2251,12 +2254,14 @@ int av_fetch_compact_async(av_engine* e, int64_t* ticket) {
   if (e->cpend[s]) AV_HIP(hipEventSynchronize(e->cev[s]));
   e->cpend[s] = false;
   const avk::EncodeParams p = encode_params(e);
-  rc = grow_dev(&e->cdev[s], &e->cdev_bytes[s], compact_bound(e, p, c));
+  e->cdev_hwm = std::max(e->cdev_hwm, compact_bound(e, p, c));
+  rc = grow_dev(&e->cdev[s], &e->cdev_bytes[s], e->cdev_hwm);
   if (rc != AV_OK) return rc;
   Encoded r;
   rc = encode_log(e, c, true, e->cdev[s], &r);  // synchronizes the engine stream
   if (rc != AV_OK) return rc;
-  rc = grow_pinned(&e->chost[s], &e->chost_bytes[s], (size_t)r.bytes + 16);
+  e->chost_hwm = std::max(e->chost_hwm, (size_t)r.bytes + 16);
+  rc = grow_pinned(&e->chost[s], &e->chost_bytes[s], e->chost_hwm);
   if (rc != AV_OK) return rc;
   if (e->copy_blocks) {  // a small copy kernel (the header's bytes are copied too, and overwritten on wait)
     void* hdev = nullptr;
@@ -2958,6 +2963,20 @@ int av_peer_group_serial(av_engine** engines, int32_t world) {
   }
   AV_HIP(hipSetDevice(engines[0]->cfg.device));
   for (int r = 0; r < world; ++r) AV_HIP(hipStreamSynchronize(engines[r]->stream));
+  // the snapshot buffers the real exchange uses (av_peer_handles): fine-grained unless option
+  // "peer_fine" is 0, so that the group's parity runs and per-rank timings see the same memory type
+  for (int r = 0; r < world; ++r) {
+    av_engine* e = engines[r];
+    if (!e->peer_fine) continue;
+    for (int b = 0; b < 3; ++b) {
+      uint32_t* fine = nullptr;
+      AV_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&fine), e->pref_alloc_words * 4,
+                                   hipDeviceMallocFinegrained));
+      AV_HIP(hipMemcpy(fine, e->pref[b], e->pref_alloc_words * 4, hipMemcpyDeviceToDevice));
+      AV_HIP(hipFree(e->pref[b]));
+      e->pref[b] = fine;
+    }
+  }
   auto* g = new PeerGroup();
   if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
     delete g;

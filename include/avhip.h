@@ -292,10 +292,16 @@ int av_discard_updates(av_engine* e);
  * slots of one 32-record lane), dense records (a lane's whole round)}; a
  * lane's updates of one round are one entry. Sizing input for av_resize_log. */
 int av_log_entries(av_engine* e, int64_t out[3]);
-/* Re-allocate the (empty: AV_ERR_UNSUPPORTED otherwise) device log for
+/* Re-allocate the (empty: AV_ERR_UNSUPPORTED otherwise) device log for about
  * entries[k] entries of each kind (8, 32 and 48 B each at k = 8), instead of
  * av_config.update_log_capacity's worst case per update (36 B per update).
- * One round never needs more than one entry per lane of each kind. */
+ * The log is sharded by the round kernel's writer waves: each writer wave gets
+ * ceil(entries[k] / writers) + 1 entries, i.e. the sizing assumes the entries
+ * are spread evenly over the writers. That holds for entries[k] = the lane
+ * count (one round never needs more than one entry per lane of each kind); a
+ * measured count with skewed emission can overflow one shard while the total
+ * stays below entries[k] — the overflow is detected (av_update_log_overflowed,
+ * AV_ERR_OVERFLOW on fetch), never silent. */
 int av_resize_log(av_engine* e, const int64_t entries[3]);
 /* Algorithmic bytes moved by the round kernels since creation: state planes
  * read/written, gathered vote words, published words, 8 B per StatusUpdate
@@ -414,7 +420,10 @@ int av_peer_init(av_engine* e, int32_t world, int32_t rank, const uint8_t* handl
  * rank order, then round r + 1) replaces the device barrier, so per-rank
  * kernel times are those of a rank alone on the device. A rank may run a round
  * only when every lower rank has run it and no higher rank has
- * (AV_ERR_UNSUPPORTED otherwise). Destroy the group's engines together. */
+ * (AV_ERR_UNSUPPORTED otherwise). The snapshot buffers are made fine-grained
+ * as av_peer_handles makes them (option "peer_fine", default 1). Destroy the
+ * group's engines together: once one is destroyed, the others' rounds, pushes
+ * and syncs return AV_ERR_UNSUPPORTED. */
 int av_peer_group_serial(av_engine** engines, int32_t world);
 /* Need-masked exchange (option "peer_mask", default on for 2..9 ranks when a
  * row's 32-word segments never straddle a wave: BL a power of two <= 32 or a
