@@ -53,6 +53,12 @@
 #ifndef AVK_CC_PREFETCH
 #define AVK_CC_PREFETCH 0
 #endif
+// A/B build knob: the storm path's publish loads (overwritten word, stale and need bytes) issued
+// before the tile's plane stores (1) or by publish itself, after them (0, default: measured 3 % faster
+// on masked C4p node shards at 8 ranks, profiles/r06/ab_pub_preload.log)
+#ifndef AVK_PUB_PRELOAD
+#define AVK_PUB_PRELOAD 0
+#endif
 
 namespace avk {
 namespace {
@@ -117,18 +123,38 @@ __device__ __forceinline__ void push_word(const RoundParams& p, uint32_t* dst, u
 // in LDS and stored after the wave's last tile (flush_pushes), so that no load of a later tile waits
 // for them (vmcnt counts loads and stores in issue order, and a system-scope store to a peer completes
 // only at the peer: pushed from inside the tile loop, every tile waited for the last one's pushes).
+// The loads publish() needs (the overwritten word, the segment's stale byte, the node's need byte),
+// issued by the caller before the tile's plane stores: vmcnt counts loads and stores in issue order,
+// so loads issued after the stores would make the tile wait for the stores' completion too (a round
+// trip per tile in every peer-push round; the stale and need bytes exist on need-masked engines only).
+struct PubPre {
+  uint32_t old, st, nm;
+  bool have;
+};
+__device__ __forceinline__ PubPre publish_loads(const RoundParams& p, uint32_t prow, uint32_t nl) {
+  PubPre q{0u, 0u, p.peer_all, true};
+  q.old = p.pref_out[prow];
+  if (p.stale) {
+    q.st = p.stale[nl * p.segs + ((prow - (p.n0 + nl) * p.PS) >> 5)];
+    if (p.need) q.nm = (uint32_t)p.need[nl];
+  }
+  return q;
+}
+
 template <int POL, bool CC>
 __device__ __forceinline__ void publish(const RoundParams& p, uint32_t prow, uint32_t pub, uint32_t old,
-                                        SweepAcc& acc, bool known, uint32_t nl, uint32_t slot) {
+                                        SweepAcc& acc, bool known, uint32_t nl, uint32_t slot,
+                                        const PubPre* pre = nullptr) {
   if (CC && p.count_changed) {
-    if (!known && !AVK_CC_PREFETCH) old = p.pref_out[prow];
+    const bool pl = pre && pre->have;  // loaded ahead (an unknown word only)
+    if (!known && !AVK_CC_PREFETCH) old = pl ? pre->old : p.pref_out[prow];
     uint32_t nm = p.peer_all, st = 0u, si = 0u;
     if (p.stale) {
       si = nl * p.segs + ((prow - (p.n0 + nl) * p.PS) >> 5);
-      st = p.stale[si];
+      st = pl ? pre->st : p.stale[si];
       // a word known unchanged (a settled tile) goes out only where a change was withheld: the need
       // mask is read only then (settled rounds after the catch-up read one byte per lane, not two)
-      if (p.need && (!known || __ballot(st != 0u) != 0ull)) nm = (uint32_t)p.need[nl];
+      if (p.need && (!known || __ballot(st != 0u) != 0ull)) nm = pl ? pre->nm : (uint32_t)p.need[nl];
     }
     const unsigned long long m = __ballot(pub != old);
     const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
@@ -612,6 +638,9 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   if (K == 8 && p.hivirt && ((!WARM && p.fresh) || (klazy && (in.kw & kHiVirt))))
     hv = kdefer || __ballot(active && ((Kp[4] | Kp[5] | Kp[6] | died) != 0u)) == 0ull;
   if (active && !(kAblatePhase && KLZ_ABLATE && (p.ablate_phase & 4u))) {
+    const bool known = AVK_CC_PREFETCH || (kdefer && pend >= 2u);  // (publish)
+    PubPre pre{0u, 0u, 0u, false};
+    if (AVK_PUB_PRELOAD && CC && p.count_changed && !known) pre = publish_loads(p, node * p.PS + b, node - p.n0);
     if (!kdefer) {
       u32x4 o2, o3;
 #pragma unroll
@@ -626,9 +655,8 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
     const uint32_t prow = node * p.PS + b;  // < N * PS < 2^31
     const uint32_t pub = nbyz ? byz_pattern(p.round + 1u) : A;
     if (p.uni_out) acc.umis |= pub != in.uref ? 1u : 0u;  // uniform rows (kernels.h)
-    const bool known = AVK_CC_PREFETCH || (kdefer && pend >= 2u);  // (publish)
     publish<POL, CC>(p, prow, pub, AVK_CC_PREFETCH ? in.old : (nbyz ? byz_pattern(p.round - 2u) : pub), acc,
-                     known, node - p.n0, acc.qslot);
+                     known, node - p.n0, acc.qslot, &pre);
     // a record deleted this round keeps the vote/consider planes stored
     // above: K7 marks it dead, every reader masks by K7 (k_read_records,
     // k_add_targets resets all planes) and the next round's store zeroes them

@@ -16,6 +16,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -147,6 +148,14 @@ class Engine {
   void RunRounds(int32_t rounds);
   int64_t Round() const;
   std::vector<uint64_t> FetchUpdates();
+  // One node's StatusUpdates of one round, in the reference's append order (processor.go:94,111).
+  using Deliver = std::function<void(int64_t round, NodeID node, const std::vector<StatusUpdate>& updates)>;
+  // `rounds` batched rounds, every round's StatusUpdates handed to deliver node by node: round r + 1
+  // computes while round r's compact stream is copied (av_fetch_compact_async / _wait) and decoded.
+  void Rounds(int32_t rounds, const Deliver& deliver);
+  // Walk a compact StatusUpdate stream (include/avhip.h av_compact_header) in place: Hash through
+  // the catalog (a slot never interned is its own Hash).
+  void DecodeCompact(const void* stream, int64_t bytes, const Deliver& deliver) const;
 
  private:
   EngineOptions opt_;

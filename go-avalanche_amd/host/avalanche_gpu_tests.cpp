@@ -3,6 +3,7 @@
 // Run by tests/test_cpp_mirror.py (-m gpu). Exit code = number of failures.
 #include <cstdio>
 #include <functional>
+#include <tuple>
 #include <memory>
 #include <string>
 #include <vector>
@@ -233,6 +234,30 @@ void network_rounds() {
   EXPECT(engine->Round() == 20);
 }
 
+// Pipelined delivery through the mirror (Engine::Rounds over the compact stream) hands every node
+// exactly the StatusUpdates a plain round + FetchUpdates gives, in the same order.
+void pipelined_rounds() {
+  EngineOptions o;
+  o.n_nodes = 3000;
+  o.n_targets = 700;
+  o.k = 8;
+  o.byz_threshold = (uint32_t)(0.2 * 4294967296.0);
+  auto a = std::make_shared<Engine>(o), b = std::make_shared<Engine>(o);
+  EXPECT(av_init_records(a->handle(), AV_INIT_PAIRS, 0) == AV_OK);
+  EXPECT(av_init_records(b->handle(), AV_INIT_PAIRS, 0) == AV_OK);
+  std::vector<std::tuple<int64_t, NodeID, Hash, int>> got, want;
+  b->Rounds(6, [&](int64_t r, NodeID n, const std::vector<StatusUpdate>& ups) {
+    for (const auto& u : ups) got.emplace_back(r, n, u.hash, (int)u.status);
+  });
+  for (int r = 0; r < 6; ++r) {
+    a->RunRounds(1);
+    for (uint64_t u : a->FetchUpdates())
+      want.emplace_back(r, (NodeID)av_update_node(u), (Hash)av_update_target(u), av_update_status(u));
+  }
+  EXPECT(!want.empty());
+  EXPECT(got == want);
+}
+
 }  // namespace
 
 int main() {
@@ -241,6 +266,7 @@ int main() {
       {"TestMultiBlockRegister", multi_block_register},
       {"SuitableNodeAndInvalidTarget", suitable_node_and_invalid_target},
       {"NetworkRounds", network_rounds},
+      {"PipelinedRounds", pipelined_rounds},
   };
   for (const auto& t : tests) {
     g_test = t.first;

@@ -1,5 +1,6 @@
 // processor.cpp — C++ mirror of go-avalanche's Processor over the C ABI.
 #include <algorithm>
+#include <cstring>
 
 #include "avalanche.hpp"
 
@@ -88,6 +89,59 @@ std::vector<uint64_t> Engine::FetchUpdates() {
   check(av_fetch_updates(h_, out.data(), (int64_t)out.size(), &n));
   out.resize((size_t)n);
   return out;
+}
+
+void Engine::Rounds(int32_t rounds, const Deliver& deliver) {
+  SyncValidity();
+  std::vector<int64_t> pend;
+  auto drain = [&](int64_t t) {
+    const void* s = nullptr;
+    int64_t n = 0;
+    check(av_fetch_compact_wait(h_, t, &s, &n));
+    DecodeCompact(s, n, deliver);
+  };
+  for (int32_t r = 0; r < rounds; ++r) {
+    check(av_run_rounds(h_, 1));
+    int64_t t = 0;
+    check(av_fetch_compact_async(h_, &t));  // waits for the round, encodes, starts the copy
+    pend.push_back(t);
+    if (pend.size() >= 2) {  // the previous round's stream landed while this round ran
+      drain(pend.front());
+      pend.erase(pend.begin());
+    }
+  }
+  for (int64_t t : pend) drain(t);
+}
+
+void Engine::DecodeCompact(const void* stream, int64_t bytes, const Deliver& deliver) const {
+  av_compact_header h;
+  if (bytes < (int64_t)sizeof(h)) throw Error(AV_ERR_INVALID_ARG, "compact stream shorter than its header");
+  std::memcpy(&h, stream, sizeof(h));
+  if (h.magic != AV_COMPACT_MAGIC || h.bytes != bytes) throw Error(AV_ERR_INVALID_ARG, "not a compact stream");
+  const auto* base = static_cast<const uint8_t*>(stream);
+  const uint64_t n_idx = (uint64_t)h.n_rounds * (uint64_t)h.chunks + 1;
+  const auto* idx = reinterpret_cast<const uint64_t*>(base + sizeof(h));
+  const uint8_t* g = base + sizeof(h) + n_idx * 16;
+  const uint32_t tb = (uint32_t)h.target_bits, cw = (uint32_t)h.code_bytes, tmask = (1u << tb) - 1u;
+  std::vector<StatusUpdate> ups;
+  for (uint64_t j = 0; j + 1 < n_idx; ++j) {
+    const int64_t round = h.log_base + (int64_t)(j / (uint64_t)h.chunks);
+    for (uint64_t at = idx[2 * j]; at < idx[2 * j + 2];) {
+      uint32_t node = 0, cnt = 0;
+      std::memcpy(&node, g + at, 4);
+      std::memcpy(&cnt, g + at + 4, 4);
+      ups.resize(cnt);
+      for (uint32_t i = 0; i < cnt; ++i) {
+        uint32_t code = 0;
+        std::memcpy(&code, g + at + 8 + (size_t)i * cw, cw);  // little-endian 2- or 4-byte code
+        const int64_t slot = h.target_base + (int64_t)((code >> 2) & tmask);
+        ups[i].hash = slot < (int64_t)hashes_.size() ? hashes_[(size_t)slot] : (Hash)slot;
+        ups[i].status = (Status)(code & 3u);
+      }
+      deliver(round, (NodeID)node, ups);
+      at += 8 + (((uint64_t)cnt * cw + 3) & ~3ull);
+    }
+  }
 }
 
 Processor::Processor(std::shared_ptr<Engine> engine, NodeID node, Connman* connman)

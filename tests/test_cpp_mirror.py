@@ -27,5 +27,6 @@ def test_cpp_mirror_reference_tests():
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
-    for name in ("TestBlockRegister", "TestMultiBlockRegister", "SuitableNodeAndInvalidTarget", "NetworkRounds"):
+    for name in ("TestBlockRegister", "TestMultiBlockRegister", "SuitableNodeAndInvalidTarget", "NetworkRounds",
+                 "PipelinedRounds"):
         assert f"PASS {name}" in r.stdout

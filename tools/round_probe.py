@@ -30,8 +30,11 @@ def main():
     ap.add_argument("--option", action="append", default=[])
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0xA7A1A9C4)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--nodes", type=int, default=None, help="override the workload's node count (size scaling)")
     args = ap.parse_args()
     n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[args.workload]
+    if args.nodes:
+        n = args.nodes
     e = avhip.Engine(n, m, k=k, seed=args.seed, byz_threshold=byz, log_capacity=min(n * m // 2 + (1 << 20), 1 << 31))
     for o in args.option:
         name, v = o.split("=")
