@@ -119,7 +119,7 @@ PARALLELISM = {
 
 KERNEL_SRC = [os.path.join(ROOT, "go-avalanche_amd", "csrc", f) for f in
               ("round_sweep.hip", "round_node.hip", "kernels.hip", "log_ops.hip", "round_common.h", "round_slots.h",
-               "kernels.h", "engine.cpp")]
+               "kernels.h", "dev_scan.h", "engine.cpp")]
 
 
 class BenchFailure(SystemExit):
@@ -792,7 +792,7 @@ def allgather_probe(world, local_rank, total_bytes=1_000_000 * 128, reps=5):
             "note": "C4 node-sharded round exchange (1M x 1000 bits), torch.distributed all_gather_into_tensor"}
 
 
-PMC_DIR = os.path.join(ROOT, "profiles", "r05")
+PMC_DIR = os.path.join(ROOT, "profiles", "r06")
 
 
 def load_pmc(wl, window, world):
