@@ -427,7 +427,8 @@ def compact_pipeline(run, rounds=4, most_updates=0):
     stream in host memory. Then the same with every stream also expanded into the caller's packed
     words (av_compact_expand, host threads; ctypes releases the GIL) on a consumer thread, which
     reads stream r while streams r + 1 and r + 2 are encoded and copied (the engine keeps three).
-    A first pass (untimed) grows the engine's delivery buffers."""
+    Two first passes (untimed) grow the engine's delivery buffers: Byzantine rows follow the absolute
+    round's parity (byz_pattern), so the same epoch rounds emit different amounts a pass later."""
     from concurrent.futures import ThreadPoolExecutor
 
     eng = run.eng
@@ -436,7 +437,7 @@ def compact_pipeline(run, rounds=4, most_updates=0):
     words = np.empty(max(most_updates, 1) + (1 << 20), np.uint64)
     words.fill(0)
     pool = ThreadPoolExecutor(max_workers=1)
-    for mode in ("warm", "stream", "expanded"):
+    for mode in ("warm", "warm", "stream", "expanded"):
         run.goto(0)
         eng.synchronize()
         a0 = eng.applied_votes()
