@@ -150,6 +150,11 @@ struct av_engine {
   // diagnostics option "unsynced_shard": a node-sharded engine runs rounds with no exchange (other
   // shards' preference rows keep their initial values; per-rank kernel timing only, invalid results)
   bool unsynced_shard = false;
+  // diagnostics option "warm_pref": before each timed round, read the snapshots the round gathers
+  // from (untimed), as a GPU of the rank's own would hold them in its caches (tools/group_model.py:
+  // the serial group runs every rank's kernel on one GPU, each after the others' traffic)
+  bool warm_pref = false;
+  uint32_t* touch_sink = nullptr;
   // round kernels (option "kernel"): 2 = k_round_sweep (uncapped) / k_round_node (capped), k <= 8;
   // 1 = k_round_fast / k_round_capped (the first versions; any k, A/B baseline)
   int kernel = 2;
@@ -805,6 +810,11 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     p.uni_post = peer && sweep && !replay ? 1u : 0u;  // the slot reaches the peers in the barrier kernel
   }
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (e->warm_pref && sweep) {  // diagnostics (untimed): the round's gather sources, read once
+    if (!e->touch_sink) AV_HIP(hipMalloc(&e->touch_sink, 64));
+    AV_HIP(avk::launch_touch(p.pref_prev, (size_t)e->N * e->PS * 4u, e->touch_sink, e->stream));
+    AV_HIP(avk::launch_touch(p.pref_in, (size_t)e->N * e->PS * 4u, e->touch_sink, e->stream));
+  }
   if (e->timing) {
     AV_HIP(hipEventCreate(&ev0));
     AV_HIP(hipEventCreate(&ev1));
@@ -1084,6 +1094,7 @@ int av_destroy(av_engine* e) {
   }
   if (e->invs_host) (void)hipHostFree(e->invs_host);
   if (e->enc_err) (void)hipFree(e->enc_err);
+  if (e->touch_sink) (void)hipFree(e->touch_sink);
   if (e->enc_tot) (void)hipFree(e->enc_tot);
   if (e->changed) (void)hipFree(e->changed);
   if (e->push_tbl) (void)hipFree(e->push_tbl);
@@ -2679,6 +2690,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     if (rc != AV_OK) return rc;
   } else if (n == "unsynced_shard") {
     e->unsynced_shard = value != 0;
+  } else if (n == "warm_pref") {
+    e->warm_pref = value != 0;
   } else if (n == "round_marker") {
     e->round_marker = value != 0;
   } else if (n == "virtual_votes") {  // 0: always store the vote planes (A/B)

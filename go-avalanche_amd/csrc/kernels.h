@@ -471,6 +471,8 @@ hipError_t launch_encode_log(const EncodeParams& p, uint64_t entries, void* scra
 // Copy bytes (rounded up to 16; both buffers 16-B aligned and that large) from device memory into
 // host-mapped pinned memory with `blocks` workgroups (k_stream_out).
 hipError_t launch_stream_out(const void* src, void* dst, uint64_t bytes, uint32_t blocks, hipStream_t s);
+// diagnostics: read `bytes` of src once (log_ops.hip k_touch)
+hipError_t launch_touch(const void* src, uint64_t bytes, uint32_t* sink, hipStream_t s);
 // Drop-in batch grouping: stable radix sort of (lane key, position) into (keys_s, perm_s) (keys_t,
 // perm_t: the other buffer set), run-length encoding into lanes / offs (n_runs + 1) / *n_runs, and the
 // (vote index, packed vote) entries in grouped order. scratch: group_votes_scratch_words(n) u64.

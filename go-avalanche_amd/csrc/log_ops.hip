@@ -783,6 +783,29 @@ hipError_t launch_stream_out(const void* src, void* dst, uint64_t bytes, uint32_
   return hipGetLastError();
 }
 
+// Diagnostics (engine option "warm_pref"): read a buffer once, so that the round kernel timed after
+// it finds the lines where a GPU of its own would have them (tools/group_model.py --warm-pref). The
+// sum is stored only if it equals a value no read can produce in practice, so the loads stay.
+namespace {
+__global__ __launch_bounds__(256) void k_touch(const u32x4* __restrict__ src, uint64_t n16, uint32_t* sink) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256u;
+  uint32_t acc = 0u;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n16; i += stride) {
+    const u32x4 v = src[i];
+    acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+}  // namespace
+
+hipError_t launch_touch(const void* src, uint64_t bytes, uint32_t* sink, hipStream_t s) {
+  const uint64_t n16 = bytes / 16u;
+  if (!n16) return hipSuccess;
+  const uint32_t g = (uint32_t)std::min<uint64_t>(4096, (n16 + 255u) / 256u);
+  hipLaunchKernelGGL(k_touch, dim3(g), dim3(256), 0, s, static_cast<const u32x4*>(src), n16, sink);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // Drop-in RegisterVotes batch (engine.cpp av_register_votes_batch): group the votes by lane (node,
 // 32-target block) keeping their order inside a lane — the stable radix sort of (lane, position) —

@@ -1007,7 +1007,6 @@ __device__ __forceinline__ uint32_t settled_run_uni(const RoundParams& p, uint32
     for (uint32_t i = 0; i < kUniRun; ++i) {
       const uint32_t g = (t0 + i) * 64u + lane;
       const bool active = g < p.L;
-      const uint32_t rel = rel0 + i * npt;
       const uint32_t P0 = active ? vw : 0u;  // polled = live (kPendAllLive) and valid
       const uint32_t A = Av[i];
       const uint32_t mis = __ballot((refp ^ A) & P0) != 0ull ? 1u : 0u;  // always evaluated: no branch

@@ -217,6 +217,9 @@ for s in "$@"; do
     barrierfold) step barrierfold 300 bash -c 'for o in fold_arrival=0 fold_arrival=1; do python tools/barrier_cost.py --world 2 --nodes 131072 --option $o --json gpurun_out/barrier2_big_$o.json && python tools/barrier_cost.py --world 2 --nodes 1000000 --rounds 40 --option $o --json gpurun_out/barrier2_c4_$o.json && python tools/barrier_cost.py --world 2 --option $o --json gpurun_out/barrier2_small_$o.json || exit 1; done' ;;
     abw6) step abw6 600 bash -c 'for w in c4 c4p c4pb; do for v in base w6 w7; do echo "== $w $v"; if [ $v = base ]; then python tools/round_probe.py --workload $w; else AVHIP_LIB=go-avalanche_amd/lib/variants/libavhip_$v.so python tools/round_probe.py --workload $w; fi; done; done' ;;
     mall) step mall 600 python tools/mall_probe.py --workload c4p --shards 1,8 --kinds nodes,targets --json $OUT/mall_probe_c4p.json ;;
+    gm_warm) step gm_warm_c4p 900 python tools/group_model.py --workload c4p --ranks 8 --kinds targets,masked --all-option warm_pref=1 --json $OUT/gm_warm_c4p.json && \
+             step gm_cold_c4p 900 python tools/group_model.py --workload c4p --ranks 8 --kinds targets,masked --json $OUT/gm_cold_c4p.json && \
+             step gm_warm_c4 900 python tools/group_model.py --workload c4 --ranks 8 --kinds targets,masked --all-option warm_pref=1 --json $OUT/gm_warm_c4.json ;;
     pmcall) for W in c4 c4p c4pb c3 c5; do WL=$W bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $?; done
             WL=c2 PMC_LAUNCHES=2 PMC_REPLAY=1 bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $? ;;
     bench4) step bench 900 python bench.py --detail gpurun_out/bench_detail.json ;;

@@ -91,10 +91,13 @@ def window(engs, init, warmup, steps, on_round):
         e.set_timing(False)
 
 
+ALL_OPTIONS = []  # --all-option: set on every engine (one-GPU, target shards, groups)
+
+
 def run_single(n, m, k, byz, init, warmup, steps, options=(), **kw):
     e = avhip.Engine(n, m, k=k, seed=SEED, byz_threshold=byz, log_capacity=log_cap(kw.get("nl", n), m), **{
         k2: v for k2, v in kw.items() if k2 != "nl"})
-    for name, v in options:
+    for name, v in list(ALL_OPTIONS) + list(options):
         e.set_option(name, v)
     rows = []
     window([e], init, warmup, steps, lambda r, ms, pw: None)  # device warm-up
@@ -114,7 +117,7 @@ def run_group(n, m, k, byz, init, warmup, steps, g, mask, t_range=None, options=
         engs.append(avhip.Engine(n, mm, k=k, seed=SEED, byz_threshold=byz, log_capacity=log_cap(per, mm), **kw))
     for e in engs:
         e.set_option("peer_mask", mask)
-        for name, v in options:
+        for name, v in list(ALL_OPTIONS) + list(options):
             e.set_option(name, v)
         e.init_records(*init)
     avhip.peer_group_serial(engs)
@@ -153,8 +156,12 @@ def main():
                     help="name=value on the target-shard engines (an extra 'targets+' row)")
     ap.add_argument("--variant", action="append", default=[],
                     help="name:opt=v,opt=v -- an extra masked node-shard row with engine options (A/B)")
+    ap.add_argument("--all-option", action="append", default=[],
+                    help="name=value on every engine, e.g. warm_pref=1: each rank's gather sources read "
+                         "(untimed) before its timed kernel, as its own GPU's caches would hold them")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
+    ALL_OPTIONS.extend((o.split("=")[0], int(o.split("=")[1])) for o in args.all_option)
     topts = [(o.split("=")[0], int(o.split("=")[1])) for o in args.target_option]
     N, M, K, init_mode, init_param, byz, replay, desc = WORKLOADS[args.workload]
     assert not replay, "sim workloads only"
@@ -163,7 +170,7 @@ def main():
     t0 = time.time()
     one = run_single(N, M, K, byz, init, args.warmup, args.steps)
     t1 = sum(r["ms"] for r in one)
-    out = {"workload": desc, "window": f"{args.warmup}+{args.steps}", "one_gpu": one, "one_gpu_ms": t1,
+    out = {"workload": desc, "window": f"{args.warmup}+{args.steps}", "all_options": args.all_option, "one_gpu": one, "one_gpu_ms": t1,
            "link_GBs_per_direction": XGMI_LINK_GBS, "barrier_us": args.barrier_us, "ranks": {},
            "model": "round = max over ranks of max(kernel ms, busiest link ms) + barrier; link ms = words pushed "
                     "/ peers * 4 B / link GB/s (one xGMI link per peer, pushes overlap the kernel)"}
