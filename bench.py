@@ -536,13 +536,13 @@ def measure(wl, args, world, rank, local_rank, steps, warmup):
     # ---- device warm-up (untimed): after process start the GPU runs these
     # kernels up to ~15 % slower for the first ~20-30 ms of sustained load
     # (tools/gap_probe.py --events-first): one untimed epoch,
-    # one round at a time in a log of one entry per lane and kind (what one
-    # round can emit at most), counting each round's entries; then the log is
-    # sized for the largest timed segment
+    # one round at a time in a log of two single words and one record per lane
+    # (what one round can emit at most), counting each round's entries; then the
+    # log is sized for the largest timed segment
     log_bytes = None
     if not replay:
         lanes = eng.layout_info()["lanes"]
-        eng.resize_log(lanes, lanes, lanes)
+        eng.resize_log(2 * lanes, lanes, lanes)
         per_round = {}
         run.steps(EPOCH, timed=False, entries=per_round)
         log_bytes = size_log(eng, per_round, warmup, steps)

@@ -620,10 +620,24 @@ __device__ __forceinline__ uint32_t lane_updates8(const uint32_t* E, int K) {
 //  * AVK_MED_S4 = 0: a 16-byte record folding up to kMedMax updates into 10-bit fields, walked one
 //    update per step (the round-3 form, kept for A/B).
 constexpr uint32_t kLkSingle = 1u << 8, kLkMed = 2u << 8, kLkDense = 3u << 8;
+constexpr uint32_t kLkTwo = 1u << 10;  // a single-word lane with two updates (SMAX = 2)
 
-template <int K>
+// SMAX (AVK_MED_S4, k = 8): a lane with at most SMAX updates logs them as single packed words (8 B
+// each) instead of a 32-B slot record. At 2 (round 6, build knob AVK_SINGLE_MAX for k_round_sweep)
+// two words take 16 B where the record took 32, and in conflicting rounds a third of the lanes have
+// exactly two updates (the pair's two targets flip together): C4p's log shrinks from 25.6 to 20.3 B
+// per lane. The store needs no per-update loop (the second update is the first's slot's next bit, or
+// the next slot's only bit). Measured level (C4p epoch 6.43-6.50 ms at 1 and 2, C4 3.58-3.65, C4pb
+// 6.49-6.52; profiles/r06/delivery/ab_smax.log): the storm rounds are not paced by the log's bytes,
+// and two words are two entries for the delivery encoder, so 1 stays the default.
+#ifndef AVK_SINGLE_MAX
+#define AVK_SINGLE_MAX 1
+#endif
+
+template <int K, int SMAX = 1>
 __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32_t shard, uint32_t lane,
                                                     const uint32_t (&E)[K], uint32_t died, uint32_t& updates) {
+  static_assert(SMAX == 1 || SMAX == 2, "one or two single words per lane");
   EmitRes r;
   uint32_t any = 0;
 #pragma unroll
@@ -639,10 +653,11 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
 #pragma unroll
   for (int j = 0; j < K; ++j) nz |= (E[j] != 0u ? 1u : 0u) << j;
   const uint32_t ns = (uint32_t)__popc(nz);
-  const bool single = cnt == 1u;
-  const bool med = cnt >= 2u && (ns <= 3u || (ns == 4u && died == 0u));
-  const bool dense = cnt >= 2u && !med;
-  r.lk = nz | (single ? kLkSingle : med ? kLkMed : dense ? kLkDense : 0u);
+  const bool two = SMAX >= 2 && cnt == 2u;
+  const bool single = cnt == 1u || two;
+  const bool med = cnt > (uint32_t)SMAX && (ns <= 3u || (ns == 4u && died == 0u));
+  const bool dense = cnt > (uint32_t)SMAX && !med;
+  r.lk = nz | (single ? kLkSingle : med ? kLkMed : dense ? kLkDense : 0u) | (two ? kLkTwo : 0u);
 #else
   (void)died;
   const uint32_t dmin = AVK_MED_DENSE_MIN ? AVK_MED_DENSE_MIN : max(p.dense_min, kMedMax + 1u);
@@ -651,6 +666,9 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
   r.tot_d = (uint32_t)__popcll(__ballot(dense));
   r.tot_m = (uint32_t)__popcll(__ballot(med));
   r.tot_s = (uint32_t)__popcll(__ballot(single));
+#if AVK_MED_S4
+  if constexpr (SMAX >= 2) r.tot_s += (uint32_t)__popcll(__ballot(two));  // words, not lanes
+#endif
   updates += wave_sum(cnt);
   if (p.ablate_emit == 1u) return r;  // diagnostics: the cost of the round without its log stores
   // one atomic instruction, lanes 0 / 1 / 2 reserving the singles / medium / dense runs
@@ -681,7 +699,7 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
 
 // The store half: every lane with updates stores its one entry at its rank among the wave's lanes
 // of its kind (see emit_updates_med). Returns the bytes stored (wave-uniform).
-template <int K>
+template <int K, int SMAX = 1>
 __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_t shard, uint32_t lane,
                                                    uint32_t node, uint32_t tbase, const uint32_t (&E)[K],
                                                    uint32_t A_final, uint32_t died, const EmitRes& r,
@@ -692,7 +710,9 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
   if constexpr (K == 8) {
     const uint32_t kind = r.lk & (3u << 8), nz = r.lk & 0xFFu;
     const bool dense = kind == kLkDense, med = kind == kLkMed, single = kind == kLkSingle;
+    const bool two = SMAX >= 2 && (r.lk & kLkTwo) != 0u;
     const uint64_t dl = __ballot(dense), ml = __ballot(med), sl = __ballot(single);
+    const uint64_t tl = SMAX >= 2 ? __ballot(two) : 0ull;
     const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 0);
     const uint32_t mbase = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 1);
     const uint32_t dbase = (uint32_t)__builtin_amdgcn_readlane((int)r.raw, 2);
@@ -702,7 +722,9 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
     const bool ovf = st_d < r.tot_d || st_m < r.tot_m || st_s < r.tot_s;
     const uint64_t key = pack_update(round_rel, node, 0u, tbase, 0u, p.round_shift);
     const uint64_t mine = dense ? dl : med ? ml : sl;
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+    uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+    if (SMAX >= 2 && single)  // the lower lanes' second words come first
+      rank += __builtin_amdgcn_mbcnt_hi((uint32_t)(tl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tl, 0u));
     if (dense) {
       if (rank < st_d) {
         constexpr uint32_t DW = dense_words(K);
@@ -731,11 +753,24 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
           pst4<AVK_LOG_NT>(q + 1, u32x4{o0, o1, o2, hasd ? died : o3});
         }
       } else if (single && rank < st_s) {
-        // the one update: slot ffbl(nz), record ffbl(o0); status from A_final and died (vote.go:77-91)
+        // the first update: slot ffbl(nz), record ffbl(o0); status from A_final and died (vote.go:77-91)
         const uint32_t j = ffbl_u32(nz), bit = ffbl_u32(o0);
-        const uint32_t a = bfe1(A_final, bit), d = bfe1(died, bit);
-        const uint32_t st = (a << 1) | (~(a ^ d) & 1u);
+        uint32_t a = bfe1(A_final, bit);
         uint64_t* const w = p.log + (size_t)shard * p.log_cap + base + rank;
+        if (SMAX >= 2 && two) {
+          // the second: o0's next bit (same slot), else the next slot's only bit. A record with both
+          // (the same bit in two slots: a flip and its flip back) had A_final ^ 1 after the first
+          const uint32_t rest = o0 & (o0 - 1u);
+          const uint32_t j2 = rest ? j : ffbl_u32(nz & (nz - 1u)), bit2 = ffbl_u32(rest ? rest : o1);
+          a ^= (j2 != j && bit2 == bit) ? 1u : 0u;
+          const uint32_t a2 = bfe1(A_final, bit2), d2 = bfe1(died, bit2);
+          const uint64_t word2 = key + ((uint64_t)j2 << 24) + ((uint64_t)bit2 << 2) + ((a2 << 1) | (~(a2 ^ d2) & 1u));
+          if (rank + 1u < st_s) {
+            if constexpr (AVK_LOG_NT) __builtin_nontemporal_store(word2, w + 1); else w[1] = word2;
+          }
+        }
+        const uint32_t d = bfe1(died, bit);
+        const uint32_t st = (a << 1) | (~(a ^ d) & 1u);
         const uint64_t word = key + ((uint64_t)j << 24) + ((uint64_t)bit << 2) + st;
         if constexpr (AVK_LOG_NT) __builtin_nontemporal_store(word, w); else *w = word;
       }

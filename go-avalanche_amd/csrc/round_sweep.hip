@@ -615,7 +615,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   // StatusUpdate log reservation (k = 8) before this tile's plane and published-word stores, so that
   // reading the atomics' results waits for them alone, not for those stores (round_common.h)
   EmitRes er{};
-  if constexpr (K == 8) er = emit_reserve_med<K>(p, acc.shard, lane, E, died, acc.updates);
+  if constexpr (K == 8) er = emit_reserve_med<K, AVK_SINGLE_MAX>(p, acc.shard, lane, E, died, acc.updates);
 #endif
   {
     uint32_t cy = 0u;
@@ -695,7 +695,7 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
   uint32_t emitted;
   if constexpr (K == 8)
 #if AVK_EMIT_HOIST
-    emitted = emit_store_med<K>(p, acc.shard, lane, node, p.t0 + b * 32u, E, A, died, er, p.round_rel);
+    emitted = emit_store_med<K, AVK_SINGLE_MAX>(p, acc.shard, lane, node, p.t0 + b * 32u, E, A, died, er, p.round_rel);
 #else
     emitted = emit_updates_med<K>(p, acc.shard, lane, node, p.t0 + b * 32u, E, A, died, acc.updates, p.round_rel);
 #endif

@@ -290,15 +290,18 @@ int av_live_records(av_engine* e, int32_t honest_only, int64_t* out);
 int av_discard_updates(av_engine* e);
 /* Log entries pending, per kind: out = {single updates, slot records (2-4
  * slots of one 32-record lane), dense records (a lane's whole round)}; a
- * lane's updates of one round are one entry. Sizing input for av_resize_log. */
+ * lane's updates of one round are one slot or dense record, or (k = 8 sweep
+ * rounds: at most two updates) one or two single words. Sizing input for
+ * av_resize_log. */
 int av_log_entries(av_engine* e, int64_t out[3]);
 /* Re-allocate the (empty: AV_ERR_UNSUPPORTED otherwise) device log for about
  * entries[k] entries of each kind (8, 32 and 48 B each at k = 8), instead of
  * av_config.update_log_capacity's worst case per update (36 B per update).
  * The log is sharded by the round kernel's writer waves: each writer wave gets
  * ceil(entries[k] / writers) + 1 entries, i.e. the sizing assumes the entries
- * are spread evenly over the writers. That holds for entries[k] = the lane
- * count (one round never needs more than one entry per lane of each kind); a
+ * are spread evenly over the writers. That holds for entries = {2, 1, 1} x the
+ * lane count (one round never needs more than two single words or one record
+ * per lane); a
  * measured count with skewed emission can overflow one shard while the total
  * stays below entries[k] — the overflow is detected (av_update_log_overflowed,
  * AV_ERR_OVERFLOW on fetch), never silent. */

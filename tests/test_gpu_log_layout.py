@@ -170,15 +170,16 @@ def test_solo_barrier_is_sticky():
 
 @pytest.mark.parametrize("n,m", [(6000, 1000), (5000, 2000)], ids=["even", "uneven_writers"])
 def test_resize_log_one_entry_per_lane(n, m):
-    """A log of one entry per lane and kind holds any single round (a lane's
-    updates of a round are one entry), here the storm round of conflicting
-    pairs; av_log_entries counts them by kind; a log holding updates is not
+    """A log of two single words and one record per lane holds any single round
+    (a lane's updates of a round are one record, or at most two single words),
+    here the storm round of conflicting pairs, whose lanes mostly log exactly
+    two words; av_log_entries counts them by kind; a log holding updates is not
     re-sized. 5000 x 2000 (BL 63: 1231 writer waves over 256 shards) gives
     some shards one writer more than others: the sizing serves the fullest
     shard (C3's bench log overflowed at one entry per lane before)."""
     e = avhip.Engine(n, m, k=8, seed=9, log_capacity=1 << 20)
     lanes = e.layout_info()["lanes"]
-    e.resize_log(lanes, lanes, lanes)
+    e.resize_log(2 * lanes, lanes, lanes)
     ref = avhip.Engine(n, m, k=8, seed=9, log_capacity=1 << 26)
     for x in (e, ref):
         x.init_records(avhip.INIT_PAIRS, 0)
@@ -187,10 +188,10 @@ def test_resize_log_one_entry_per_lane(n, m):
             x.run_rounds(1)
         ent = e.log_entries()
         assert not e.log_overflowed()
-        assert 0 < sum(ent) <= e.updates_count() and max(ent) <= lanes
+        assert 0 < sum(ent) <= e.updates_count() and ent[0] <= 2 * lanes and max(ent[1:]) <= lanes
         if r == 1:
             with pytest.raises(avhip.AvError):
-                e.resize_log(lanes, lanes, lanes)
+                e.resize_log(2 * lanes, lanes, lanes)
         assert np.array_equal(e.fetch_updates(decode=False), ref.fetch_updates(decode=False))
     # sized below one round's needs: the overflow is reported, never silent
     e.resize_log(16, 16, 16)

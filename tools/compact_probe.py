@@ -40,7 +40,7 @@ def main():
         k_, v_ = o.split("=")
         e.set_option(k_, int(v_))
     lanes = e.layout_info()["lanes"]
-    e.resize_log(lanes, lanes, lanes)
+    e.resize_log(2 * lanes, lanes, lanes)
     words = np.empty(150_000_000, np.uint64)
     words.fill(0)
     out = {"workload": a.workload, "options": a.option, "phases": [], "pipelined": []}

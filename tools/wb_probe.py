@@ -48,7 +48,7 @@ def main():
         n, m, k, init_mode, init_param, byz, replay, desc = WORKLOADS[wl]
         e = avhip.Engine(n, m, k=k, seed=0xA7A1A9C4, byz_threshold=byz, log_capacity=0)
         lanes = e.layout_info()["lanes"]
-        e.resize_log(lanes, lanes, lanes)
+        e.resize_log(2 * lanes, lanes, lanes)
         for end in [int(x) for x in args.ends.split(",")]:
             for run in [int(x) for x in args.runs.split(",")]:
                 e.set_option("materialize_run", run)
