@@ -268,6 +268,7 @@ struct av_engine {
   // responder variant (option "responder", kernels.h pub_mode) and the nodes
   // that no longer poll (av_set_polling); both run the first-generation kernel
   uint32_t dense_min = 0;  // option "dense_min" (kernels.h dense records; default dense_min(k))
+  uint32_t wave_dense = 0;  // option "wave_dense" (kernels.h RoundParams::wave_dense; A/B)
   int32_t pub_mode = 0;
   uint32_t* readd = nullptr;     // [L] pub_mode 2: re-add marks
   uint32_t* died_out = nullptr;  // [L] pub_mode 2: records deleted this round
@@ -429,6 +430,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.died_out = e->pub_mode == 2 ? e->died_out : nullptr;
   p.nopoll = e->any_nopoll ? e->nopoll : nullptr;
   p.dense_min = e->dense_min;
+  p.wave_dense = e->wave_dense;
   return p;
 }
 
@@ -2722,6 +2724,9 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     rc = refresh_pref(e);  // republish the current snapshot under the new rule
     if (rc != AV_OK) return rc;
     AV_HIP(hipStreamSynchronize(e->stream));
+  } else if (n == "wave_dense") {  // A/B: the dense log must hold one record per lane with updates
+    AV_CHECK(value >= 0 && value <= 64, AV_ERR_INVALID_ARG, "bad wave_dense");
+    e->wave_dense = (uint32_t)value;
   } else if (n == "dense_min") {  // tuning (A/B): fewer updates per dense record; the dense log may fill sooner
     AV_CHECK(value >= 1 && value <= 32 * (int64_t)e->k + 1, AV_ERR_INVALID_ARG, "bad dense_min");
     e->dense_min = (uint32_t)value;

@@ -653,10 +653,12 @@ __device__ __forceinline__ EmitRes emit_reserve_med(const RoundParams& p, uint32
 #pragma unroll
   for (int j = 0; j < K; ++j) nz |= (E[j] != 0u ? 1u : 0u) << j;
   const uint32_t ns = (uint32_t)__popc(nz);
-  const bool two = SMAX >= 2 && cnt == 2u;
-  const bool single = cnt == 1u || two;
-  const bool med = cnt > (uint32_t)SMAX && (ns <= 3u || (ns == 4u && died == 0u));
-  const bool dense = cnt > (uint32_t)SMAX && !med;
+  // (A/B option wave_dense: a wave with many lanes holding updates logs them all dense)
+  const bool wd = p.wave_dense != 0u && (uint32_t)__popcll(__ballot(cnt != 0u)) >= p.wave_dense;
+  const bool two = !wd && SMAX >= 2 && cnt == 2u;
+  const bool single = !wd && (cnt == 1u || two);
+  const bool med = !wd && cnt > (uint32_t)SMAX && (ns <= 3u || (ns == 4u && died == 0u));
+  const bool dense = wd ? cnt != 0u : cnt > (uint32_t)SMAX && !med;
   r.lk = nz | (single ? kLkSingle : med ? kLkMed : dense ? kLkDense : 0u) | (two ? kLkTwo : 0u);
 #else
   (void)died;
@@ -734,7 +736,7 @@ __device__ __forceinline__ uint32_t emit_store_med(const RoundParams& p, uint32_
         pst4<AVK_LOG_NT>(q + 1, u32x4{E[2], E[3], E[4], E[5]});
         pst4<AVK_LOG_NT>(q + 2, u32x4{E[6], E[7], A_final, died});
       }
-    } else {
+    } else if (med || single) {  // (lanes without updates skip the network: a wave of dense lanes skips it)
       // the first 4 slots with updates, in slot order: shift in from the last slot down
       uint32_t o0 = 0u, o1 = 0u, o2 = 0u, o3 = 0u;
 #pragma unroll
