@@ -7,7 +7,8 @@ C5; flip-flop voters for C3).
 * C4 (1M nodes x 1000 targets, Bernoulli(0.8)) and C3 (100k x 2000, 20 %
   Byzantine, double-spend pairs): every round's StatusUpdates are compared as
   an order-independent digest (count, sum and xor of splitmix64 over the
-  packed words: av_updates_digest vs the oracle's avo_sim_round_ex), the
+  packed words: av_updates_digest vs the oracle's avo_sim_round_ex; in some
+  rounds the whole stream delivered to the host, in canonical order), the
   applied-vote count every round, and the full record state at several rounds
   including the finalization storm (C4 rounds 16-18). C3 also compares the
   full update rows of some rounds.
@@ -57,9 +58,28 @@ def compare_state(eng, sim, n, where, chunk=100_000):
             raise AssertionError(f"state mismatch {where}: {msg}")
 
 
-def step(eng, sim, r, collect_rows=False):
-    """One round on both sides; StatusUpdates compared (digest, or rows)."""
+def step(eng, sim, r, collect_rows=False, order=None):
+    """One round on both sides; StatusUpdates compared (digest, or rows). order="words" / "compact":
+    the round's whole stream is delivered to the host (av_fetch_updates, or the compact stream
+    expanded by av_compact_expand) and must be strictly ascending packed words — the canonical
+    (round, node, slot, target) order, processor.go:94,111 — whose digest equals the oracle's: a
+    sorted sequence of distinct words is fixed by its set, so this pins the full-size stream's order
+    and content without holding the oracle's rows."""
     eng.run_rounds(1)
+    if order:
+        from oracle import cabi
+        if order == "compact":
+            s = eng.fetch_compact()
+            assert avhip.compact_header(s)["log_base"] == eng.round - 1
+            raw = avhip.compact_expand(s)
+            del s
+        else:
+            raw = eng.fetch_updates(decode=False)
+        exp, applied = sim.run_round(threads=T, collect=False, round_rel=0)
+        assert raw.size == exp[0], f"round {r}: {raw.size} words, oracle {exp[0]}"
+        assert np.all(raw[1:] > raw[:-1]), f"round {r}: delivered words not in canonical order"
+        assert cabi.update_digest(raw) == exp, f"round {r}: delivered stream differs from the oracle's"
+        return applied, exp[0]
     if collect_rows:
         got = eng.fetch_updates()
         exp, applied = sim.run_round(threads=T)
@@ -89,12 +109,17 @@ def c4_pair(oracle):
     sim.close()
 
 
+# rounds whose whole stream is delivered to the host in canonical order (step's `order`)
+C4_ORDER = {1: "words", 17: "compact"}
+C4P_ORDER = {3: "compact", 12: "words"}
+
+
 def run_c4(c4_pair, last, states):
     eng, sim, st = c4_pair
     n, m = C4["n"], C4["m"]
     while st["round"] <= last:
         r = st["round"]
-        applied, _ = step(eng, sim, r)
+        applied, _ = step(eng, sim, r, order=C4_ORDER.get(r))
         st["applied"] += applied
         st["round"] += 1
         if r < 16:  # all records live: every node polls every target k times (R1)
@@ -158,7 +183,7 @@ def run_c4p(pair, last, states):
     n, m = C4P["n"], C4P["m"]
     while st["round"] <= last:
         r = st["round"]
-        applied, nupd = step(eng, sim, r)
+        applied, nupd = step(eng, sim, r, order=C4P_ORDER.get(r))
         print(f"C4p(b) round {r}: {nupd} StatusUpdates, digest equal", flush=True)
         st["applied"] += applied
         st["emitted"].append(nupd)
@@ -299,3 +324,24 @@ def test_c5_fullsize_sampled_oracle(oracle):
     # a finalized node publishes its decision (R2)
     assert np.array_equal(eng.read_pref(n - 50_000, n), ((recs >> 16) & 1).astype(np.uint8))
     eng.close()
+
+
+def test_c5_whole_network_rounds_0_5(oracle):
+    """C5's whole network (10M nodes x 256 targets, BL = 8) against the oracle holding all of it
+    (C5 parity was sampled only): rounds 0-5 (the fresh round, the storm rounds and the
+    first settled ones) with every round's update digest over all nodes, the applied votes, one
+    round's stream delivered in canonical order, and the full record state after rounds 2 and 5."""
+    n, m, k = 10_000_000, 256, 8
+    eng = avhip.Engine(n, m, k=k, seed=SEED, log_capacity=1_500_000_000)
+    eng.init_records(avhip.INIT_BERNOULLI, P80)
+    sim = oracle.Sim(n, m, k, seed=SEED, init_mode=avhip.INIT_BERNOULLI, init_param=P80, threads=T)
+    try:
+        for r in range(6):
+            applied, nupd = step(eng, sim, r, order="compact" if r == 1 else None)
+            print(f"C5 round {r}: {nupd} StatusUpdates equal", flush=True)
+            assert applied == n * m * k, r
+            if r in (2, 5):
+                compare_state(eng, sim, n, f"C5 after round {r}", chunk=500_000)
+    finally:
+        eng.close()
+        sim.close()
