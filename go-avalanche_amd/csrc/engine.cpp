@@ -269,6 +269,7 @@ struct av_engine {
   // that no longer poll (av_set_polling); both run the first-generation kernel
   uint32_t dense_min = 0;  // option "dense_min" (kernels.h dense records; default dense_min(k))
   uint32_t wave_dense = 0;  // option "wave_dense" (kernels.h RoundParams::wave_dense; A/B)
+  uint32_t uni_votes = 1;   // option "uni_votes" (kernels.h RoundParams::uni_votes)
   int32_t pub_mode = 0;
   uint32_t* readd = nullptr;     // [L] pub_mode 2: re-add marks
   uint32_t* died_out = nullptr;  // [L] pub_mode 2: records deleted this round
@@ -431,6 +432,7 @@ avk::RoundParams round_params(const av_engine* e, const uint32_t* replay) {
   p.nopoll = e->any_nopoll ? e->nopoll : nullptr;
   p.dense_min = e->dense_min;
   p.wave_dense = e->wave_dense;
+  p.uni_votes = e->uni_votes;
   return p;
 }
 
@@ -2724,6 +2726,8 @@ int av_set_option(av_engine* e, const char* name, int64_t value) {
     rc = refresh_pref(e);  // republish the current snapshot under the new rule
     if (rc != AV_OK) return rc;
     AV_HIP(hipStreamSynchronize(e->stream));
+  } else if (n == "uni_votes") {
+    e->uni_votes = value != 0 ? 1u : 0u;
   } else if (n == "wave_dense") {  // A/B: the dense log must hold one record per lane with updates
     AV_CHECK(value >= 0 && value <= 64, AV_ERR_INVALID_ARG, "bad wave_dense");
     e->wave_dense = (uint32_t)value;

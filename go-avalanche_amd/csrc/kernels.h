@@ -241,6 +241,8 @@ struct RoundParams {
   uint32_t* died_out;
   const uint32_t* nopoll;
   uint32_t dense_min;  // a lane with >= dense_min updates logs one dense record (default dense_min(k))
+  uint32_t uni_votes;  // k = 8 warm sweep, uniform input (uni_in): general-path tiles take the reference word
+                       // as their 8 votes instead of gathering them (option "uni_votes"; round_sweep.hip load_tile)
   uint32_t wave_dense; // k = 8 sweep (A/B option "wave_dense"): a wave with >= wave_dense lanes holding updates
                        // logs every such lane as a dense record (one store branch, no slot-word network); 0 off
 };

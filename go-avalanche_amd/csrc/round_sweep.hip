@@ -280,9 +280,14 @@ __device__ __forceinline__ LaneIdx lane_idx(const RoundParams& p, uint32_t tile,
   return x;
 }
 
+// uvotes (uniform input, p.uni_votes; the warm k = 8 sweep only): every row of pref_in is the reference
+// row of pref_prev (kernels.h uni_in), so each of the 8 votes a lane would gather is that row's word
+// for its block: one load of it instead of 8 gathers (a klazy round whose tiles are not yet settled
+// candidates, e.g. C4's round 4 after the network converged in round 3)
 template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE, bool VVM = false, bool FRESH = false, bool CC = true>
 __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
-                                          TileIn<K, REPLAY, WARM>& in, const WaveDraw* wd = nullptr) {
+                                          TileIn<K, REPLAY, WARM>& in, const WaveDraw* wd = nullptr,
+                                          bool uvotes = false) {
   const LaneIdx x = lane_idx(p, tile, lane);
   const uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
   const u32x4* const grp = reinterpret_cast<const u32x4*>(tp) + lane;
@@ -386,6 +391,12 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
         drawn = true;
       }
     }
+    if (uvotes) {  // wave-uniform: no draw of this round's peers, no gathers
+      const uint32_t rw = at_byte(p.pref_prev, p.ref_node * rb + bo);
+#pragma unroll
+      for (int j = 0; j < K; ++j) in.w[j] = rw;
+      return;
+    }
     if (!drawn) draw_peers<K>(p, p.round, x.node, x.nl, nlA, nn, lane, peers);
     if (!have_rows) {
 #pragma unroll
@@ -427,7 +438,8 @@ __device__ __forceinline__ void ref_flag_store(const RoundParams& p, uint32_t la
 
 template <int K, bool REPLAY, bool WARM, int POL, bool VVM = false, bool REF = false, bool CC = true>
 __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
-                                             const TileIn<K, REPLAY, WARM>& in, uint32_t extra_bytes, SweepAcc& acc) {
+                                             const TileIn<K, REPLAY, WARM>& in, uint32_t extra_bytes, SweepAcc& acc,
+                                             bool uvotes = false) {
   const LaneIdx x = lane_idx(p, tile, lane);
   const bool active = x.active;
   const uint32_t b = x.b, node = x.node;
@@ -714,14 +726,15 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
                           // virtual K4..K7 group (kHiVirt): not read (if K was read), not written
                           (WARM && (in.kw & kHiVirt) && !(kunread && kdefer) ? 16u : 0u) + (hv && !kdefer ? 16u : 0u);
   // V read: 32 B stored, 28 B regathered (stale), 0 B uniform
+  // uvotes: one 4-B reference word read instead of the K gathered votes
   acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale == kVStale ? 4u : in.stale == kVUniform ? 32u : 0u) -
                                  (virt ? 32u : 0u) - (cvirt ? 32u : 0u) + (p.count_changed ? 4u : 0u) -
-                                 kbytes - (astore ? 0u : 4u)
+                                 kbytes - (astore ? 0u : 4u) - (uvotes ? 4u * K - 4u : 0u)
                            : 0u;
   acc.emitted_bytes += emitted;
   // sim rounds gather 8 peer words per lane (each word of the round-start snapshot is gathered by
   // ~k lanes: 28 of the 32 B re-read), stale tiles 7 more from the previous snapshot (24 B re-read)
-  if constexpr (!REPLAY) acc.reread += active ? 4u * K - 4u + (in.stale == kVStale ? 24u : 0u) : 0u;
+  if constexpr (!REPLAY) acc.reread += active ? (uvotes ? 4u : 4u * K - 4u) + (in.stale == kVStale ? 24u : 0u) : 0u;
 }
 
 // Settled-tile fast path (kModeWarm, k = 8, klazy round, the wave's parked
@@ -1274,8 +1287,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           }
         }
         TileIn<K, false, true> in;
-        load_tile<K, false, true, POL, false, true, false, CC>(p, tile, lane, in, &wd);
-        process_tile<K, false, true, POL, true, REF, CC>(p, tile, lane, in, 0u, acc);
+        const bool uvotes = K == 8 && uniform && p.uni_votes && p.vv;  // (kernel-uniform)
+        load_tile<K, false, true, POL, false, true, false, CC>(p, tile, lane, in, &wd, uvotes);
+        process_tile<K, false, true, POL, true, REF, CC>(p, tile, lane, in, 0u, acc, uvotes);
       } else if constexpr (MODE == kModeFresh) {
         TileIn<K, false, false> in;
         load_tile<K, false, false, POL, false, true, true>(p, tile, lane, in);

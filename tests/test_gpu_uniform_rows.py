@@ -133,3 +133,36 @@ def test_uni_merge_on_off_identical(tpw, merge, m):
     np.testing.assert_array_equal(a[1], b[1])
     np.testing.assert_array_equal(a[2], b[2])
     assert a[3] == b[3] > 0
+
+
+@pytest.mark.parametrize("m,byz", [(1000, 0), (125, 0), (1000, BYZ20)], ids=["bl32", "bl4", "bl32_byz"])
+def test_uni_votes_on_off_identical_and_taken(m, byz):
+    """Option uni_votes (round_sweep.hip load_tile): with a uniform input snapshot the tiles that
+    are not settled candidates take the reference word as their 8 votes instead of gathering them.
+    Same digests, records, published rows and finalizations as with it off, through convergence,
+    the settled rounds and the finalization storm; with honest voters the converging rounds move
+    fewer bytes (the path was taken), with Byzantine voters no snapshot is uniform (nothing changes)."""
+    n = 20_000
+    out = []
+    for on in (1, 0):
+        eng = avhip.Engine(n, m, k=8, seed=11, byz_threshold=byz, log_capacity=1 << 26)
+        eng.set_option("uni_votes", on)
+        eng.init_records(avhip.INIT_BERNOULLI, P80)
+        digests, nbytes = [], 0
+        for r in range(22):
+            b0 = eng.alg_bytes()
+            eng.run_rounds(1)
+            nbytes += eng.alg_bytes() - b0
+            digests.append(eng.updates_digest())
+            eng.discard_updates()
+        out.append((digests, eng.read_records(), eng.read_pref(), nbytes, eng.finalized_count()))
+        eng.close()
+    on, off = out
+    assert on[0] == off[0]
+    np.testing.assert_array_equal(on[1], off[1])
+    np.testing.assert_array_equal(on[2], off[2])
+    assert on[4] == off[4] > 0
+    if byz:
+        assert on[3] == off[3]
+    else:
+        assert on[3] < off[3], (on[3], off[3])
