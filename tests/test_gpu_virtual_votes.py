@@ -94,14 +94,18 @@ def test_virtual_votes_bytes():
     """Per-lane bytes of a warm k=8 sim round: 172 B with stored vote planes;
     140 B in the first round that leaves them unstored (no V write); 136 B
     once the tile is stale (7 regathered words instead of the 8 V planes);
-    108 B once the tile was settled (the vote register is the A plane)."""
+    108 B once the tile was settled (the vote register is the A plane);
+    80 B when, in addition, the round's input snapshot is uniform (option
+    uni_votes: one reference word read instead of the 8 gathered votes)."""
     n, m = 4000, 1000
-    e = avhip.Engine(n, m, k=8, seed=1, log_capacity=1 << 22)
-    e.set_option("count_lazy", 0)  # count planes stored every round (test_gpu_count_lazy.py)
-    e.init_records(avhip.INIT_ACCEPTED, 0)
-    lanes = e.layout_info()["lanes"]
-    e.run_rounds(2)  # round 0 fresh (V left virtual); round 1 warm and stale
-    b = e.alg_bytes()
-    e.run_rounds(1)
-    assert e.alg_bytes() - b == lanes * 108 + 0  # round 1 settled: uniform; no updates, no flips
-    e.close()
+    for uv, per_lane in ((0, 108), (1, 80)):
+        e = avhip.Engine(n, m, k=8, seed=1, log_capacity=1 << 22)
+        e.set_option("count_lazy", 0)  # count planes stored every round (test_gpu_count_lazy.py)
+        e.set_option("uni_votes", uv)
+        e.init_records(avhip.INIT_ACCEPTED, 0)
+        lanes = e.layout_info()["lanes"]
+        e.run_rounds(2)  # round 0 fresh (V left virtual); round 1 warm and stale
+        b = e.alg_bytes()
+        e.run_rounds(1)
+        assert e.alg_bytes() - b == lanes * per_lane + 0  # round 1 settled: uniform; no updates, no flips
+        e.close()
