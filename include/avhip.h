@@ -379,14 +379,24 @@ int av_sample_peers(av_engine* e, int64_t round, int64_t n0, int64_t n1, int32_t
  * of the deferred state's write-back), "pref_uncached" (0; 1: snapshot
  * buffers in uncached memory; exact, measured slower), "peer_mask" (1:
  * need-masked peer pushes; set before the exchange), "push_defer" (1: a
- * wave's pushes queued in LDS and issued after its tiles), "peer_fine" (1).
+ * wave's pushes queued in LDS and issued after its tiles), "peer_fine" (1),
+ * "uni_votes" (1: in a round whose input snapshot is uniform, every tile takes
+ * the reference word as its votes instead of gathering them; exact),
+ * "wave_dense" (0; n: a wave with >= n lanes holding updates logs them all as
+ * dense records; exact, measured slower).
+ * StatusUpdate delivery: "enc_buckets" (2^26: (round, node) buckets per
+ * encoder pass; a log spanning more takes several passes), "copy_blocks" (0:
+ * the compact stream's copy to host memory by the runtime's copy; n: by an
+ * n-workgroup copy kernel; measured slower).
  * Diagnostics that make results invalid: "ablate_gather",
  * "ablate_emit" (StatusUpdates counted, not stored), "ablate_node"
  * (k_round_node: 1 = lanes past the cap skipped, 4 = no plane stores),
  * "unsynced_shard". Diagnostics that leave results valid: "count_changed"
  * (1: count changed published words in every sweep round, av_changed_words),
  * "solo_barrier" (1: a one-rank peer barrier after every round of an engine
- * without an exchange: the barrier's fixed cost alone). */
+ * without an exchange: the barrier's fixed cost alone), "warm_pref" (1: the
+ * snapshots a sweep round gathers from are read once, untimed, before its
+ * timed kernel: the cache state of a GPU of its own, tools/group_model.py). */
 int av_set_option(av_engine* e, const char* name, int64_t value);
 
 /* ---- measurement ---- */
