@@ -810,6 +810,8 @@ int launch_one_round(av_engine* e, const uint32_t* replay) {
     p.uni_rank = (uint32_t)std::max(0, e->peer_rank);
     p.uni_out = e->pref[nb] + e->uni_off;
     p.uni_in = e->uni_ok[e->cur] ? e->pref[e->cur] + e->uni_off : nullptr;
+    const int pv = av_engine::prv(e->cur);
+    p.uni_prev = e->uni_ok[pv] ? e->pref[pv] + e->uni_off : nullptr;
     p.uni_merge = e->uni_merge;
     p.uni_post = peer && sweep && !replay ? 1u : 0u;  // the slot reaches the peers in the barrier kernel
   }

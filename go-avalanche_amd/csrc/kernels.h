@@ -212,6 +212,7 @@ struct RoundParams {
   // can only read as a mismatch (tags are unique per round), never hide one.
   uint32_t* uni_out;
   const uint32_t* uni_in;
+  const uint32_t* uni_prev;  // pref_prev + uni_off (nullptr: its slots not maintained); round_sweep.hip kUniPrev
   uint32_t uni_world, uni_rank, uni_off;
   uint32_t uni_merge;  // a round with a uniform input: every uni_merge-th wave takes uni_merge runs (1: off)
   uint32_t uni_post;   // peer-push rounds: the rank's slot reaches the peers after the round (launch_peer_barrier)

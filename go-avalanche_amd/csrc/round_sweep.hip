@@ -280,14 +280,19 @@ __device__ __forceinline__ LaneIdx lane_idx(const RoundParams& p, uint32_t tile,
   return x;
 }
 
-// uvotes (uniform input, p.uni_votes; the warm k = 8 sweep only): every row of pref_in is the reference
-// row of pref_prev (kernels.h uni_in), so each of the 8 votes a lane would gather is that row's word
-// for its block: one load of it instead of 8 gathers (a klazy round whose tiles are not yet settled
-// candidates, e.g. C4's round 4 after the network converged in round 3)
+constexpr uint32_t kUniVotes = 1u, kUniPrev = 2u;
+// uflags (p.uni_votes; the warm k = 8 sweep only), kernel-uniform:
+//  * kUniVotes: the input snapshot is uniform (kernels.h uni_in): every row of pref_in is the
+//    reference row of pref_prev, so each of the 8 votes a lane would gather is that row's word for
+//    its block: one load of it instead of 8 gathers (a klazy round whose tiles are not yet settled
+//    candidates, e.g. C5's round 4 after the network converged);
+//  * kUniPrev: pref_prev is uniform too (kernels.h uni_prev): a stale tile's vote register (last
+//    round's 8 votes, gathered from pref_prev) is its reference row's word: no regather (the round
+//    after, e.g. C4's and C5's round 5).
 template <int K, bool REPLAY, bool WARM, int POL, bool ABLATE, bool VVM = false, bool FRESH = false, bool CC = true>
 __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
                                           TileIn<K, REPLAY, WARM>& in, const WaveDraw* wd = nullptr,
-                                          bool uvotes = false) {
+                                          uint32_t uflags = 0u) {
   const LaneIdx x = lane_idx(p, tile, lane);
   const uint32_t* const tp = p.planes + (size_t)tile * (kPlanes * 64u);
   const u32x4* const grp = reinterpret_cast<const u32x4*>(tp) + lane;
@@ -358,7 +363,11 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
       if (wd && wd->ok) {  // the wave's draws, made once for its run of tiles (implies off32)
         const uint32_t base = (x.nl - wd->nlA) * 2u;
         const bool nog = kAblatePhase && (p.ablate_phase & 1u);  // diagnostics: no gathers (votes from the row offsets)
-        if (in.stale == kVStale) {
+        if (in.stale == kVStale && (uflags & kUniPrev)) {  // every regathered word is the reference word
+          const uint32_t rp = at_byte(p.pref_prev, p.ref_node * rb + bo);
+          in.v0 = u32x4{rp, rp, rp, rp};
+          in.v1 = u32x4{rp, rp, rp, 0u};
+        } else if (in.stale == kVStale) {
           uint32_t pp[K];
           pick_parked(p, wd->sdp, wd->badp, base, x.node, p.round - 1u, rb, pp);
 #pragma unroll
@@ -391,7 +400,7 @@ __device__ __forceinline__ void load_tile(const RoundParams& p, uint32_t tile, u
         drawn = true;
       }
     }
-    if (uvotes) {  // wave-uniform: no draw of this round's peers, no gathers
+    if (uflags & kUniVotes) {  // kernel-uniform: no draw of this round's peers, no gathers
       const uint32_t rw = at_byte(p.pref_prev, p.ref_node * rb + bo);
 #pragma unroll
       for (int j = 0; j < K; ++j) in.w[j] = rw;
@@ -439,7 +448,7 @@ __device__ __forceinline__ void ref_flag_store(const RoundParams& p, uint32_t la
 template <int K, bool REPLAY, bool WARM, int POL, bool VVM = false, bool REF = false, bool CC = true>
 __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile, uint32_t lane,
                                              const TileIn<K, REPLAY, WARM>& in, uint32_t extra_bytes, SweepAcc& acc,
-                                             bool uvotes = false) {
+                                             uint32_t uflags = 0u) {
   const LaneIdx x = lane_idx(p, tile, lane);
   const bool active = x.active;
   const uint32_t b = x.b, node = x.node;
@@ -726,15 +735,19 @@ __device__ __forceinline__ void process_tile(const RoundParams& p, uint32_t tile
                           // virtual K4..K7 group (kHiVirt): not read (if K was read), not written
                           (WARM && (in.kw & kHiVirt) && !(kunread && kdefer) ? 16u : 0u) + (hv && !kdefer ? 16u : 0u);
   // V read: 32 B stored, 28 B regathered (stale), 0 B uniform
-  // uvotes: one 4-B reference word read instead of the K gathered votes
+  // uflags: one 4-B reference word read instead of the K gathered votes / the 7 regathered ones
   acc.lane_bytes += active ? lane_bytes + extra_bytes - (in.stale == kVStale ? 4u : in.stale == kVUniform ? 32u : 0u) -
                                  (virt ? 32u : 0u) - (cvirt ? 32u : 0u) + (p.count_changed ? 4u : 0u) -
-                                 kbytes - (astore ? 0u : 4u) - (uvotes ? 4u * K - 4u : 0u)
+                                 kbytes - (astore ? 0u : 4u) - ((uflags & kUniVotes) ? 4u * K - 4u : 0u) -
+                                 (in.stale == kVStale && (uflags & kUniPrev) ? 24u : 0u)
                            : 0u;
   acc.emitted_bytes += emitted;
   // sim rounds gather 8 peer words per lane (each word of the round-start snapshot is gathered by
   // ~k lanes: 28 of the 32 B re-read), stale tiles 7 more from the previous snapshot (24 B re-read)
-  if constexpr (!REPLAY) acc.reread += active ? (uvotes ? 4u : 4u * K - 4u) + (in.stale == kVStale ? 24u : 0u) : 0u;
+  if constexpr (!REPLAY)
+    acc.reread += active ? ((uflags & kUniVotes) ? 4u : 4u * K - 4u) +
+                               (in.stale == kVStale ? ((uflags & kUniPrev) ? 4u : 24u) : 0u)
+                         : 0u;
 }
 
 // Settled-tile fast path (kModeWarm, k = 8, klazy round, the wave's parked
@@ -1116,6 +1129,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
   bool uniform = p.uni_in != nullptr;
   if (uniform)
     for (uint32_t r = 0; r < p.uni_world; ++r) uniform = uniform && p.uni_in[r] != p.round;
+  // (and of pref_prev: its slots carry round - 1's tag if a row of it differed)
+  bool uniform_prev = uniform && p.uni_prev != nullptr && K == 8 && p.uni_votes && p.vv;
+  if (uniform_prev)
+    for (uint32_t r = 0; r < p.uni_world; ++r) uniform_prev = uniform_prev && p.uni_prev[r] != p.round - 1u;
+  const uint32_t uflags = (K == 8 && uniform && p.uni_votes && p.vv ? kUniVotes : 0u) | (uniform_prev ? kUniPrev : 0u);
   if constexpr (MODE == kModeWarmPipe) {
     // software-pipelined: tile t + nwaves's loads (state, peer draw, gathers)
     // are in flight while tile t is computed
@@ -1287,9 +1305,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == kMo
           }
         }
         TileIn<K, false, true> in;
-        const bool uvotes = K == 8 && uniform && p.uni_votes && p.vv;  // (kernel-uniform)
-        load_tile<K, false, true, POL, false, true, false, CC>(p, tile, lane, in, &wd, uvotes);
-        process_tile<K, false, true, POL, true, REF, CC>(p, tile, lane, in, 0u, acc, uvotes);
+        load_tile<K, false, true, POL, false, true, false, CC>(p, tile, lane, in, &wd, uflags);
+        process_tile<K, false, true, POL, true, REF, CC>(p, tile, lane, in, 0u, acc, uflags);
       } else if constexpr (MODE == kModeFresh) {
         TileIn<K, false, false> in;
         load_tile<K, false, false, POL, false, true, true>(p, tile, lane, in);

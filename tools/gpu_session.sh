@@ -225,7 +225,7 @@ for s in "$@"; do
     ab_wd) step ab_wd 900 bash -c 'for i in 1 2; do for w in c4p c4; do for o in "wave_dense=0" "wave_dense=32" "wave_dense=1"; do echo "== $w $o"; python tools/round_probe.py --workload $w --rounds 6 --option $o | tail -7; done; done; done' ;;
     wdtests) step wdtests 600 env AVHIP_TEST_OPTIONS=wave_dense=1 python -u -m pytest tests/test_gpu_compact.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     ab_uv) step ab_uv 900 bash -c 'for i in 1 2; do for w in c4 c5; do for o in "uni_votes=1" "uni_votes=0"; do echo "== $w $o"; python tools/round_probe.py --workload $w --rounds 10 --option $o | tail -11; done; done; done' ;;
-    uvtests) step uvtests 900 python -u -m pytest tests/test_gpu_uniform_rows.py tests/test_gpu_bench_protocol.py tests/test_gpu_fullsize.py -k "uniform or uni_ or protocol or c4_fullsize or c5_whole" -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
+    uvtests) step uvtests 900 python -u -m pytest tests/test_gpu_uniform_rows.py tests/test_gpu_bench_protocol.py tests/test_gpu_count_lazy.py tests/test_gpu_virtual_votes.py tests/test_gpu_fullsize.py -k "uniform or uni_ or protocol or lazy or virtual or c4_fullsize or c5_whole" -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     pmcall) for W in c4 c4p c4pb c3 c5; do WL=$W bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $?; done
             WL=c2 PMC_LAUNCHES=2 PMC_REPLAY=1 bash "$0" pmcb_sq pmcb_fetch pmcb_write pmcb_sum || exit $? ;;
     bench4) step bench 900 python bench.py --detail gpurun_out/bench_detail.json ;;
